@@ -1,0 +1,232 @@
+"""bench.py — BASELINE.json metric: "GiB/s device-resident Snappy encode+decode, 64 KiB chunks".
+
+One step = one pass of the hot path over one batch of device-resident chunks:
+    encode leg: masked CRC32C of every 64 KiB chunk (SnappyFrameEncoder.calculateAndWriteChecksum)
+                + Snappy.encode of every chunk            (configs[1])
+    decode leg: Snappy.decode of every chunk + CRC32C verify against the stored checksum (configs[2])
+value = Σ uncompressed bytes of all ranks / (max over ranks of the timed wall time) / 2^30,
+i.e. the round-trip rate Σ U / (t_enc + t_dec) of SURVEY.md §8d, inputs already resident in HBM.
+
+Multi-GPU (weak scaling): one process per GPU (torchrun), each rank owns a contiguous shard of
+chunk indices generated on its own device; no data-path collective.  RCCL is used for the timing
+barrier/max-reduction and for one all-gather of per-rank compressed byte totals (the offset
+exchange that lays the shards out as one stream), outside the timed region.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--chunks C] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident Snappy encode+decode, 64 KiB chunks, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+CHUNK = 65536
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--chunks", type=int, default=1 << 20, help="64 KiB chunks per GPU (configs[1]: 1M)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """The oracle (C restatement of Snappy.encode/decode + Crc32c, byte-at-a-time CRC like Crc32c.java)
+    timed on this host: encode+CRC then decode+CRC-verify of text-like 64 KiB chunks."""
+    import ctypes as C
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import pyoracle as O
+
+    L = O.lib()
+    nchunk = 64
+    chunks = [O.textgen_chunk(i, CHUNK) for i in range(nchunk)]
+    cap = L.orc_snappy_max_compressed_length(CHUNK)
+
+    def work(deadline):
+        out = (C.c_uint8 * cap)()
+        dec = (C.c_uint8 * CHUNK)()
+        olen, cons = C.c_size_t(0), C.c_size_t(0)
+        done = 0
+        i = 0
+        while time.perf_counter() < deadline:
+            c = chunks[i % nchunk]
+            crc = L.orc_snappy_checksum(c, CHUNK)
+            n = L.orc_snappy_encode(c, CHUNK, out)
+            st = L.orc_snappy_decode(C.cast(out, C.c_char_p), n, dec, CHUNK, C.byref(olen), C.byref(cons))
+            crc2 = L.orc_snappy_checksum(C.cast(dec, C.c_char_p), olen.value)
+            assert st == 0 and olen.value == CHUNK and crc == crc2
+            done += 1
+            i += 1
+        return done
+
+    # single thread
+    t0 = time.perf_counter()
+    d1 = work(t0 + seconds / 3)
+    t1 = time.perf_counter()
+    single = d1 * CHUNK / (t1 - t0) / 2**30
+    # all cores of this box's share (ctypes releases the GIL during the C calls)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        dl = t0 + seconds * 2 / 3
+        counts = list(ex.map(work, [dl] * threads))
+    t1 = time.perf_counter()
+    multi = sum(counts) * CHUNK / (t1 - t0) / 2**30
+    return {"value": round(multi, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/netty_oracle.c encode+CRC32C then decode+verify of text-like 64 KiB chunks, "
+                      f"{sum(counts)} chunks on {threads} threads in {t1 - t0:.1f}s (+ {d1} chunks single-thread)",
+            "single_thread_value": round(single, 4)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    from netty_amd import batch as B
+
+    n = args.chunks
+    # HBM budget: src + dec (n*64 KiB each) + encoded slots (n*cap) + encoder workspace (~8.6 GB)
+    cap = (B.snappy_max_compressed_length(CHUNK) + 15) // 16 * 16
+    free, total = torch.cuda.mem_get_info(dev)
+    need = n * (2 * CHUNK + cap) + (10 << 30)
+    if need > free:
+        n = int((free - (10 << 30)) // (2 * CHUNK + cap))
+    first = rank * n  # contiguous shard of chunk indices per rank
+
+    src = torch.empty(n * CHUNK, dtype=torch.uint8, device=dev)
+    B.textgen(src, first, n, CHUNK)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * CHUNK
+    ln = torch.full((n,), CHUNK, dtype=torch.int32, device=dev)
+    enc = torch.empty(n * cap, dtype=torch.uint8, device=dev)
+    eoff = torch.arange(n, dtype=torch.int64, device=dev) * cap
+    dec = torch.empty_like(src)
+    elen = torch.empty(n, dtype=torch.int32, device=dev)
+    est = torch.empty(n, dtype=torch.int32, device=dev)
+    crc = torch.empty(n, dtype=torch.int32, device=dev)
+    dlen = torch.empty(n, dtype=torch.int32, device=dev)
+    dst = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    ev = {k: [] for k in ("crc", "enc", "dec")}
+
+    def step(record):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        if record:
+            e[0].record()
+        B.crc32c_masked(src, off, ln, out=crc)
+        if record:
+            e[1].record()
+        B.snappy_encode(src, off, ln, enc, eoff, out_len=elen, status=est)
+        if record:
+            e[2].record()
+        B.snappy_decode(enc, eoff, elen, dec, off, expected_crc=crc, out_len=dlen, status=dst)
+        if record:
+            e[3].record()
+            ev["crc"].append((e[0], e[1]))
+            ev["enc"].append((e[1], e[2]))
+            ev["dec"].append((e[2], e[3]))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # verification (outside the timed region): statuses, lengths, identity
+    ok = (int((est != 0).sum()) == 0 and int((dst != 0).sum()) == 0 and bool(torch.equal(dlen, ln))
+          and bool(torch.equal(dec, src)))
+    comp_bytes = int(elen.to(torch.int64).sum().item())
+    totals = torch.tensor([comp_bytes], dtype=torch.int64, device=dev)
+    if world > 1:
+        gathered = [torch.zeros_like(totals) for _ in range(world)]
+        dist.all_gather(gathered, totals)  # offset exchange for a single global stream layout
+        totals_all = [int(x.item()) for x in gathered]
+        okt = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+    else:
+        totals_all = [comp_bytes]
+
+    def avg_ms(pairs):
+        return sum(a.elapsed_time(b) for a, b in pairs) / max(1, len(pairs))
+
+    t_crc, t_enc, t_dec = avg_ms(ev["crc"]), avg_ms(ev["enc"]), avg_ms(ev["dec"])
+    U = n * CHUNK
+    C_ = comp_bytes
+
+    def roof(algo_bytes, ms):
+        a = algo_bytes / (ms / 1e3) / 1e9
+        return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None}
+
+    r_dec = roof(C_ + U, t_dec)       # decode: C_in + U_out per chunk
+    r_enc = roof(U + C_, t_enc)       # encode: U_in + C_out per chunk
+    r_dec["kernel"], r_enc["kernel"] = "nx::dec::k_snappy_decode<4096>", "nx::k_snappy_encode_naive"
+    dominant = r_enc if t_enc >= t_dec else r_dec
+
+    value = world * U / elapsed * args.steps / 2**30
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic text-like 64 KiB chunks (include/netty_amd_textgen.h: 4096-word Zipf(1.1) vocabulary), "
+                "generated on device",
+        "config": {"workload": "configs[1]+configs[2]: Snappy encode (+frame CRC32C) then decode + CRC32C verify of "
+                               "text-like 64 KiB chunks, device-resident",
+                   "chunk_bytes": CHUNK, "chunks_per_gpu": n, "global_chunks": n * world,
+                   "parallelism": f"dp{world} (independent chunk shards, no data-path collective)"},
+        "roofline": dominant,
+        "roofline_decode": r_dec, "roofline_encode": r_enc,
+        "encode_gib_s": round(U / ((t_crc + t_enc) / 1e3) / 2**30, 3),
+        "decode_gib_s": round(U / (t_dec / 1e3) / 2**30, 3),
+        "kernel_ms": {"crc32c": round(t_crc, 3), "encode": round(t_enc, 3), "decode_crc": round(t_dec, 3)},
+        "compression_ratio": round(C_ / U, 4), "compressed_bytes_per_rank": totals_all,
+        "verified": ok,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

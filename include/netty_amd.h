@@ -1,0 +1,194 @@
+/*
+ * netty_amd.h — C-ABI of the MI355X-native codec-compression hot path (libnetty_amd.so).
+ *
+ * Plain pointers and sizes only (no torch / HIP types in the signatures; `stream` is a
+ * hipStream_t passed as void*, NULL = default stream).  Two layers:
+ *
+ *  (1) Device batch kernels — thousands of independent chunks per launch, all buffers
+ *      device-resident.  Each replaces the per-ByteBuf Java call named in its comment.
+ *      Chunk i reads in[in_off[i] .. in_off[i]+in_len[i]) and writes out[out_off[i] ..].
+ *      Every entry point is asynchronous on `stream`, returns NX_OK or NX_ERR_INVALID_ARG /
+ *      NX_ERR_HIP for launch problems, and reports per-chunk results in device arrays
+ *      (status[i] >= 0 ok, < 0 = include/netty_amd_status.h).
+ *
+ *  (2) Host handler layer — the framing state machines of SnappyFrameEncoder/Decoder,
+ *      FastLzFrameEncoder/Decoder and LzfEncoder/Decoder over host memory (a direct
+ *      ByteBuf's memoryAddress(), ByteBuf.java:2395-2403), batching every chunk of a call
+ *      into one GPU launch (H2D → kernel → D2H).  This is what the JNI glue in
+ *      INTEGRATION.md binds, one native handle per Netty handler instance.
+ *
+ * Reference paths below are relative to
+ * /root/reference/codec-compression/src/main/java/io/netty/handler/codec/compression/.
+ */
+#ifndef NETTY_AMD_H
+#define NETTY_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+#include "netty_amd_status.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ library */
+const char* nx_version(void);
+const char* nx_status_string(int32_t status);
+/* Number of visible GPUs (0 when none); never initialises more than hipGetDeviceCount. */
+int32_t nx_device_count(void);
+/* Upper bound of Snappy.encode output for `n` input bytes (buffer sizing, cf. Snappy.java:82). */
+size_t nx_snappy_max_compressed_length(size_t n);
+/* FastLz.calculateOutputBufferLength (FastLz.java:84-87) + FastLZ tail slack. */
+size_t nx_fastlz_max_compressed_length(size_t n);
+size_t nx_lzf_max_compressed_length(size_t n);
+
+/* ------------------------------------------------------------------ (1) device batch kernels */
+
+/* Replaces Snappy.encode(ByteBuf in, ByteBuf out, int length)  Snappy.java:82-165
+ * (in.readerIndex()==0, as SnappyFrameEncoder's readSlice gives).  in_len[i] <= 65536.
+ * out capacity per chunk >= nx_snappy_max_compressed_length(in_len[i]).
+ * out_len[i] = bytes written (preamble + tags), status[i] = NX_OK. */
+int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                               uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
+                               int32_t* status, uint32_t n, void* stream);
+
+/* Replaces Snappy.decode(ByteBuf in, ByteBuf out)  Snappy.java:315-393 as driven by
+ * SnappyFrameDecoder.decode for one COMPRESSED_DATA chunk (SnappyFrameDecoder.java:194-224),
+ * fused with Snappy.validateChecksum over the output (Snappy.java:700-707).
+ *   out_cap[i]   — output ByteBuf max capacity (65536 in the frame decoder, :203); NULL = 65536;
+ *                  must be <= 2^24 (Snappy blocks; the out buffer needs out_cap[i] bytes).
+ *   out_len[i]   — bytes produced (partial output on a silently truncated chunk, as Java).
+ *   consumed[i]  — input bytes consumed by the decoder state machine (nullable).
+ *   expected_masked_crc — NULL: no verification; else status NX_ERR_SNAPPY_CRC_MISMATCH on mismatch.
+ *   crc_out[i]   — masked CRC32C of the produced output (nullable). */
+int32_t nx_snappy_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                               uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                               uint32_t* out_len, uint32_t* consumed, int32_t* status,
+                               const uint32_t* expected_masked_crc, uint32_t* crc_out,
+                               uint32_t n, void* stream);
+
+/* Same contract as nx_snappy_decode_batch, reference-structured variant: one lane runs the serial
+ * state machine per chunk (cross-check / baseline for the wave-cooperative kernel). */
+int32_t nx_snappy_decode_batch_naive(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                     uint32_t* out_len, uint32_t* consumed, int32_t* status,
+                                     const uint32_t* expected_masked_crc, uint32_t* crc_out,
+                                     uint32_t n, void* stream);
+
+/* Replaces Snappy.calculateChecksum(ByteBuf, off, len)  Snappy.java:668-676
+ * (Crc32c.java:105-124 + maskChecksum :720-722).  masked_out[i] = mask(crc32c(chunk i)). */
+int32_t nx_crc32c_masked_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len,
+                               uint32_t* masked_out, uint32_t n, void* stream);
+
+/* Replaces FastLz.compress(input, inOffset, inLength, output, outOffset, level)
+ * FastLz.java:96-399.  level[i] in {0,1,2} (0 = AUTO); u16_limit[i] = readableBytes() - inOffset
+ * of the Java call (the readU16 quirk, FastLz.java:552-557; NULL = in_len[i]); when
+ * u16_limit[i] > in_len[i] the bytes following the chunk in `in` must be readable.
+ * out_len[i] = compress return value. */
+int32_t nx_fastlz_compress_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                 uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
+                                 const int32_t* level, const int32_t* u16_limit, int32_t* status,
+                                 uint32_t n, void* stream);
+
+/* Replaces FastLz.decompress(input, inOffset, inLength, output, outOffset, outLength)
+ * FastLz.java:409-543.  out_len_limit[i] = originalLength; in_avail[i] = readable bytes from
+ * the chunk start (NULL = in_len[i]).  result[i] = Java return value (0 on overflow/underflow)
+ * or NX_ERR_FASTLZ_BAD_LEVEL / NX_ERR_FASTLZ_INPUT_OOB. */
+int32_t nx_fastlz_decompress_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                   const uint32_t* in_avail, uint8_t* out, const uint64_t* out_off,
+                                   const uint32_t* out_len_limit, int32_t* result,
+                                   uint32_t n, void* stream);
+
+/* java.util.zip.Adler32 over each chunk (FastLzFrameEncoder.java:142-146 / Decoder :171-180). */
+int32_t nx_adler32_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len,
+                         uint32_t* out, uint32_t n, void* stream);
+
+/* Replaces LZFEncoder.appendEncoded(...) for one chunk (LzfEncoder.java:218-221): writes a complete
+ * "ZV" block (compressed if it saves bytes, else non-compressed).  in_len[i] <= 65535.
+ * PARITY UNPINNED vs com.ning:compress-lzf (third-party, not in the reference). */
+int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                            uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
+                            int32_t* status, uint32_t n, void* stream);
+
+/* Replaces ChunkDecoder.decodeChunk(in, inPos, out, outPos, outEnd)  LzfDecoder.java:205:
+ * decodes one compressed LZF body into exactly out_len[i] bytes. status NX_OK / NX_ERR_LZF_CORRUPT. */
+int32_t nx_lzf_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                            uint8_t* out, const uint64_t* out_off, const uint32_t* out_len,
+                            int32_t* status, uint32_t n, void* stream);
+
+/* Bench/test data: the text-like generator of include/netty_amd_textgen.h on the device.
+ * Chunk k (global index first_chunk + k) is written to out + k*chunk_len. */
+int32_t nx_textgen_device(uint8_t* out, uint64_t first_chunk, uint32_t n_chunks, uint32_t chunk_len,
+                          void* stream);
+
+/* Device-memory helpers for callers without their own allocator (ctypes tests, JNI). */
+void* nx_device_alloc(size_t bytes);
+int32_t nx_device_free(void* p);
+int32_t nx_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int32_t nx_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int32_t nx_stream_sync(void* stream);
+
+/* ------------------------------------------------------------------ (2) host handler layer */
+/* Output list of one decode()/encode() call: messages are views into an arena owned by the
+ * handle (valid until the next call on the same handle). */
+typedef struct {
+    const uint8_t* data;
+    size_t len;
+} nx_msg;
+
+/* SnappyFrameEncoder / snappyEncoderWithJumboFrames()  SnappyFrameEncoder.java:60-117 */
+typedef struct nx_snappy_frame_encoder nx_snappy_frame_encoder;
+nx_snappy_frame_encoder* nx_snappy_frame_encoder_new(int32_t jumbo);
+void nx_snappy_frame_encoder_free(nx_snappy_frame_encoder* e);
+size_t nx_snappy_frame_max_encoded_length(size_t n);
+/* encode(ctx, in, out): appends the framed bytes for `in` to out (capacity out_cap).
+ * Returns bytes written (>= 0) or a negative status. */
+int64_t nx_snappy_frame_encoder_encode(nx_snappy_frame_encoder* e, const uint8_t* in, size_t n,
+                                       uint8_t* out, size_t out_cap);
+
+/* SnappyFrameDecoder(boolean validateChecksums)  SnappyFrameDecoder.java:67-231.
+ * decode(): runs ByteToMessageDecoder.callDecode over the cumulation in[0..n)
+ * (ByteToMessageDecoder.java:464-517): *consumed = bytes read; msgs/n_msgs = decoded messages.
+ * Returns NX_OK or a negative status (the decoder is then corrupted, :227-230); *err_msg gets the
+ * reference's exception message. */
+typedef struct nx_snappy_frame_decoder nx_snappy_frame_decoder;
+nx_snappy_frame_decoder* nx_snappy_frame_decoder_new(int32_t validate_checksums);
+void nx_snappy_frame_decoder_free(nx_snappy_frame_decoder* d);
+int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, const uint8_t* in, size_t n,
+                                       size_t* consumed, const nx_msg** msgs, size_t* n_msgs,
+                                       const char** err_msg);
+
+/* FastLzFrameEncoder(level, checksum)  FastLzFrameEncoder.java:100-172.
+ * reader_index = in.readerIndex() of the Java message (enters the readU16 quirk). */
+typedef struct nx_fastlz_frame_encoder nx_fastlz_frame_encoder;
+nx_fastlz_frame_encoder* nx_fastlz_frame_encoder_new(int32_t level, int32_t checksum);
+void nx_fastlz_frame_encoder_free(nx_fastlz_frame_encoder* e);
+size_t nx_fastlz_frame_max_encoded_length(size_t n);
+int64_t nx_fastlz_frame_encoder_encode(nx_fastlz_frame_encoder* e, const uint8_t* buf, size_t reader_index,
+                                       size_t n, uint8_t* out, size_t out_cap);
+
+/* FastLzFrameDecoder(checksum)  FastLzFrameDecoder.java:113-207 */
+typedef struct nx_fastlz_frame_decoder nx_fastlz_frame_decoder;
+nx_fastlz_frame_decoder* nx_fastlz_frame_decoder_new(int32_t validate_checksums);
+void nx_fastlz_frame_decoder_free(nx_fastlz_frame_decoder* d);
+int32_t nx_fastlz_frame_decoder_decode(nx_fastlz_frame_decoder* d, const uint8_t* in, size_t n,
+                                       size_t* consumed, const nx_msg** msgs, size_t* n_msgs,
+                                       const char** err_msg);
+
+/* LzfEncoder(totalLength, compressThreshold)  LzfEncoder.java:127-216 */
+typedef struct nx_lzf_encoder nx_lzf_encoder;
+nx_lzf_encoder* nx_lzf_encoder_new(int32_t compress_threshold);
+void nx_lzf_encoder_free(nx_lzf_encoder* e);
+size_t nx_lzf_frame_max_encoded_length(size_t n);
+int64_t nx_lzf_encoder_encode(nx_lzf_encoder* e, const uint8_t* in, size_t n, uint8_t* out, size_t out_cap);
+
+/* LzfDecoder  LzfDecoder.java:112-241 */
+typedef struct nx_lzf_decoder nx_lzf_decoder;
+nx_lzf_decoder* nx_lzf_decoder_new(void);
+void nx_lzf_decoder_free(nx_lzf_decoder* d);
+int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
+                              const nx_msg** msgs, size_t* n_msgs, const char** err_msg);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,54 @@
+/*
+ * netty_amd_status.h — per-chunk status codes shared by the C-ABI (include/netty_amd.h)
+ * and the CPU oracle (oracle/netty_oracle.c).
+ *
+ * Netty's codecs signal failure with Java exceptions; Netty's own JNI layer returns
+ * negative errno-style ints that the Java side turns into exceptions
+ * (transport-native-unix-common/src/main/c/netty_unix_filedescriptor.c:115-117 →
+ * FileDescriptor.java:105-110).  This build follows that convention: every batch entry
+ * point writes one int32 status per chunk, >= 0 on success, < 0 = one of the codes below.
+ * Each code maps 1:1 to a reference throw site (file:line relative to
+ * codec-compression/src/main/java/io/netty/handler/codec/compression/).
+ */
+#ifndef NETTY_AMD_STATUS_H
+#define NETTY_AMD_STATUS_H
+
+#define NX_OK 0
+
+/* Snappy.java:414-416  "Preamble is greater than 4 bytes" */
+#define NX_ERR_SNAPPY_PREAMBLE_TOO_LONG   (-1)
+/* Snappy.java:638-640  "Offset is less than minimum permissible value" */
+#define NX_ERR_SNAPPY_OFFSET_ZERO         (-2)
+/* Snappy.java:642-645  "Offset is greater than maximum value supported by this implementation" */
+#define NX_ERR_SNAPPY_OFFSET_NEGATIVE     (-3)
+/* Snappy.java:647-649  "Offset exceeds size of chunk" */
+#define NX_ERR_SNAPPY_OFFSET_BEYOND       (-4)
+/* SnappyFrameDecoder.java:203 buffer(…, 65536) max capacity → IndexOutOfBoundsException */
+#define NX_ERR_SNAPPY_OUTPUT_OVERFLOW     (-5)
+/* Snappy.java:480-492: code-63 literal length negative as Java int → IllegalArgumentException */
+#define NX_ERR_SNAPPY_LITERAL_LEN_INVALID (-6)
+/* Snappy.java:700-706  "mismatching checksum: %x (expected: %x)" */
+#define NX_ERR_SNAPPY_CRC_MISMATCH        (-7)
+
+/* FastLz.java:412-416  "invalid level: %d (expected: %d or %d)" */
+#define NX_ERR_FASTLZ_BAD_LEVEL           (-20)
+/* FastLz.java:444-465: match bytes read past the readable input → IndexOutOfBoundsException */
+#define NX_ERR_FASTLZ_INPUT_OOB           (-21)
+/* FastLzFrameDecoder.java:160-164  originalLength/actual length mismatch */
+#define NX_ERR_FASTLZ_LENGTH_MISMATCH     (-22)
+/* FastLzFrameDecoder.java:171-179  "stream corrupted: mismatching checksum" */
+#define NX_ERR_FASTLZ_CRC_MISMATCH        (-23)
+
+/* LzfDecoder.java:205 → ChunkDecoder.decodeChunk throws on corrupt data (3rd-party) */
+#define NX_ERR_LZF_CORRUPT                (-30)
+
+/* Frame-level format errors raised by the host framing state machines (SnappyFrameDecoder.java:
+ * 116-118,128-133,138-140,152-157,159-165,181-201; FastLzFrameDecoder.java:121-124;
+ * LzfDecoder.java:120-122,134-137).  The handle's err_msg carries the reference message. */
+#define NX_ERR_FRAME_CORRUPT              (-40)
+
+#define NX_ERR_INVALID_ARG                (-100)
+#define NX_ERR_HIP                        (-101)
+#define NX_ERR_NO_DEVICE                  (-102)
+
+#endif

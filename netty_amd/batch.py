@@ -1,0 +1,138 @@
+"""Device-resident batch API (thin wrappers over the C-ABI batch kernels).
+
+All tensors are torch tensors on the same HIP device; torch is used only as the device
+allocator / stream provider.  Chunk i is ``data[off[i] : off[i] + length[i]]``.  Calls are
+asynchronous on torch's current stream.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _chk(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {rc} ({_lib.status_string(rc)})")
+
+
+def snappy_max_compressed_length(n: int) -> int:
+    return _lib.load().nx_snappy_max_compressed_length(n)
+
+
+def snappy_encode(inp, in_off, in_len, out, out_off, out_len=None, status=None):
+    """Snappy.encode per chunk (Snappy.java:82-165).  Returns (out_len, status) int tensors."""
+    n = in_len.numel()
+    dev = inp.device
+    out_len = torch.empty(n, dtype=torch.int32, device=dev) if out_len is None else out_len
+    status = torch.empty(n, dtype=torch.int32, device=dev) if status is None else status
+    _chk(_lib.load().nx_snappy_encode_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_len),
+                                            _ptr(status), n, _stream()), "nx_snappy_encode_batch")
+    return out_len, status
+
+
+def snappy_decode(inp, in_off, in_len, out, out_off, out_cap=None, expected_crc=None, want_crc=False, consumed=False,
+                  naive=False, out_len=None, status=None):
+    """Snappy.decode per chunk (+ fused masked-CRC32C verify).  Returns dict of tensors."""
+    n = in_len.numel()
+    dev = inp.device
+    out_len = torch.empty(n, dtype=torch.int32, device=dev) if out_len is None else out_len
+    status = torch.empty(n, dtype=torch.int32, device=dev) if status is None else status
+    cons = torch.empty(n, dtype=torch.int32, device=dev) if consumed else None
+    crc = torch.empty(n, dtype=torch.int32, device=dev) if want_crc else None
+    fn = _lib.load().nx_snappy_decode_batch_naive if naive else _lib.load().nx_snappy_decode_batch
+    _chk(fn(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(cons),
+            _ptr(status), _ptr(expected_crc), _ptr(crc), n, _stream()), "nx_snappy_decode_batch")
+    return {"out_len": out_len, "status": status, "consumed": cons, "crc": crc}
+
+
+def crc32c_masked(inp, off, length, out=None):
+    """Snappy.calculateChecksum per chunk (Snappy.java:668-676)."""
+    n = length.numel()
+    out = torch.empty(n, dtype=torch.int32, device=inp.device) if out is None else out
+    _chk(_lib.load().nx_crc32c_masked_batch(_ptr(inp), _ptr(off), _ptr(length), _ptr(out), n, _stream()),
+         "nx_crc32c_masked_batch")
+    return out
+
+
+def fastlz_compress(inp, in_off, in_len, out, out_off, level=None, u16_limit=None):
+    n = in_len.numel()
+    dev = inp.device
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    _chk(_lib.load().nx_fastlz_compress_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_len),
+                                              _ptr(level), _ptr(u16_limit), _ptr(status), n, _stream()),
+         "nx_fastlz_compress_batch")
+    return out_len, status
+
+
+def fastlz_decompress(inp, in_off, in_len, out, out_off, out_len_limit, in_avail=None):
+    n = in_len.numel()
+    res = torch.empty(n, dtype=torch.int32, device=inp.device)
+    _chk(_lib.load().nx_fastlz_decompress_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(in_avail), _ptr(out),
+                                                _ptr(out_off), _ptr(out_len_limit), _ptr(res), n, _stream()),
+         "nx_fastlz_decompress_batch")
+    return res
+
+
+def adler32(inp, off, length):
+    n = length.numel()
+    out = torch.empty(n, dtype=torch.int32, device=inp.device)
+    _chk(_lib.load().nx_adler32_batch(_ptr(inp), _ptr(off), _ptr(length), _ptr(out), n, _stream()), "nx_adler32_batch")
+    return out
+
+
+def lzf_encode(inp, in_off, in_len, out, out_off):
+    n = in_len.numel()
+    dev = inp.device
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    _chk(_lib.load().nx_lzf_encode_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_len),
+                                         _ptr(status), n, _stream()), "nx_lzf_encode_batch")
+    return out_len, status
+
+
+def lzf_decode(inp, in_off, in_len, out, out_off, out_len):
+    n = in_len.numel()
+    status = torch.empty(n, dtype=torch.int32, device=inp.device)
+    _chk(_lib.load().nx_lzf_decode_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_len),
+                                         _ptr(status), n, _stream()), "nx_lzf_decode_batch")
+    return status
+
+
+def textgen(out, first_chunk: int, n_chunks: int, chunk_len: int):
+    """Fill out[k*chunk_len:(k+1)*chunk_len] with text-like chunk first_chunk+k."""
+    _chk(_lib.load().nx_textgen_device(_ptr(out), first_chunk, n_chunks, chunk_len, _stream()), "nx_textgen_device")
+    return out
+
+
+def pack(chunks: list[bytes], device, align: int = 16, pad: int = 0):
+    """Pack host chunks into one device tensor; returns (data, off[int64], len[int32])."""
+    offs, cur = [], 0
+    for c in chunks:
+        offs.append(cur)
+        cur += (len(c) + align - 1) // align * align
+    buf = bytearray(cur + pad + 16)
+    for o, c in zip(offs, chunks):
+        buf[o:o + len(c)] = c
+    data = torch.frombuffer(bytes(buf), dtype=torch.uint8).to(device)
+    off = torch.tensor(offs, dtype=torch.int64, device=device)
+    ln = torch.tensor([len(c) for c in chunks], dtype=torch.int32, device=device)
+    return data, off, ln
+
+
+def out_slots(lengths: list[int], device, align: int = 16):
+    offs, cur = [], 0
+    for n in lengths:
+        offs.append(cur)
+        cur += (n + align - 1) // align * align
+    data = torch.zeros(cur + 16, dtype=torch.uint8, device=device)
+    return data, torch.tensor(offs, dtype=torch.int64, device=device)

@@ -1,0 +1,58 @@
+// capi_misc.cpp — library-level C-ABI entry points (version, status strings, sizing, device helpers).
+#include <hip/hip_runtime.h>
+#include "../../include/netty_amd.h"
+
+extern "C" const char* nx_version(void) { return "netty_amd 0.1.0 (gfx950)"; }
+
+extern "C" const char* nx_status_string(int32_t s) {
+    switch (s) {
+        case NX_OK: return "ok";
+        case NX_ERR_SNAPPY_PREAMBLE_TOO_LONG: return "Preamble is greater than 4 bytes";
+        case NX_ERR_SNAPPY_OFFSET_ZERO: return "Offset is less than minimum permissible value";
+        case NX_ERR_SNAPPY_OFFSET_NEGATIVE: return "Offset is greater than maximum value supported by this implementation";
+        case NX_ERR_SNAPPY_OFFSET_BEYOND: return "Offset exceeds size of chunk";
+        case NX_ERR_SNAPPY_OUTPUT_OVERFLOW: return "decoded data exceeds the output buffer's maximum capacity";
+        case NX_ERR_SNAPPY_LITERAL_LEN_INVALID: return "literal length is negative";
+        case NX_ERR_SNAPPY_CRC_MISMATCH: return "mismatching checksum";
+        case NX_ERR_FASTLZ_BAD_LEVEL: return "invalid level";
+        case NX_ERR_FASTLZ_INPUT_OOB: return "compressed data references bytes past the readable input";
+        case NX_ERR_FASTLZ_LENGTH_MISMATCH: return "stream corrupted: originalLength and actual length mismatch";
+        case NX_ERR_FASTLZ_CRC_MISMATCH: return "stream corrupted: mismatching checksum";
+        case NX_ERR_LZF_CORRUPT: return "Corrupt LZF data";
+        case NX_ERR_FRAME_CORRUPT: return "corrupted frame";
+        case NX_ERR_INVALID_ARG: return "invalid argument";
+        case NX_ERR_HIP: return "HIP runtime error";
+        case NX_ERR_NO_DEVICE: return "no GPU device";
+        default: return "unknown status";
+    }
+}
+
+extern "C" int32_t nx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" size_t nx_snappy_max_compressed_length(size_t n) { return 32 + n + n / 6; }
+extern "C" size_t nx_fastlz_max_compressed_length(size_t n) {
+    size_t a = (size_t)((double)n * 1.06);  // FastLz.calculateOutputBufferLength (FastLz.java:84-87)
+    if (a < 66) a = 66;
+    return a + 16;
+}
+extern "C" size_t nx_lzf_max_compressed_length(size_t n) { return n + n / 32 + 16; }
+
+extern "C" void* nx_device_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) return nullptr;
+    return p;
+}
+extern "C" int32_t nx_device_free(void* p) { return hipFree(p) == hipSuccess ? NX_OK : NX_ERR_HIP; }
+extern "C" int32_t nx_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream) == hipSuccess ? NX_OK : NX_ERR_HIP;
+}
+extern "C" int32_t nx_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream) == hipSuccess ? NX_OK : NX_ERR_HIP;
+}
+extern "C" int32_t nx_stream_sync(void* stream) {
+    return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? NX_OK : NX_ERR_HIP;
+}

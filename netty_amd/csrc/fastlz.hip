@@ -1,0 +1,441 @@
+// fastlz.hip — FastLZ level 1/2 compress + decompress (FastLz.java:96-557) and Adler32, batched.
+//
+// FastLZ is a serial byte-oriented LZ77 whose match search depends on an evolving 8192-entry
+// hash table (FastLz.java:112,139-142), so each chunk runs as one lane's serial state machine;
+// a batch of thousands of 4–64 KiB chunks fills the chip.  The hash table lives in a per-lane
+// device workspace with the same (stamp << 16 | position) trick as the Snappy encoder.  Java's
+// `htab` is initialised to 0 (= position 0) on every call; a stamp mismatch reads as 0.
+//
+// The readU16 quirk (FastLz.java:552-557: an ABSOLUTE index compared against readableBytes())
+// is reproduced through the per-chunk u16_limit = readableBytes() - inOffset of the Java call.
+#include "nx_common.hpp"
+
+namespace nx {
+namespace flz {
+
+constexpr int32_t MAX_DISTANCE = 8191;
+constexpr int32_t MAX_FARDISTANCE = 65535 + MAX_DISTANCE - 1;
+constexpr int32_t HASH_LOG = 13;
+constexpr int32_t HASH_SIZE = 1 << HASH_LOG;
+constexpr int32_t HASH_MASK = HASH_SIZE - 1;
+constexpr int32_t MAX_COPY = 32;
+constexpr int32_t MAX_LEN = 256 + 8;
+
+__device__ __forceinline__ int32_t read_u16(const uint8_t* in, int32_t o, int32_t lim) {
+    if (o + 1 >= lim) return in[o];
+    return ((int32_t)in[o + 1] << 8) | in[o];
+}
+
+__device__ __forceinline__ int32_t hashf(const uint8_t* in, int32_t o, int32_t lim) {
+    int32_t v = read_u16(in, o, lim);
+    v ^= read_u16(in, o + 1, lim) ^ (v >> (16 - HASH_LOG));
+    return v & HASH_MASK;
+}
+
+__device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, uint8_t* __restrict__ out, int32_t proposedLevel,
+                            int32_t lim, uint32_t* __restrict__ htab, uint32_t stamp) {
+    const int32_t level = proposedLevel == 0 ? (inLength < 65536 ? 1 : 2) : proposedLevel;
+    int32_t ip = 0;
+    int32_t ipBound = ip + inLength - 2;
+    const int32_t ipLimit = ip + inLength - 12;
+    int32_t op = 0;
+    int32_t copy;
+    const uint32_t stag = stamp << 16;
+#define HGET(h) ((htab[(h)] & 0xFFFF0000u) == stag ? (int32_t)(htab[(h)] & 0xFFFFu) : 0)
+#define HSET(h, v) (htab[(h)] = stag | (uint32_t)(v))
+    if (inLength < 4) {
+        if (inLength != 0) {
+            out[op++] = (uint8_t)(inLength - 1);
+            ipBound++;
+            while (ip <= ipBound) out[op++] = in[ip++];
+            return inLength + 1;
+        }
+        return 0;
+    }
+    copy = 2;
+    out[op++] = MAX_COPY - 1;
+    out[op++] = in[ip++];
+    out[op++] = in[ip++];
+    while (ip < ipLimit) {
+        int32_t ref = 0;
+        int64_t distance = 0;
+        int32_t len = 3;
+        int32_t anchor = ip;
+        bool matchLabel = false;
+        if (level == 2) {
+            if (in[ip] == in[ip - 1] && read_u16(in, ip - 1, lim) == read_u16(in, ip + 1, lim)) {
+                distance = 1;
+                ip += 3;
+                ref = anchor + (3 - 1);
+                matchLabel = true;
+            }
+        }
+        if (!matchLabel) {
+            const int32_t hval = hashf(in, ip, lim);
+            ref = HGET(hval);
+            distance = anchor - ref;
+            HSET(hval, anchor);
+            bool lit = false;
+            if (distance == 0 || (level == 1 ? distance >= MAX_DISTANCE : distance >= MAX_FARDISTANCE)) {
+                lit = true;
+            } else if (in[ref++] != in[ip++]) {
+                lit = true;
+            } else if (in[ref++] != in[ip++]) {
+                lit = true;
+            } else if (in[ref++] != in[ip++]) {
+                lit = true;
+            }
+            if (!lit && level == 2 && distance >= MAX_DISTANCE) {
+                if (in[ip++] != in[ref++]) {
+                    lit = true;
+                } else if (in[ip++] != in[ref++]) {
+                    lit = true;
+                } else {
+                    len += 2;
+                }
+            }
+            if (lit) {
+                out[op++] = in[anchor++];
+                ip = anchor;
+                copy++;
+                if (copy == MAX_COPY) {
+                    copy = 0;
+                    out[op++] = MAX_COPY - 1;
+                }
+                continue;
+            }
+        }
+        ip = anchor + len;
+        distance--;
+        if (distance == 0) {
+            const uint8_t x = in[ip - 1];
+            while (ip < ipBound) {
+                if (in[ref++] != x) break;
+                ip++;
+            }
+        } else {
+            bool missMatch = false;
+            for (int i = 0; i < 8; i++) {
+                if (in[ref++] != in[ip++]) {
+                    missMatch = true;
+                    break;
+                }
+            }
+            if (!missMatch) {
+                while (ip < ipBound) {
+                    if (in[ref++] != in[ip++]) break;
+                }
+            }
+        }
+        if (copy != 0) {
+            out[op - copy - 1] = (uint8_t)(copy - 1);
+        } else {
+            op--;
+        }
+        copy = 0;
+        ip -= 3;
+        len = ip - anchor;
+        if (level == 2) {
+            if (distance < MAX_DISTANCE) {
+                if (len < 7) {
+                    out[op++] = (uint8_t)((len << 5) + (int32_t)(distance >> 8));
+                    out[op++] = (uint8_t)(distance & 255);
+                } else {
+                    out[op++] = (uint8_t)((7 << 5) + (int32_t)(distance >> 8));
+                    for (len -= 7; len >= 255; len -= 255) out[op++] = 255;
+                    out[op++] = (uint8_t)len;
+                    out[op++] = (uint8_t)(distance & 255);
+                }
+            } else {
+                distance -= MAX_DISTANCE;
+                if (len < 7) {
+                    out[op++] = (uint8_t)((len << 5) + 31);
+                    out[op++] = 255;
+                    out[op++] = (uint8_t)(distance >> 8);
+                    out[op++] = (uint8_t)(distance & 255);
+                } else {
+                    out[op++] = (uint8_t)((7 << 5) + 31);
+                    for (len -= 7; len >= 255; len -= 255) out[op++] = 255;
+                    out[op++] = (uint8_t)len;
+                    out[op++] = 255;
+                    out[op++] = (uint8_t)(distance >> 8);
+                    out[op++] = (uint8_t)(distance & 255);
+                }
+            }
+        } else {
+            if (len > MAX_LEN - 2) {
+                while (len > MAX_LEN - 2) {
+                    out[op++] = (uint8_t)((7 << 5) + (int32_t)(distance >> 8));
+                    out[op++] = (uint8_t)(MAX_LEN - 2 - 7 - 2);
+                    out[op++] = (uint8_t)(distance & 255);
+                    len -= MAX_LEN - 2;
+                }
+            }
+            if (len < 7) {
+                out[op++] = (uint8_t)((len << 5) + (int32_t)(distance >> 8));
+                out[op++] = (uint8_t)(distance & 255);
+            } else {
+                out[op++] = (uint8_t)((7 << 5) + (int32_t)(distance >> 8));
+                out[op++] = (uint8_t)(len - 7);
+                out[op++] = (uint8_t)(distance & 255);
+            }
+        }
+        int32_t hv = hashf(in, ip, lim);
+        HSET(hv, ip);
+        ip++;
+        hv = hashf(in, ip, lim);
+        HSET(hv, ip);
+        ip++;
+        out[op++] = MAX_COPY - 1;
+    }
+    ipBound++;
+    while (ip <= ipBound) {
+        out[op++] = in[ip++];
+        copy++;
+        if (copy == MAX_COPY) {
+            copy = 0;
+            out[op++] = MAX_COPY - 1;
+        }
+    }
+    if (copy != 0) {
+        out[op - copy - 1] = (uint8_t)(copy - 1);
+    } else {
+        op--;
+    }
+    if (level == 2) out[0] |= 1 << 5;
+#undef HGET
+#undef HSET
+    return op;
+}
+
+__device__ int32_t decompress(const uint8_t* __restrict__ in, int32_t inLength, int32_t in_avail, uint8_t* __restrict__ out,
+                              int32_t outLength) {
+    bool oob = false;
+#define FIN(i) ((i) < in_avail ? (int32_t)in[(i)] : (oob = true, 0))
+    if (in_avail < 1) return NX_ERR_FASTLZ_INPUT_OOB;
+    const int32_t level = ((int32_t)(int8_t)in[0] >> 5) + 1;
+    if (level != 1 && level != 2) return NX_ERR_FASTLZ_BAD_LEVEL;
+    int32_t ip = 0, op = 0;
+    int64_t ctrl = in[ip++] & 31;
+    int loop = 1;
+    do {
+        int64_t ref = op;
+        int64_t len = ctrl >> 5;
+        int64_t ofs = (ctrl & 31) << 8;
+        if (ctrl >= 32) {
+            len--;
+            ref -= ofs;
+            int32_t code;
+            if (len == 6) {
+                if (level == 1) {
+                    len += FIN(ip);
+                    ip++;
+                } else {
+                    do {
+                        code = FIN(ip);
+                        ip++;
+                        if (oob) return NX_ERR_FASTLZ_INPUT_OOB;
+                        len += code;
+                    } while (code == 255);
+                }
+            }
+            if (level == 1) {
+                ref -= FIN(ip);
+                ip++;
+            } else {
+                code = FIN(ip);
+                ip++;
+                ref -= code;
+                if (code == 255 && ofs == (31 << 8)) {
+                    ofs = (int64_t)FIN(ip) << 8;
+                    ip++;
+                    ofs += FIN(ip);
+                    ip++;
+                    ref = (int32_t)(op - ofs - MAX_DISTANCE);
+                }
+            }
+            if (oob) return NX_ERR_FASTLZ_INPUT_OOB;
+            if (op + len + 3 > outLength) return 0;
+            if (ref - 1 < 0) return 0;
+            if (ip < inLength) {
+                ctrl = FIN(ip);
+                ip++;
+                if (oob) return NX_ERR_FASTLZ_INPUT_OOB;
+            } else {
+                loop = 0;
+            }
+            if (ref == op) {
+                const uint8_t b = out[ref - 1];
+                out[op++] = b;
+                out[op++] = b;
+                out[op++] = b;
+                while (len != 0) {
+                    out[op++] = b;
+                    --len;
+                }
+            } else {
+                ref--;
+                out[op++] = out[ref++];
+                out[op++] = out[ref++];
+                out[op++] = out[ref++];
+                while (len != 0) {
+                    out[op++] = out[ref++];
+                    --len;
+                }
+            }
+        } else {
+            ctrl++;
+            if (op + ctrl > outLength) return 0;
+            if (ip + ctrl > inLength) return 0;
+            out[op++] = in[ip++];
+            for (--ctrl; ctrl != 0; ctrl--) out[op++] = in[ip++];
+            loop = ip < inLength ? 1 : 0;
+            if (loop) ctrl = in[ip++];
+        }
+    } while (loop != 0);
+#undef FIN
+    return op;
+}
+
+__global__ void __launch_bounds__(256) k_compress(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                  const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                  const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
+                                                  const int32_t* __restrict__ level, const int32_t* __restrict__ lim,
+                                                  int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ ws,
+                                                  uint32_t stamp_base) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    uint32_t* htab = ws + (size_t)tid * HASH_SIZE;
+    uint32_t iter = 0;
+    for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
+        const uint32_t len = in_len[c];
+        const int32_t lv = level ? level[c] : 0;
+        if (len > 65535u || (lv != 0 && lv != 1 && lv != 2)) {
+            status[c] = NX_ERR_INVALID_ARG;
+            out_len[c] = 0;
+            continue;
+        }
+        const int32_t l16 = lim ? lim[c] : (int32_t)len;
+        const uint32_t stamp = ((stamp_base + iter) % 65535u) + 1u;
+        out_len[c] = (uint32_t)compress(in + in_off[c], (int32_t)len, out + out_off[c], lv, l16, htab, stamp);
+        status[c] = NX_OK;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_decompress(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                    const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ in_avail,
+                                                    uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                                    const uint32_t* __restrict__ out_lim, int32_t* __restrict__ result, uint32_t n) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    for (uint32_t c = tid; c < n; c += nthreads) {
+        const uint32_t il = in_len[c];
+        const uint32_t av = in_avail ? in_avail[c] : il;
+        result[c] = decompress(in + in_off[c], (int32_t)il, (int32_t)av, out + out_off[c], (int32_t)out_lim[c]);
+    }
+}
+
+// Adler32 (java.util.zip.Adler32): one wave per chunk, lanes take 16-byte slots of 1 KiB blocks.
+// a = 1 + Σ b_i, b = n + Σ (n - i) b_i (mod 65521), computed with 64-bit partial sums.
+__global__ void __launch_bounds__(256) k_adler32(const uint8_t* __restrict__ in, const uint64_t* __restrict__ off,
+                                                 const uint32_t* __restrict__ len, uint32_t* __restrict__ out, uint32_t n) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wpb = blockDim.x / 64;
+    for (uint32_t c = blockIdx.x * wpb + (threadIdx.x >> 6); c < n; c += gridDim.x * wpb) {
+        const uint8_t* p = in + off[c];
+        const uint32_t L = len[c];
+        uint64_t sa = 0, sb = 0;  // Σ b_i, Σ (L - i) b_i
+        for (uint32_t base = 0; base < L; base += 1024) {
+            const uint32_t i0 = base + 16u * lane;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t i = i0 + k;
+                if (i < L) {
+                    const uint32_t b = p[i];
+                    sa += b;
+                    sb += (uint64_t)(L - i) * b;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            sa += __shfl_xor(sa, 1 << j);
+            sb += __shfl_xor(sb, 1 << j);
+        }
+        if (lane == 0) {
+            const uint32_t a = (uint32_t)((1u + sa) % 65521u);
+            const uint32_t b = (uint32_t)(((uint64_t)L + sb) % 65521u);
+            out[c] = (b << 16) | a;
+        }
+    }
+}
+
+}  // namespace flz
+}  // namespace nx
+
+#include <mutex>
+namespace {
+std::mutex g_mu;
+uint32_t* g_ws = nullptr;
+size_t g_ws_threads = 0;
+uint32_t g_stamp = 0;
+int g_dev = -1;
+}  // namespace
+
+extern "C" int32_t nx_fastlz_compress_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                            const uint64_t* out_off, uint32_t* out_len, const int32_t* level,
+                                            const int32_t* u16_limit, int32_t* status, uint32_t n, void* stream) {
+    if (n == 0) return NX_OK;
+    if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
+    int dev = 0, cus = 256;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const size_t want = (size_t)cus * 8 * 64;
+    const size_t threads = n < want ? ((n + 255) / 256) * 256 : want;
+    std::lock_guard<std::mutex> lk(g_mu);
+    const size_t per = (size_t)nx::flz::HASH_SIZE * sizeof(uint32_t);
+    if (!g_ws || g_ws_threads < threads || g_dev != dev) {
+        if (g_ws) (void)hipFree(g_ws);
+        g_ws = nullptr;
+        const size_t cap = threads > want ? threads : want;
+        NX_HIP_CHECK(hipMalloc(&g_ws, cap * per));
+        NX_HIP_CHECK(hipMemsetAsync(g_ws, 0, cap * per, (hipStream_t)stream));
+        g_ws_threads = cap;
+        g_dev = dev;
+        g_stamp = 0;
+    }
+    const uint32_t iters = (uint32_t)((n + threads - 1) / threads);
+    if ((uint64_t)g_stamp + iters >= 65535u) {
+        NX_HIP_CHECK(hipMemsetAsync(g_ws, 0, g_ws_threads * per, (hipStream_t)stream));
+        g_stamp = 0;
+    }
+    hipLaunchKernelGGL(nx::flz::k_compress, dim3((unsigned)(threads / 256)), dim3(256), 0, (hipStream_t)stream, in, in_off, in_len,
+                       out, out_off, out_len, level, u16_limit, status, n, g_ws, g_stamp);
+    NX_HIP_CHECK(hipGetLastError());
+    g_stamp += iters;
+    return NX_OK;
+}
+
+extern "C" int32_t nx_fastlz_decompress_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                              const uint32_t* in_avail, uint8_t* out, const uint64_t* out_off,
+                                              const uint32_t* out_len_limit, int32_t* result, uint32_t n, void* stream) {
+    if (n == 0) return NX_OK;
+    if (!in || !in_off || !in_len || !out || !out_off || !out_len_limit || !result) return NX_ERR_INVALID_ARG;
+    unsigned grid = (n + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL(nx::flz::k_decompress, dim3(grid), dim3(256), 0, (hipStream_t)stream, in, in_off, in_len, in_avail, out,
+                       out_off, out_len_limit, result, n);
+    NX_HIP_CHECK(hipGetLastError());
+    return NX_OK;
+}
+
+extern "C" int32_t nx_adler32_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t* out, uint32_t n,
+                                    void* stream) {
+    if (n == 0) return NX_OK;
+    if (!in || !off || !len || !out) return NX_ERR_INVALID_ARG;
+    unsigned grid = n / 4 + 1;
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(nx::flz::k_adler32, dim3(grid), dim3(256), 0, (hipStream_t)stream, in, off, len, out, n);
+    NX_HIP_CHECK(hipGetLastError());
+    return NX_OK;
+}

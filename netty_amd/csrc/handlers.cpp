@@ -1,0 +1,1016 @@
+// handlers.cpp — host handler layer: Netty's framing state machines over host memory, with every
+// chunk of one encode()/decode() call batched into a single GPU launch.
+//
+//   SnappyFrameEncoder   SnappyFrameEncoder.java:79-152
+//   SnappyFrameDecoder   SnappyFrameDecoder.java:85-258 (+ ByteToMessageDecoder.callDecode :464-517)
+//   FastLzFrameEncoder   FastLzFrameEncoder.java:111-172
+//   FastLzFrameDecoder   FastLzFrameDecoder.java:113-207
+//   LzfEncoder           LzfEncoder.java:169-246
+//   LzfDecoder           LzfDecoder.java:112-241
+//
+// Headers are parsed on the host exactly as the Java decode() does (they are a few bytes per
+// chunk); the per-chunk arithmetic (Snappy/FastLZ/LZF, CRC32C, Adler32) runs on the GPU.  Results
+// are applied in stream order, so the first failing chunk truncates the message list and marks the
+// decoder corrupted just like the reference's exception path.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+#include <vector>
+#include "../../include/netty_amd.h"
+#include "nx_common.hpp"
+
+extern "C" int32_t nx_snappy_decode_batch(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*, const uint64_t*,
+                                          const uint32_t*, uint32_t*, uint32_t*, int32_t*, const uint32_t*, uint32_t*, uint32_t,
+                                          void*);
+
+namespace {
+
+// ------------------------------------------------------------------ device context
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool ensure(size_t n) {
+        if (n <= cap) return true;
+        size_t c = cap ? cap : 4096;
+        while (c < n) c += c / 2 + 4096;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, c) != hipSuccess) return false;
+        cap = c;
+        return true;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct Gpu {
+    hipStream_t s = nullptr;
+    bool ok = false;
+    DevBuf din, dout, a0, a1, a2, a3, a4, a5, a6;
+    Gpu() {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
+        ok = nx::crc_tables_init() == NX_OK;
+    }
+    ~Gpu() {
+        if (s) (void)hipStreamDestroy(s);
+    }
+    bool h2d(void* d, const void* h, size_t n) { return n == 0 || hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s) == hipSuccess; }
+    bool d2h(void* h, const void* d, size_t n) { return n == 0 || hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s) == hipSuccess; }
+    bool sync() { return hipStreamSynchronize(s) == hipSuccess; }
+};
+
+inline uint32_t le24(const uint8_t* p) { return p[0] | (p[1] << 8) | ((uint32_t)p[2] << 16); }
+inline uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
+inline uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+inline uint32_t be24(const uint8_t* p) { return ((uint32_t)p[0] << 16) | ((uint32_t)p[1] << 8) | p[2]; }
+inline uint32_t be32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
+
+struct MsgList {
+    std::vector<nx_msg> msgs;
+    std::vector<std::vector<uint8_t>> owned;  // decoded payloads (stable storage)
+    std::string err;
+    void clear() {
+        msgs.clear();
+        owned.clear();
+        err.clear();
+    }
+};
+
+const uint8_t kStreamStart[10] = {0xff, 0x06, 0x00, 0x00, 0x73, 0x4e, 0x61, 0x50, 0x70, 0x59};
+
+}  // namespace
+
+// ======================================================================= Snappy frame encoder
+struct nx_snappy_frame_encoder {
+    Gpu g;
+    bool started = false;
+    int32_t slice;
+};
+
+extern "C" nx_snappy_frame_encoder* nx_snappy_frame_encoder_new(int32_t jumbo) {
+    auto* e = new nx_snappy_frame_encoder();
+    if (!e->g.ok) {
+        delete e;
+        return nullptr;
+    }
+    e->slice = jumbo ? 65535 : 32767;  // SnappyFrameEncoder.java:31,39
+    return e;
+}
+extern "C" void nx_snappy_frame_encoder_free(nx_snappy_frame_encoder* e) { delete e; }
+extern "C" size_t nx_snappy_frame_max_encoded_length(size_t n) { return 10 + (n / 32767 + 2) * 8 + 32 + n + n / 6; }
+
+extern "C" int64_t nx_snappy_frame_encoder_encode(nx_snappy_frame_encoder* e, const uint8_t* in, size_t n, uint8_t* out,
+                                                  size_t out_cap) {
+    if (!e) return NX_ERR_INVALID_ARG;
+    if (n == 0) return 0;  // !in.isReadable()
+    if (out_cap < nx_snappy_frame_max_encoded_length(n)) return NX_ERR_INVALID_ARG;
+    size_t op = 0;
+    if (!e->started) {
+        e->started = true;
+        memcpy(out, kStreamStart, 10);
+        op = 10;
+    }
+    struct Sl {
+        uint64_t off;
+        uint32_t len;
+        bool comp;
+    };
+    std::vector<Sl> sl;
+    int64_t dl = (int64_t)n;
+    if (dl > 18) {  // MIN_COMPRESSIBLE_LENGTH (:46,90-113)
+        uint64_t pos = 0;
+        for (;;) {
+            if (dl < 18) {
+                sl.push_back({pos, (uint32_t)dl, false});
+                break;
+            }
+            uint32_t len = dl > e->slice ? (uint32_t)e->slice : (uint32_t)dl;
+            sl.push_back({pos, len, true});
+            pos += len;
+            if (dl > e->slice) dl -= e->slice; else break;
+        }
+    } else {
+        sl.push_back({0, (uint32_t)n, false});
+    }
+    const uint32_t ns = (uint32_t)sl.size();
+    std::vector<uint64_t> ioff(ns), ooff(ns);
+    std::vector<uint32_t> ilen(ns);
+    uint64_t ocur = 0;
+    for (uint32_t i = 0; i < ns; ++i) {
+        ioff[i] = sl[i].off;
+        ilen[i] = sl[i].len;
+        ooff[i] = ocur;
+        ocur += nx_snappy_max_compressed_length(sl[i].len);
+        ocur = (ocur + 15) & ~15ull;
+    }
+    Gpu& g = e->g;
+    if (!g.din.ensure(n) || !g.dout.ensure(ocur) || !g.a0.ensure(8ull * ns) || !g.a1.ensure(8ull * ns) ||
+        !g.a2.ensure(4ull * ns) || !g.a3.ensure(4ull * ns) || !g.a4.ensure(4ull * ns) || !g.a5.ensure(4ull * ns))
+        return NX_ERR_HIP;
+    bool ok = g.h2d(g.din.p, in, n) && g.h2d(g.a0.p, ioff.data(), 8ull * ns) && g.h2d(g.a1.p, ooff.data(), 8ull * ns) &&
+              g.h2d(g.a2.p, ilen.data(), 4ull * ns);
+    if (!ok) return NX_ERR_HIP;
+    // masked CRC32C of every slice (calculateAndWriteChecksum :150-152, writeUnencodedChunk :119-124)
+    int32_t r = nx_crc32c_masked_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.a5.as<uint32_t>(), ns, g.s);
+    if (r != NX_OK) return r;
+    // Snappy.encode of every slice (uncompressed slices are encoded too but ignored: keeps one launch)
+    r = nx_snappy_encode_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.dout.as<uint8_t>(),
+                               g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), g.a4.as<int32_t>(), ns, g.s);
+    if (r != NX_OK) return r;
+    std::vector<uint32_t> clen(ns), crc(ns);
+    std::vector<uint8_t> hout(ocur);
+    ok = g.d2h(clen.data(), g.a3.p, 4ull * ns) && g.d2h(crc.data(), g.a5.p, 4ull * ns) && g.d2h(hout.data(), g.dout.p, ocur) && g.sync();
+    if (!ok) return NX_ERR_HIP;
+    for (uint32_t i = 0; i < ns; ++i) {
+        if (sl[i].comp) {
+            const uint32_t chunkLength = clen[i] + 4;  // setChunkLength (:126-132)
+            if (chunkLength >> 24) return NX_ERR_INVALID_ARG;
+            out[op++] = 0;
+            out[op++] = (uint8_t)chunkLength;
+            out[op++] = (uint8_t)(chunkLength >> 8);
+            out[op++] = (uint8_t)(chunkLength >> 16);
+            memcpy(out + op, &crc[i], 4);
+            op += 4;
+            memcpy(out + op, hout.data() + ooff[i], clen[i]);
+            op += clen[i];
+        } else {
+            const uint32_t cl = sl[i].len + 4;
+            out[op++] = 1;
+            out[op++] = (uint8_t)cl;
+            out[op++] = (uint8_t)(cl >> 8);
+            out[op++] = (uint8_t)(cl >> 16);
+            memcpy(out + op, &crc[i], 4);
+            op += 4;
+            memcpy(out + op, in + sl[i].off, sl[i].len);
+            op += sl[i].len;
+        }
+    }
+    return (int64_t)op;
+}
+
+// ======================================================================= Snappy frame decoder
+struct nx_snappy_frame_decoder {
+    Gpu g;
+    bool validate;
+    bool started = false;
+    bool corrupted = false;
+    uint64_t skip = 0;  // numBytesToSkip
+    MsgList ml;
+};
+
+extern "C" nx_snappy_frame_decoder* nx_snappy_frame_decoder_new(int32_t validate) {
+    auto* d = new nx_snappy_frame_decoder();
+    if (!d->g.ok) {
+        delete d;
+        return nullptr;
+    }
+    d->validate = validate != 0;
+    return d;
+}
+extern "C" void nx_snappy_frame_decoder_free(nx_snappy_frame_decoder* d) { delete d; }
+
+namespace {
+enum class SAct { Stream, Skip, Uncomp, Comp, Error };
+struct SnappyAction {
+    SAct kind;
+    size_t data = 0;     // payload position (after the 4-byte masked checksum)
+    uint32_t dlen = 0;   // payload bytes
+    uint32_t crc = 0;    // stored masked checksum
+    size_t end = 0;      // reader index after this action
+    uint64_t skip = 0;   // numBytesToSkip after this action
+    int job = -1;        // GPU job index
+    std::string err;     // Error action: the reference exception message
+};
+
+// One SnappyFrameDecoder.decode() call over in[p..n) (SnappyFrameDecoder.java:85-231), with the
+// chunk work deferred.  Returns false when decode() would return without consuming (need more).
+bool snappy_parse_one(const uint8_t* in, size_t n, size_t& p, bool& started, uint64_t& skip, std::vector<SnappyAction>& acts) {
+    if (skip) {  // :91-99
+        uint64_t s = skip < (uint64_t)(n - p) ? skip : (uint64_t)(n - p);
+        p += s;
+        skip -= s;
+        SnappyAction a{SAct::Skip};
+        a.end = p;
+        a.skip = skip;
+        acts.push_back(a);
+        return s > 0;
+    }
+    const size_t inSize = n - p;
+    if (inSize < 4) return false;
+    const uint8_t type = in[p];
+    const uint32_t chunkLength = le24(in + p + 1);
+    SnappyAction a{SAct::Error};
+    a.end = p;
+    a.skip = skip;
+    char buf[160];
+    auto fail = [&](const char* msg) {
+        a.kind = SAct::Error;
+        a.err = msg;
+        acts.push_back(a);
+        return false;
+    };
+    if (type == 0xff) {  // STREAM_IDENTIFIER (:115-136)
+        if (chunkLength != 6) {
+            snprintf(buf, sizeof buf, "Unexpected length of stream identifier: %u", chunkLength);
+            return fail(buf);
+        }
+        if (inSize < 10) return false;
+        a.end = p + 10;
+        if (memcmp(in + p + 4, "sNaPpY", 6) != 0) return fail("Unexpected stream identifier contents. Mismatched snappy protocol version?");
+        started = true;
+        p += 10;
+        a.kind = SAct::Stream;
+        acts.push_back(a);
+        return true;
+    }
+    if (type == 0) {  // COMPRESSED_DATA (:180-224)
+        if (!started) return fail("Received COMPRESSED_DATA tag before STREAM_IDENTIFIER");
+        if (inSize < 4 + (size_t)chunkLength) return false;
+        if (chunkLength < 4) return fail("Received COMPRESSED_DATA shorter than its checksum");
+        a.crc = le32(in + p + 4);
+        // snappy.getPreamble(in): the varint is read from the cumulation (Snappy.java:404-441)
+        uint32_t ulen = 0;
+        int bi = 0;
+        bool complete = false;
+        for (size_t q = p + 8; q < n; ++q) {
+            const uint32_t cur = in[q];
+            ulen |= (cur & 0x7f) << (bi++ * 7);
+            if ((cur & 0x80) == 0) {
+                complete = true;
+                break;
+            }
+            if (bi >= 4) return fail("Preamble is greater than 4 bytes");
+        }
+        if (!complete) ulen = 0;
+        if (ulen > 65536) return fail("Received COMPRESSED_DATA that contains uncompressed data that exceeds 65536 bytes");
+        a.kind = SAct::Comp;
+        a.data = p + 8;
+        a.dlen = chunkLength - 4;
+        p += 4 + chunkLength;
+        a.end = p;
+        acts.push_back(a);
+        return true;
+    }
+    if (type == 1) {  // UNCOMPRESSED_DATA (:158-179)
+        if (!started) return fail("Received UNCOMPRESSED_DATA tag before STREAM_IDENTIFIER");
+        if (chunkLength > 65536 + 4) return fail("Received UNCOMPRESSED_DATA larger than 65540 bytes");
+        if (inSize < 4 + (size_t)chunkLength) return false;
+        if (chunkLength < 4) return fail("Received UNCOMPRESSED_DATA shorter than its checksum");
+        a.kind = SAct::Uncomp;
+        a.crc = le32(in + p + 4);
+        a.data = p + 8;
+        a.dlen = chunkLength - 4;
+        p += 4 + chunkLength;
+        a.end = p;
+        acts.push_back(a);
+        return true;
+    }
+    if (type & 0x80) {  // RESERVED_SKIPPABLE (:137-150)
+        if (!started) return fail("Received RESERVED_SKIPPABLE tag before STREAM_IDENTIFIER");
+        p += 4;
+        const uint64_t s = chunkLength < (uint64_t)(n - p) ? chunkLength : (uint64_t)(n - p);
+        p += s;
+        if (s != chunkLength) skip = chunkLength - s;
+        a.kind = SAct::Skip;
+        a.end = p;
+        a.skip = skip;
+        acts.push_back(a);
+        return true;
+    }
+    snprintf(buf, sizeof buf, "Found reserved unskippable chunk type: 0x%x", (unsigned)type);  // :151-157
+    return fail(buf);
+}
+}  // namespace
+
+extern "C" int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
+                                                  const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {
+    if (!d || (!in && n)) return NX_ERR_INVALID_ARG;
+    MsgList& ml = d->ml;
+    ml.clear();
+    size_t rd = 0;
+    auto finish = [&](int32_t r) {
+        *consumed = rd;
+        *msgs = ml.msgs.data();
+        *n_msgs = ml.msgs.size();
+        if (err_msg) *err_msg = ml.err.empty() ? nullptr : ml.err.c_str();
+        return r;
+    };
+    auto corrupt = [&](size_t at, int32_t code, const std::string& msg) {
+        ml.err = msg;
+        d->corrupted = true;  // :227-230
+        rd = at;
+        return finish(code);
+    };
+    if (d->corrupted) {  // :86-89
+        rd = n;
+        return finish(NX_OK);
+    }
+    for (;;) {  // loops again only for the validating-mode leftover case below
+        std::vector<SnappyAction> acts;
+        size_t p = rd;
+        bool started = d->started;
+        uint64_t skip = d->skip;
+        while (p < n && snappy_parse_one(in, n, p, started, skip, acts)) {
+        }
+        // ---- one GPU batch: decode every compressed chunk; CRC every uncompressed one if validating
+        std::vector<int> comp_idx, unc_idx;
+        size_t lo = (size_t)-1, hi = 0;
+        for (size_t i = 0; i < acts.size(); ++i) {
+            SnappyAction& a = acts[i];
+            if (a.kind == SAct::Comp) {
+                a.job = (int)comp_idx.size();
+                comp_idx.push_back((int)i);
+            } else if (a.kind == SAct::Uncomp && d->validate) {
+                a.job = (int)unc_idx.size();
+                unc_idx.push_back((int)i);
+            } else {
+                continue;
+            }
+            lo = a.data < lo ? a.data : lo;
+            hi = a.data + a.dlen > hi ? a.data + a.dlen : hi;
+        }
+        const uint32_t ncomp = (uint32_t)comp_idx.size(), nunc = (uint32_t)unc_idx.size(), nj = ncomp + nunc;
+        std::vector<uint32_t> olen(ncomp), cons(ncomp), ucrc(nunc);
+        std::vector<int32_t> st(ncomp);
+        std::vector<uint8_t> hout((size_t)ncomp * 65536);
+        Gpu& g = d->g;
+        if (nj) {
+            const size_t span = hi - lo;
+            std::vector<uint64_t> ioff(nj), ooff(ncomp);
+            std::vector<uint32_t> ilen(nj), expect(ncomp);
+            for (uint32_t j = 0; j < ncomp; ++j) {
+                const SnappyAction& a = acts[comp_idx[j]];
+                ioff[j] = a.data - lo;
+                ilen[j] = a.dlen;
+                ooff[j] = (uint64_t)j * 65536;
+                expect[j] = a.crc;
+            }
+            for (uint32_t j = 0; j < nunc; ++j) {
+                const SnappyAction& a = acts[unc_idx[j]];
+                ioff[ncomp + j] = a.data - lo;
+                ilen[ncomp + j] = a.dlen;
+            }
+            if (!g.din.ensure(span + 1) || !g.dout.ensure((size_t)ncomp * 65536 + 16) || !g.a0.ensure(8ull * nj) ||
+                !g.a1.ensure(8ull * ncomp + 8) || !g.a2.ensure(4ull * nj) || !g.a3.ensure(4ull * ncomp + 4) ||
+                !g.a4.ensure(4ull * ncomp + 4) || !g.a5.ensure(4ull * ncomp + 4) || !g.a6.ensure(4ull * nj + 4))
+                return finish(NX_ERR_HIP);
+            bool ok = g.h2d(g.din.p, in + lo, span) && g.h2d(g.a0.p, ioff.data(), 8ull * nj) && g.h2d(g.a2.p, ilen.data(), 4ull * nj) &&
+                      g.h2d(g.a1.p, ooff.data(), 8ull * ncomp) && g.h2d(g.a5.p, expect.data(), 4ull * ncomp);
+            if (!ok) return finish(NX_ERR_HIP);
+            int32_t* d_st = g.a6.as<int32_t>();
+            uint32_t* d_ucrc = g.a6.as<uint32_t>() + ncomp;
+            if (ncomp) {
+                int32_t r = nx_snappy_decode_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.dout.as<uint8_t>(),
+                                                   g.a1.as<uint64_t>(), nullptr, g.a3.as<uint32_t>(), g.a4.as<uint32_t>(), d_st,
+                                                   d->validate ? g.a5.as<uint32_t>() : nullptr, nullptr, ncomp, g.s);
+                if (r != NX_OK) return finish(r);
+            }
+            if (nunc) {
+                int32_t r = nx_crc32c_masked_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>() + ncomp, g.a2.as<uint32_t>() + ncomp, d_ucrc,
+                                                   nunc, g.s);
+                if (r != NX_OK) return finish(r);
+            }
+            ok = g.d2h(olen.data(), g.a3.p, 4ull * ncomp) && g.d2h(cons.data(), g.a4.p, 4ull * ncomp) &&
+                 g.d2h(st.data(), d_st, 4ull * ncomp) && g.d2h(ucrc.data(), d_ucrc, 4ull * nunc) &&
+                 g.d2h(hout.data(), g.dout.p, (size_t)ncomp * 65536) && g.sync();
+            if (!ok) return finish(NX_ERR_HIP);
+        }
+        // ---- apply in stream order (the first failing chunk ends the call, as the Java exception does)
+        bool reparse = false;
+        char buf[128];
+        for (const SnappyAction& a : acts) {
+            if (a.kind == SAct::Error) return corrupt(a.end, NX_ERR_FRAME_CORRUPT, a.err);
+            if (a.kind == SAct::Stream) {
+                d->started = true;
+            } else if (a.kind == SAct::Uncomp) {
+                if (d->validate && ucrc[a.job] != a.crc) {  // :171-175
+                    snprintf(buf, sizeof buf, "mismatching checksum: %x (expected: %x)", ucrc[a.job], a.crc);
+                    return corrupt(a.end, NX_ERR_SNAPPY_CRC_MISMATCH, buf);
+                }
+                ml.msgs.push_back({in + a.data, a.dlen});  // readRetainedSlice: a view of the cumulation
+            } else if (a.kind == SAct::Comp) {
+                const int j = a.job;
+                const uint8_t* outj = hout.data() + (size_t)j * 65536;
+                if (st[j] == NX_ERR_SNAPPY_CRC_MISMATCH) {
+                    snprintf(buf, sizeof buf, "mismatching checksum: %x (expected: %x)", nx::host_mask(nx::host_crc32c(outj, olen[j])), a.crc);
+                    return corrupt(a.end, st[j], buf);
+                }
+                if (st[j] != NX_OK) return corrupt(a.end, st[j], nx_status_string(st[j]));
+                ml.owned.emplace_back(outj, outj + olen[j]);
+                ml.msgs.push_back({ml.owned.back().data(), olen[j]});
+                if (d->validate && cons[j] < a.dlen) {
+                    // validating mode restores the writer index and leaves the unread chunk bytes in
+                    // the cumulation (:206-212); they are parsed again as the next chunk header.
+                    rd = a.data + cons[j];
+                    d->skip = 0;
+                    reparse = true;
+                    break;
+                }
+            }
+            rd = a.end;
+            d->skip = a.skip;
+        }
+        if (!reparse) break;
+    }
+    return finish(NX_OK);
+}
+
+// ======================================================================= FastLZ frame encoder
+struct nx_fastlz_frame_encoder {
+    Gpu g;
+    int32_t level;
+    bool checksum;
+};
+
+extern "C" nx_fastlz_frame_encoder* nx_fastlz_frame_encoder_new(int32_t level, int32_t checksum) {
+    if (level != 0 && level != 1 && level != 2) return nullptr;  // FastLzFrameEncoder.java:101-105
+    auto* e = new nx_fastlz_frame_encoder();
+    if (!e->g.ok) {
+        delete e;
+        return nullptr;
+    }
+    e->level = level;
+    e->checksum = checksum != 0;
+    return e;
+}
+extern "C" void nx_fastlz_frame_encoder_free(nx_fastlz_frame_encoder* e) { delete e; }
+extern "C" size_t nx_fastlz_frame_max_encoded_length(size_t n) { return (n / 65535 + 1) * (12 + 82) + n + n / 16; }
+
+extern "C" int64_t nx_fastlz_frame_encoder_encode(nx_fastlz_frame_encoder* e, const uint8_t* buf, size_t r0, size_t n,
+                                                  uint8_t* out, size_t out_cap) {
+    if (!e) return NX_ERR_INVALID_ARG;
+    if (n == 0) return 0;
+    if (out_cap < nx_fastlz_frame_max_encoded_length(n)) return NX_ERR_INVALID_ARG;
+    const uint8_t* in = buf + r0;
+    const size_t w = r0 + n;
+    const uint32_t nc = (uint32_t)((n + 65534) / 65535);
+    std::vector<uint64_t> ioff(nc), ooff(nc);
+    std::vector<uint32_t> ilen(nc);
+    std::vector<int32_t> lim(nc), lvl(nc, e->level);
+    uint64_t oc = 0;
+    for (uint32_t i = 0; i < nc; ++i) {
+        const size_t r = r0 + (size_t)i * 65535;
+        ioff[i] = (uint64_t)i * 65535;
+        ilen[i] = (uint32_t)((n - ioff[i]) < 65535 ? (n - ioff[i]) : 65535);
+        const int64_t l64 = (int64_t)(w - r) - (int64_t)r;  // readableBytes() - inOffset (FastLz.java:552-557)
+        lim[i] = l64 < -0x40000000 ? -0x40000000 : (int32_t)l64;
+        ooff[i] = oc;
+        oc += nx_fastlz_max_compressed_length(ilen[i]) + 16;
+    }
+    Gpu& g = e->g;
+    if (!g.din.ensure(n) || !g.dout.ensure(oc) || !g.a0.ensure(8ull * nc) || !g.a1.ensure(8ull * nc) || !g.a2.ensure(4ull * nc) ||
+        !g.a3.ensure(4ull * nc) || !g.a4.ensure(4ull * nc) || !g.a5.ensure(4ull * nc) || !g.a6.ensure(8ull * nc))
+        return NX_ERR_HIP;
+    bool ok = g.h2d(g.din.p, in, n) && g.h2d(g.a0.p, ioff.data(), 8ull * nc) && g.h2d(g.a1.p, ooff.data(), 8ull * nc) &&
+              g.h2d(g.a2.p, ilen.data(), 4ull * nc) && g.h2d(g.a5.p, lim.data(), 4ull * nc) &&
+              g.h2d(g.a6.p, lvl.data(), 4ull * nc);
+    if (!ok) return NX_ERR_HIP;
+    int32_t r = nx_fastlz_compress_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.dout.as<uint8_t>(),
+                                         g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), g.a6.as<int32_t>(), g.a5.as<int32_t>(),
+                                         g.a4.as<int32_t>(), nc, g.s);
+    if (r != NX_OK) return r;
+    std::vector<uint32_t> ad(nc);
+    if (e->checksum) {
+        // reuse a4 (status no longer needed after the compress kernel ran: stream-ordered)
+        r = nx_adler32_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.a4.as<uint32_t>(), nc, g.s);
+        if (r != NX_OK) return r;
+    }
+    std::vector<uint32_t> clen(nc);
+    std::vector<uint8_t> hout(oc);
+    ok = g.d2h(clen.data(), g.a3.p, 4ull * nc) && g.d2h(hout.data(), g.dout.p, oc) && (!e->checksum || g.d2h(ad.data(), g.a4.p, 4ull * nc)) &&
+         g.sync();
+    if (!ok) return NX_ERR_HIP;
+    size_t op = 0;
+    for (uint32_t i = 0; i < nc; ++i) {
+        const uint32_t length = ilen[i];
+        const size_t outputIdx = op;
+        out[op] = 'F';
+        out[op + 1] = 'L';
+        out[op + 2] = 'Z';
+        size_t outputOffset = outputIdx + 4 + (e->checksum ? 4 : 0);
+        if (e->checksum) {
+            const uint32_t c = ad[i];
+            out[outputIdx + 4] = (uint8_t)(c >> 24);
+            out[outputIdx + 5] = (uint8_t)(c >> 16);
+            out[outputIdx + 6] = (uint8_t)(c >> 8);
+            out[outputIdx + 7] = (uint8_t)c;
+        }
+        uint8_t blockType;
+        uint32_t chunkLength;
+        if (length >= 32 && clen[i] < length) {  // MIN_LENGTH_TO_COMPRESSION (FastLz.java:59), :153-158
+            blockType = 1;
+            chunkLength = clen[i];
+            out[outputOffset] = (uint8_t)(chunkLength >> 8);
+            out[outputOffset + 1] = (uint8_t)chunkLength;
+            outputOffset += 2;
+            memcpy(out + outputOffset + 2, hout.data() + ooff[i], chunkLength);
+        } else {
+            blockType = 0;
+            chunkLength = length;
+            memcpy(out + outputOffset + 2, in + ioff[i], length);
+        }
+        out[outputOffset] = (uint8_t)(length >> 8);
+        out[outputOffset + 1] = (uint8_t)length;
+        out[outputIdx + 3] = (uint8_t)(blockType | (e->checksum ? 0x10 : 0));
+        op = outputOffset + 2 + chunkLength;
+    }
+    return (int64_t)op;
+}
+
+// ======================================================================= FastLZ frame decoder
+struct nx_fastlz_frame_decoder {
+    Gpu g;
+    bool validate;
+    int state = 0;  // 0 INIT_BLOCK, 1 INIT_BLOCK_PARAMS, 2 DECOMPRESS_DATA, 3 CORRUPTED
+    uint32_t chunkLength = 0, originalLength = 0, currentChecksum = 0;
+    bool isCompressed = false, hasChecksum = false;
+    MsgList ml;
+};
+
+extern "C" nx_fastlz_frame_decoder* nx_fastlz_frame_decoder_new(int32_t validate) {
+    auto* d = new nx_fastlz_frame_decoder();
+    if (!d->g.ok) {
+        delete d;
+        return nullptr;
+    }
+    d->validate = validate != 0;
+    return d;
+}
+extern "C" void nx_fastlz_frame_decoder_free(nx_fastlz_frame_decoder* d) { delete d; }
+
+extern "C" int32_t nx_fastlz_frame_decoder_decode(nx_fastlz_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
+                                                  const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {
+    if (!d || (!in && n)) return NX_ERR_INVALID_ARG;
+    MsgList& ml = d->ml;
+    ml.clear();
+    size_t rd = 0;
+    auto finish = [&](int32_t r) {
+        *consumed = rd;
+        *msgs = ml.msgs.data();
+        *n_msgs = ml.msgs.size();
+        if (err_msg) *err_msg = ml.err.empty() ? nullptr : ml.err.c_str();
+        return r;
+    };
+    if (d->state == 3) {
+        rd = n;
+        return finish(NX_OK);
+    }
+    struct Blk {
+        size_t data, end;
+        uint32_t clen, olen, cks;
+        bool comp, has_cks;
+        int job;
+        std::string err;
+    };
+    std::vector<Blk> blks;
+    // host parse (FastLzFrameDecoder.decode as driven by callDecode); persistent header state
+    int state = d->state;
+    uint32_t chunkLength = d->chunkLength, originalLength = d->originalLength, cks = d->currentChecksum;
+    bool isCompressed = d->isCompressed, hasChecksum = d->hasChecksum;
+    size_t p = 0;
+    std::string perr;
+    size_t perr_at = 0;
+    bool have_err = false;
+    for (;;) {
+        if (state == 0) {
+            if (n - p < 4) break;
+            if (be24(in + p) != (('F' << 16) | ('L' << 8) | 'Z')) {
+                perr = "unexpected block identifier";
+                perr_at = p + 3;
+                have_err = true;
+                break;
+            }
+            const uint8_t options = in[p + 3];
+            isCompressed = (options & 0x01) == 1;
+            hasChecksum = (options & 0x10) == 0x10;
+            p += 4;
+            state = 1;
+        }
+        if (state == 1) {
+            const size_t need = 2 + (isCompressed ? 2 : 0) + (hasChecksum ? 4 : 0);
+            if (n - p < need) break;
+            cks = hasChecksum ? be32(in + p) : 0;
+            p += hasChecksum ? 4 : 0;
+            chunkLength = be16(in + p);
+            p += 2;
+            originalLength = isCompressed ? be16(in + p) : chunkLength;
+            p += isCompressed ? 2 : 0;
+            state = 2;
+        }
+        if (state == 2) {
+            if (n - p < chunkLength) break;
+            blks.push_back({p, p + chunkLength, chunkLength, originalLength, cks, isCompressed, hasChecksum, -1, {}});
+            p += chunkLength;
+            state = 0;
+        }
+    }
+    // GPU: decompress every compressed block; Adler32 over every produced block if verifying
+    // (decompressed blocks in dout, raw blocks straight from the staged cumulation in din)
+    uint32_t nz = 0;
+    for (auto& b : blks)
+        if (b.comp) b.job = (int)nz++;
+    const uint32_t nb = (uint32_t)blks.size();
+    const bool want_cks = d->validate;
+    std::vector<int32_t> res(nz);
+    std::vector<uint32_t> adl(nb);
+    std::vector<uint64_t> ooff(nz);
+    uint64_t ocap = 0;
+    for (auto& b : blks)
+        if (b.comp) {
+            ooff[b.job] = ocap;
+            ocap += ((uint64_t)b.olen + 15) & ~15ull;
+        }
+    std::vector<uint8_t> hout(ocap);
+    Gpu& g = d->g;
+    uint32_t ncks = 0;
+    for (auto& b : blks) ncks += (b.has_cks && want_cks) ? 1u : 0u;
+    if (nz || ncks) {
+        const size_t lo = blks.front().data;
+        const size_t span = n - lo;  // decompress may read past its chunk (in_avail = readable bytes)
+        std::vector<uint64_t> ioff(nz);
+        std::vector<uint32_t> ilen(nz), iav(nz), olim(nz);
+        for (auto& b : blks)
+            if (b.comp) {
+                ioff[b.job] = b.data - lo;
+                ilen[b.job] = b.clen;
+                iav[b.job] = (uint32_t)(n - b.data);
+                olim[b.job] = b.olen;
+            }
+        // checksum jobs: compressed → (dout, ooff, olen); raw → (din, data-lo, clen)
+        std::vector<uint64_t> czoff, croff;
+        std::vector<uint32_t> czlen, crlen;
+        std::vector<uint32_t> cz_blk, cr_blk;
+        for (uint32_t i = 0; i < nb; ++i) {
+            const Blk& b = blks[i];
+            if (!(b.has_cks && want_cks)) continue;
+            if (b.comp) {
+                czoff.push_back(ooff[b.job]);
+                czlen.push_back(b.olen);
+                cz_blk.push_back(i);
+            } else {
+                croff.push_back(b.data - lo);
+                crlen.push_back(b.clen);
+                cr_blk.push_back(i);
+            }
+        }
+        const uint32_t ncz = (uint32_t)czoff.size(), ncr = (uint32_t)croff.size();
+        if (!g.din.ensure(span + 1) || !g.dout.ensure(ocap + 16) || !g.a0.ensure(8ull * nz + 8) || !g.a1.ensure(8ull * nz + 8) ||
+            !g.a2.ensure(4ull * nz + 4) || !g.a3.ensure(4ull * nz + 4) || !g.a4.ensure(4ull * nz + 4) || !g.a5.ensure(4ull * nz + 4) ||
+            !g.a6.ensure(16ull * (ncz + ncr) + 16))
+            return finish(NX_ERR_HIP);
+        uint64_t* d_coff = g.a6.as<uint64_t>();
+        uint32_t* d_clen = reinterpret_cast<uint32_t*>(d_coff + ncz + ncr);
+        uint32_t* d_cval = d_clen + ncz + ncr;
+        std::vector<uint64_t> coff(czoff);
+        coff.insert(coff.end(), croff.begin(), croff.end());
+        std::vector<uint32_t> clen(czlen);
+        clen.insert(clen.end(), crlen.begin(), crlen.end());
+        bool ok = g.h2d(g.din.p, in + lo, span) && g.h2d(g.a0.p, ioff.data(), 8ull * nz) && g.h2d(g.a1.p, ooff.data(), 8ull * nz) &&
+                  g.h2d(g.a2.p, ilen.data(), 4ull * nz) && g.h2d(g.a3.p, iav.data(), 4ull * nz) && g.h2d(g.a4.p, olim.data(), 4ull * nz) &&
+                  g.h2d(d_coff, coff.data(), 8ull * (ncz + ncr)) && g.h2d(d_clen, clen.data(), 4ull * (ncz + ncr));
+        if (!ok) return finish(NX_ERR_HIP);
+        if (nz) {
+            int32_t r = nx_fastlz_decompress_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.a3.as<uint32_t>(),
+                                                   g.dout.as<uint8_t>(), g.a1.as<uint64_t>(), g.a4.as<uint32_t>(), g.a5.as<int32_t>(),
+                                                   nz, g.s);
+            if (r != NX_OK) return finish(r);
+        }
+        if (ncz) {
+            int32_t r = nx_adler32_batch(g.dout.as<uint8_t>(), d_coff, d_clen, d_cval, ncz, g.s);
+            if (r != NX_OK) return finish(r);
+        }
+        if (ncr) {
+            int32_t r = nx_adler32_batch(g.din.as<uint8_t>(), d_coff + ncz, d_clen + ncz, d_cval + ncz, ncr, g.s);
+            if (r != NX_OK) return finish(r);
+        }
+        std::vector<uint32_t> cval(ncz + ncr);
+        ok = g.d2h(res.data(), g.a5.p, 4ull * nz) && g.d2h(hout.data(), g.dout.p, ocap) && g.d2h(cval.data(), d_cval, 4ull * (ncz + ncr)) &&
+             g.sync();
+        if (!ok) return finish(NX_ERR_HIP);
+        for (uint32_t k = 0; k < ncz; ++k) adl[cz_blk[k]] = cval[k];
+        for (uint32_t k = 0; k < ncr; ++k) adl[cr_blk[k]] = cval[ncz + k];
+    }
+    // apply in order
+    for (uint32_t i = 0; i < nb; ++i) {
+        Blk& b = blks[i];
+        const uint8_t* data;
+        uint32_t len;
+        if (b.comp) {
+            const int32_t r = res[b.job];
+            if (r < 0 || (uint32_t)r != b.olen) {
+                char buf[160];
+                if (r == NX_ERR_FASTLZ_BAD_LEVEL) {
+                    snprintf(buf, sizeof buf, "invalid level: %d (expected: %d or %d)", ((int8_t)in[b.data] >> 5) + 1, 1, 2);
+                } else if (r < 0) {
+                    snprintf(buf, sizeof buf, "%s", nx_status_string(r));
+                } else {
+                    snprintf(buf, sizeof buf, "stream corrupted: originalLength(%u) and actual length(%d) mismatch", b.olen, r);
+                }
+                ml.err = buf;
+                d->state = 3;
+                rd = b.data;
+                return finish(r < 0 ? r : NX_ERR_FASTLZ_LENGTH_MISMATCH);
+            }
+            data = hout.data() + ooff[b.job];
+            len = b.olen;
+        } else {
+            data = in + b.data;
+            len = b.clen;
+        }
+        if (b.has_cks && want_cks && adl[i] != b.cks) {  // FastLzFrameDecoder.java:171-180
+            char buf[160];
+            snprintf(buf, sizeof buf, "stream corrupted: mismatching checksum: %d (expected: %d)", (int32_t)adl[i], (int32_t)b.cks);
+            ml.err = buf;
+            d->state = 3;
+            rd = b.data;
+            return finish(NX_ERR_FASTLZ_CRC_MISMATCH);
+        }
+        if (len > 0) {
+            if (b.comp) {
+                ml.owned.emplace_back(data, data + len);
+                ml.msgs.push_back({ml.owned.back().data(), len});
+            } else {
+                ml.msgs.push_back({data, len});
+            }
+        }
+        rd = b.end;
+    }
+    if (have_err) {
+        ml.err = perr;
+        d->state = 3;
+        rd = perr_at;
+        return finish(NX_ERR_FRAME_CORRUPT);
+    }
+    rd = p;
+    d->state = state;
+    d->chunkLength = chunkLength;
+    d->originalLength = originalLength;
+    d->currentChecksum = cks;
+    d->isCompressed = isCompressed;
+    d->hasChecksum = hasChecksum;
+    return finish(NX_OK);
+}
+
+// ======================================================================= LZF encoder / decoder
+struct nx_lzf_encoder {
+    Gpu g;
+    int32_t threshold;
+};
+extern "C" nx_lzf_encoder* nx_lzf_encoder_new(int32_t compress_threshold) {
+    if (compress_threshold < 16) return nullptr;  // LzfEncoder.java:155-160
+    auto* e = new nx_lzf_encoder();
+    if (!e->g.ok) {
+        delete e;
+        return nullptr;
+    }
+    e->threshold = compress_threshold;
+    return e;
+}
+extern "C" void nx_lzf_encoder_free(nx_lzf_encoder* e) { delete e; }
+extern "C" size_t nx_lzf_frame_max_encoded_length(size_t n) { return (n / 65535 + 1) * 7 + n + n / 32 + 64; }
+
+extern "C" int64_t nx_lzf_encoder_encode(nx_lzf_encoder* e, const uint8_t* in, size_t n, uint8_t* out, size_t out_cap) {
+    if (!e) return NX_ERR_INVALID_ARG;
+    if (out_cap < nx_lzf_frame_max_encoded_length(n)) return NX_ERR_INVALID_ARG;
+    if ((int64_t)n < e->threshold) {  // encodeNonCompress (LzfEncoder.java:197-203,223-246)
+        size_t op = 0, ip = 0;
+        do {
+            const uint32_t len = (uint32_t)((n - ip) < 65535 ? (n - ip) : 65535);
+            out[op] = 'Z';
+            out[op + 1] = 'V';
+            out[op + 2] = 0;
+            out[op + 3] = (uint8_t)(len >> 8);
+            out[op + 4] = (uint8_t)len;
+            memcpy(out + op + 5, in + ip, len);
+            op += 5 + len;
+            ip += len;
+        } while (ip < n);
+        return (int64_t)op;
+    }
+    const uint32_t nc = (uint32_t)((n + 65534) / 65535);
+    std::vector<uint64_t> ioff(nc), ooff(nc);
+    std::vector<uint32_t> ilen(nc);
+    uint64_t oc = 0;
+    for (uint32_t i = 0; i < nc; ++i) {
+        ioff[i] = (uint64_t)i * 65535;
+        ilen[i] = (uint32_t)((n - ioff[i]) < 65535 ? (n - ioff[i]) : 65535);
+        ooff[i] = oc;
+        oc += nx_lzf_max_compressed_length(ilen[i]) + 16;
+    }
+    Gpu& g = e->g;
+    if (!g.din.ensure(n) || !g.dout.ensure(oc) || !g.a0.ensure(8ull * nc) || !g.a1.ensure(8ull * nc) || !g.a2.ensure(4ull * nc) ||
+        !g.a3.ensure(4ull * nc) || !g.a4.ensure(4ull * nc))
+        return NX_ERR_HIP;
+    bool ok = g.h2d(g.din.p, in, n) && g.h2d(g.a0.p, ioff.data(), 8ull * nc) && g.h2d(g.a1.p, ooff.data(), 8ull * nc) &&
+              g.h2d(g.a2.p, ilen.data(), 4ull * nc);
+    if (!ok) return NX_ERR_HIP;
+    int32_t r = nx_lzf_encode_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.dout.as<uint8_t>(),
+                                    g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), g.a4.as<int32_t>(), nc, g.s);
+    if (r != NX_OK) return r;
+    std::vector<uint32_t> olen(nc);
+    std::vector<uint8_t> hout(oc);
+    ok = g.d2h(olen.data(), g.a3.p, 4ull * nc) && g.d2h(hout.data(), g.dout.p, oc) && g.sync();
+    if (!ok) return NX_ERR_HIP;
+    size_t op = 0;
+    for (uint32_t i = 0; i < nc; ++i) {
+        memcpy(out + op, hout.data() + ooff[i], olen[i]);
+        op += olen[i];
+    }
+    return (int64_t)op;
+}
+
+struct nx_lzf_decoder {
+    Gpu g;
+    int state = 0;  // 0 INIT_BLOCK, 1 INIT_ORIGINAL_LENGTH, 2 DECOMPRESS_DATA, 3 CORRUPTED
+    uint32_t chunkLength = 0, originalLength = 0;
+    bool isCompressed = false;
+    MsgList ml;
+};
+extern "C" nx_lzf_decoder* nx_lzf_decoder_new(void) {
+    auto* d = new nx_lzf_decoder();
+    if (!d->g.ok) {
+        delete d;
+        return nullptr;
+    }
+    return d;
+}
+extern "C" void nx_lzf_decoder_free(nx_lzf_decoder* d) { delete d; }
+
+extern "C" int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, size_t n, size_t* consumed, const nx_msg** msgs,
+                                         size_t* n_msgs, const char** err_msg) {
+    if (!d || (!in && n)) return NX_ERR_INVALID_ARG;
+    MsgList& ml = d->ml;
+    ml.clear();
+    size_t rd = 0;
+    auto finish = [&](int32_t r) {
+        *consumed = rd;
+        *msgs = ml.msgs.data();
+        *n_msgs = ml.msgs.size();
+        if (err_msg) *err_msg = ml.err.empty() ? nullptr : ml.err.c_str();
+        return r;
+    };
+    if (d->state == 3) {
+        rd = n;
+        return finish(NX_OK);
+    }
+    struct Blk {
+        size_t data, end;
+        uint32_t clen, olen;
+        bool comp;
+        int job;
+    };
+    std::vector<Blk> blks;
+    int state = d->state;
+    uint32_t chunkLength = d->chunkLength, originalLength = d->originalLength;
+    bool isCompressed = d->isCompressed;
+    size_t p = 0;
+    std::string perr;
+    size_t perr_at = 0;
+    bool have_err = false;
+    for (;;) {
+        if (state == 0) {
+            if (n - p < 5) break;  // HEADER_LEN_NOT_COMPRESSED
+            if (be16(in + p) != (('Z' << 8) | 'V')) {
+                perr = "unexpected block identifier";
+                perr_at = p + 2;
+                have_err = true;
+                break;
+            }
+            const int8_t type = (int8_t)in[p + 2];
+            if (type != 0 && type != 1) {
+                char buf[96];
+                snprintf(buf, sizeof buf, "unknown type of chunk: %d (expected: %d or %d)", (int)type, 0, 1);
+                perr = buf;
+                perr_at = p + 3;
+                have_err = true;
+                break;
+            }
+            isCompressed = type == 1;
+            chunkLength = be16(in + p + 3);
+            p += 5;
+            state = isCompressed ? 1 : 2;
+            if (!isCompressed) continue;
+        }
+        if (state == 1) {
+            if (n - p < 2) break;
+            originalLength = be16(in + p);
+            p += 2;
+            state = 2;
+        }
+        if (state == 2) {
+            if (n - p < chunkLength) break;
+            blks.push_back({p, p + chunkLength, chunkLength, originalLength, isCompressed, -1});
+            p += chunkLength;
+            state = 0;
+        }
+    }
+    uint32_t nz = 0;
+    uint64_t ocap = 0;
+    std::vector<uint64_t> ooff;
+    for (auto& b : blks)
+        if (b.comp) {
+            b.job = (int)nz++;
+            ooff.push_back(ocap);
+            ocap += ((uint64_t)b.olen + 15) & ~15ull;
+        }
+    std::vector<int32_t> st(nz);
+    std::vector<uint8_t> hout(ocap);
+    Gpu& g = d->g;
+    if (nz) {
+        const size_t lo = blks.front().data;
+        const size_t span = p - lo;
+        std::vector<uint64_t> ioff(nz);
+        std::vector<uint32_t> ilen(nz), olen(nz);
+        for (auto& b : blks)
+            if (b.comp) {
+                ioff[b.job] = b.data - lo;
+                ilen[b.job] = b.clen;
+                olen[b.job] = b.olen;
+            }
+        if (!g.din.ensure(span + 1) || !g.dout.ensure(ocap + 16) || !g.a0.ensure(8ull * nz) || !g.a1.ensure(8ull * nz) ||
+            !g.a2.ensure(4ull * nz) || !g.a3.ensure(4ull * nz) || !g.a4.ensure(4ull * nz))
+            return finish(NX_ERR_HIP);
+        bool ok = g.h2d(g.din.p, in + lo, span) && g.h2d(g.a0.p, ioff.data(), 8ull * nz) && g.h2d(g.a1.p, ooff.data(), 8ull * nz) &&
+                  g.h2d(g.a2.p, ilen.data(), 4ull * nz) && g.h2d(g.a3.p, olen.data(), 4ull * nz);
+        if (!ok) return finish(NX_ERR_HIP);
+        int32_t r = nx_lzf_decode_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.dout.as<uint8_t>(),
+                                        g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), g.a4.as<int32_t>(), nz, g.s);
+        if (r != NX_OK) return finish(r);
+        ok = g.d2h(st.data(), g.a4.p, 4ull * nz) && g.d2h(hout.data(), g.dout.p, ocap) && g.sync();
+        if (!ok) return finish(NX_ERR_HIP);
+    }
+    for (auto& b : blks) {
+        if (b.comp) {
+            if (st[b.job] != NX_OK) {
+                ml.err = "Corrupt LZF data";
+                d->state = 3;
+                rd = b.data;
+                return finish(st[b.job]);
+            }
+            ml.owned.emplace_back(hout.begin() + ooff[b.job], hout.begin() + ooff[b.job] + b.olen);
+            ml.msgs.push_back({ml.owned.back().data(), b.olen});
+        } else if (b.clen > 0) {
+            ml.msgs.push_back({in + b.data, b.clen});
+        }
+        rd = b.end;
+    }
+    if (have_err) {
+        ml.err = perr;
+        d->state = 3;
+        rd = perr_at;
+        return finish(NX_ERR_FRAME_CORRUPT);
+    }
+    rd = p;
+    d->state = state;
+    d->chunkLength = chunkLength;
+    d->originalLength = originalLength;
+    d->isCompressed = isCompressed;
+    return finish(NX_OK);
+}

@@ -1,0 +1,68 @@
+// nx_common.hpp — shared device/host helpers for the gfx950 codec kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include "../../include/netty_amd_status.h"
+
+#define NX_WAVE 64
+
+#define NX_HIP_CHECK(x)                                  \
+    do {                                                 \
+        hipError_t _e = (x);                             \
+        if (_e != hipSuccess) return NX_ERR_HIP;         \
+    } while (0)
+
+namespace nx {
+
+// CRC32C (Castagnoli, reflected poly 0x82F63B78) — Crc32c.java:27-124.
+constexpr uint32_t kCrcPoly = 0x82F63B78u;
+
+// Device-side CRC tables (filled once by crc_tables_init() on the host):
+//   T8[k][b]   : slicing-by-8 tables, T8[0] = byte table of Crc32c.java:27-92
+//   SH[j][k][b]: "shift by 16*2^j bytes" linear maps, j = 0..6 (16 B .. 1 KiB), byte k of the state
+struct CrcTables {
+    uint32_t T8[8][256];
+    uint32_t SH[7][4][256];
+};
+// Device copy of the tables, allocated once per device by crc_tables_init() (kernels take the
+// pointer as an argument: no cross-TU device symbols, so no -fgpu-rdc).
+int crc_tables_init();                 // host: build + upload (idempotent). Returns NX_OK / NX_ERR_HIP.
+const CrcTables* crc_tables_dev();     // device pointer for the current device
+// host helpers (also used by the host handler layer)
+uint32_t host_crc32c(const uint8_t* p, size_t n);
+uint32_t host_mask(uint32_t c);
+
+__host__ __device__ inline uint32_t mask_checksum(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
+
+// GF(2) multiply modulo P in CRC (reflected) representation (zlib multmodp).
+__host__ __device__ inline uint32_t gf_multmodp(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (int i = 0; i < 32; ++i) {
+        p ^= (a & 0x80000000u) ? b : 0u;
+        a <<= 1;
+        b = (b & 1u) ? ((b >> 1) ^ kCrcPoly) : (b >> 1);
+    }
+    return p;
+}
+
+// x^(8n) mod P (reflected), by square-and-multiply.
+__host__ __device__ inline uint32_t gf_x8n(uint64_t n) {
+    uint32_t result = 0x80000000u;  // x^0
+    uint32_t sq = 0x00800000u;      // x^8
+    while (n) {
+        if (n & 1) result = gf_multmodp(sq, result);
+        sq = gf_multmodp(sq, sq);
+        n >>= 1;
+    }
+    return result;
+}
+
+// Kernel launch helper: grid-stride sizes.
+inline unsigned grid_for(uint64_t threads, unsigned block) {
+    uint64_t g = (threads + block - 1) / block;
+    if (g > 65535u * 16u) g = 65535u * 16u;
+    return (unsigned)(g ? g : 1);
+}
+
+}  // namespace nx

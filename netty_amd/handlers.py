@@ -1,0 +1,258 @@
+"""Netty's codec-compression handler API over the GPU path.
+
+Mirrors the public surface of the reference handlers (same names, constructor options,
+encode/decode contracts and error behaviour):
+
+* ``SnappyFrameEncoder()`` / ``SnappyFrameEncoder.snappy_encoder_with_jumbo_frames()``
+  — SnappyFrameEncoder.java:60-117
+* ``SnappyFrameDecoder(validate_checksums=False)`` — SnappyFrameDecoder.java:67-231
+* ``FastLzFrameEncoder(level=0, checksum=False)`` — FastLzFrameEncoder.java:58-172
+* ``FastLzFrameDecoder(validate_checksums=False)`` — FastLzFrameDecoder.java:90-207
+* ``LzfEncoder(compress_threshold=16)`` / ``LzfDecoder()`` — LzfEncoder.java / LzfDecoder.java
+
+Encoders follow ``MessageToByteEncoder.write`` (MessageToByteEncoder.java:99-131): one call per
+outbound message, empty output replaced by an empty buffer.  Decoders follow
+``ByteToMessageDecoder.channelRead`` (ByteToMessageDecoder.java:286-341): inbound bytes are
+cumulated, ``decode`` runs until it stops making progress, consumed bytes are discarded, and a
+failure raises ``DecompressionException`` and leaves the decoder corrupted (all later input is
+skipped).  The per-chunk work runs in libnetty_amd.so (HIP kernels); headers are parsed by the
+native host layer exactly as the Java decode() does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import _lib
+
+
+class DecoderException(Exception):
+    """io.netty.handler.codec.DecoderException"""
+
+
+class EncoderException(Exception):
+    """io.netty.handler.codec.EncoderException"""
+
+
+class DecompressionException(DecoderException):
+    """DecompressionException.java:23"""
+
+
+class CompressionException(EncoderException):
+    """CompressionException.java:23"""
+
+
+def _new(handle, what):
+    if not handle:
+        raise RuntimeError(f"{what}: native handle creation failed (no GPU visible, or invalid options); "
+                           f"the HIP path has no CPU fallback")
+    return handle
+
+
+class _Encoder:
+    """MessageToByteEncoder<ByteBuf> template (MessageToByteEncoder.java:99-160)."""
+
+    _free = None
+
+    def encode(self, data: bytes) -> bytes:  # pragma: no cover - overridden
+        raise NotImplementedError
+
+    def write(self, msg) -> bytes:
+        return self.encode(bytes(msg))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            getattr(_lib.load(), self._free)(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _Decoder:
+    """ByteToMessageDecoder template (ByteToMessageDecoder.java:286-341, callDecode :464-517)."""
+
+    _free = None
+    _decode_fn = None
+
+    def __init__(self):
+        self._cum = bytearray()
+
+    def channel_read(self, data) -> list[bytes]:
+        L = _lib.load()
+        self._cum += bytes(data)
+        buf = bytes(self._cum)
+        consumed = C.c_size_t(0)
+        msgs = C.POINTER(_lib.NxMsg)()
+        nmsg = C.c_size_t(0)
+        err = C.c_char_p()
+        rc = getattr(L, self._decode_fn)(self._h, buf, len(buf), C.byref(consumed), C.byref(msgs), C.byref(nmsg),
+                                         C.byref(err))
+        out = [C.string_at(msgs[i].data, msgs[i].len) if msgs[i].len else b"" for i in range(nmsg.value)]
+        del self._cum[:consumed.value]
+        if rc != 0:
+            if rc in (-100, -101, -102):
+                raise RuntimeError(f"{type(self).__name__}: native failure {rc} ({_lib.status_string(rc)})")
+            msg = err.value.decode() if err.value else _lib.status_string(rc)
+            e = DecompressionException(msg)
+            e.decoded = out  # messages fired before the failing chunk
+            e.status = rc
+            raise e
+        return out
+
+    def readable_bytes(self) -> int:
+        return len(self._cum)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            getattr(_lib.load(), self._free)(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------------------------- Snappy
+class SnappyFrameEncoder(_Encoder):
+    """SnappyFrameEncoder.java:29-153 — 32767-byte slices (65535 with jumbo frames)."""
+
+    _free = "nx_snappy_frame_encoder_free"
+
+    def __init__(self, jumbo: bool = False):
+        self._h = _new(_lib.load().nx_snappy_frame_encoder_new(1 if jumbo else 0), "SnappyFrameEncoder")
+
+    @classmethod
+    def snappy_encoder_with_jumbo_frames(cls) -> "SnappyFrameEncoder":
+        return cls(jumbo=True)
+
+    def encode(self, data: bytes) -> bytes:
+        L = _lib.load()
+        cap = L.nx_snappy_frame_max_encoded_length(len(data))
+        out = (C.c_uint8 * max(cap, 1))()
+        n = L.nx_snappy_frame_encoder_encode(self._h, data, len(data), out, cap)
+        if n < 0:
+            raise CompressionException(_lib.status_string(n))
+        return bytes(out[:n])
+
+
+class SnappyFrameDecoder(_Decoder):
+    """SnappyFrameDecoder.java:37-259 (validateChecksums defaults to false, :67-69)."""
+
+    _free = "nx_snappy_frame_decoder_free"
+    _decode_fn = "nx_snappy_frame_decoder_decode"
+
+    def __init__(self, validate_checksums: bool = False):
+        super().__init__()
+        self._h = _new(_lib.load().nx_snappy_frame_decoder_new(1 if validate_checksums else 0), "SnappyFrameDecoder")
+
+
+# Deprecated aliases kept by the reference (SnappyFramedEncoder.java:22, SnappyFramedDecoder.java:22)
+SnappyFramedEncoder = SnappyFrameEncoder
+SnappyFramedDecoder = SnappyFrameDecoder
+
+
+# ------------------------------------------------------------------------------------- FastLZ
+LEVEL_AUTO, LEVEL_1, LEVEL_2 = 0, 1, 2
+
+
+class FastLzFrameEncoder(_Encoder):
+    """FastLzFrameEncoder.java:45-173.  ``reader_index`` of encode() reproduces the readU16 quirk."""
+
+    _free = "nx_fastlz_frame_encoder_free"
+
+    def __init__(self, level: int = LEVEL_AUTO, checksum: bool = False):
+        if level not in (LEVEL_AUTO, LEVEL_1, LEVEL_2):
+            raise ValueError(f"level: {level} (expected: {LEVEL_AUTO} or {LEVEL_1} or {LEVEL_2})")
+        self._h = _new(_lib.load().nx_fastlz_frame_encoder_new(level, 1 if checksum else 0), "FastLzFrameEncoder")
+
+    def encode(self, data: bytes, reader_index: int = 0, buffer: bytes | None = None) -> bytes:
+        """Encode ``data``; if ``buffer``/``reader_index`` are given, data = buffer[reader_index:]."""
+        L = _lib.load()
+        if buffer is None:
+            buffer, reader_index = bytes(reader_index) + bytes(data), reader_index
+        n = len(buffer) - reader_index
+        cap = L.nx_fastlz_frame_max_encoded_length(n)
+        out = (C.c_uint8 * max(cap, 1))()
+        r = L.nx_fastlz_frame_encoder_encode(self._h, bytes(buffer), reader_index, n, out, cap)
+        if r < 0:
+            raise CompressionException(_lib.status_string(r))
+        return bytes(out[:r])
+
+
+class FastLzFrameDecoder(_Decoder):
+    """FastLzFrameDecoder.java:36-208."""
+
+    _free = "nx_fastlz_frame_decoder_free"
+    _decode_fn = "nx_fastlz_frame_decoder_decode"
+
+    def __init__(self, validate_checksums: bool = False):
+        super().__init__()
+        self._h = _new(_lib.load().nx_fastlz_frame_decoder_new(1 if validate_checksums else 0), "FastLzFrameDecoder")
+
+
+# ------------------------------------------------------------------------------------- LZF
+class LzfEncoder(_Encoder):
+    """LzfEncoder.java:36-253 (compressThreshold default 16, :42)."""
+
+    _free = "nx_lzf_encoder_free"
+
+    def __init__(self, compress_threshold: int = 16):
+        if compress_threshold < 16:
+            raise ValueError(f"compressThreshold:{compress_threshold} expected >=16")
+        self._h = _new(_lib.load().nx_lzf_encoder_new(compress_threshold), "LzfEncoder")
+
+    def encode(self, data: bytes) -> bytes:
+        L = _lib.load()
+        cap = L.nx_lzf_frame_max_encoded_length(len(data))
+        out = (C.c_uint8 * max(cap, 1))()
+        r = L.nx_lzf_encoder_encode(self._h, data, len(data), out, cap)
+        if r < 0:
+            raise CompressionException(_lib.status_string(r))
+        return bytes(out[:r])
+
+
+class LzfDecoder(_Decoder):
+    """LzfDecoder.java:40-242."""
+
+    _free = "nx_lzf_decoder_free"
+    _decode_fn = "nx_lzf_decoder_decode"
+
+    def __init__(self):
+        super().__init__()
+        self._h = _new(_lib.load().nx_lzf_decoder_new(), "LzfDecoder")
+
+
+# ------------------------------------------------------------------------------------- harness
+class EmbeddedChannel:
+    """The subset of io.netty.channel.embedded.EmbeddedChannel the codec tests use
+    (EmbeddedChannel.java:337-483): one handler, outbound/inbound message queues."""
+
+    def __init__(self, handler):
+        self.handler = handler
+        self._outbound: list[bytes] = []
+        self._inbound: list[bytes] = []
+
+    def write_outbound(self, *msgs) -> bool:
+        for m in msgs:
+            # MessageToByteEncoder.write: empty output is replaced by EMPTY_BUFFER (:112-117)
+            self._outbound.append(self.handler.write(m))
+        return bool(self._outbound)
+
+    def write_inbound(self, *msgs) -> bool:
+        for m in msgs:
+            self._inbound.extend(self.handler.channel_read(m))
+        return bool(self._inbound)
+
+    def read_outbound(self):
+        return self._outbound.pop(0) if self._outbound else None
+
+    def read_inbound(self):
+        return self._inbound.pop(0) if self._inbound else None
+
+    def finish(self) -> bool:
+        return bool(self._outbound or self._inbound)

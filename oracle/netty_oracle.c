@@ -1,0 +1,908 @@
+/*
+ * netty_oracle.c — CPU restatement of Netty's codec-compression hot path (parity oracle).
+ *
+ * TEST INFRASTRUCTURE ONLY (see netty_oracle.h).  Never linked into the product library.
+ *
+ * Every function follows the reference line by line; citations are relative to
+ * /root/reference/codec-compression/src/main/java/io/netty/handler/codec/compression/
+ * unless stated otherwise.  Java semantics that matter for bit-exactness are kept:
+ *   - ByteBuf.getInt is BIG-endian (AbstractByteBuf.java:432-435), so Snappy hashes BE loads;
+ *   - Java int arithmetic wraps (uint32_t here), `>>>` is a logical shift;
+ *   - FastLz.readU16 compares an ABSOLUTE index with readableBytes() (the u16_limit quirk).
+ * Pinned by the reference's KATs in tests/test_oracle_kat.py.
+ */
+#include "netty_oracle.h"
+#include "../include/netty_amd_textgen.h"
+#include <stdlib.h>
+#include <string.h>
+
+/* =====================================================================================
+ * CRC32C — Crc32c.java:27-124.  The 256-entry table (reflected poly 0x82F63B78) is
+ * generated rather than transcribed; tests pin T[1]=0xF26B8303 and the KATs.
+ * ===================================================================================== */
+static uint32_t crc_table[256];
+static int crc_ready = 0;
+
+static void crc_init(void) {
+    if (crc_ready) return;
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
+        crc_table[i] = c;
+    }
+    crc_ready = 1;
+}
+
+/* Crc32c.crc32c(crc, b) = crc >>> 8 ^ CRC_TABLE[(crc ^ b & 0xFF) & 0xFF]  (:122-124) */
+uint32_t orc_crc32c_update(uint32_t crc, const uint8_t* p, size_t n) {
+    crc_init();
+    for (size_t i = 0; i < n; ++i) crc = (crc >> 8) ^ crc_table[(crc ^ p[i]) & 0xFFu];
+    return crc;
+}
+
+/* init ~0 (:97), getValue = (crc ^ 0xFFFFFFFF) & 0xFFFFFFFF (:113-115) */
+uint32_t orc_crc32c(const uint8_t* p, size_t n) { return ~orc_crc32c_update(0xFFFFFFFFu, p, n); }
+
+/* Snappy.maskChecksum (:720-722): (int)((c >> 15 | c << 17) + 0xa282ead8) on a long. */
+uint32_t orc_mask_checksum(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
+
+/* Snappy.calculateChecksum (:668-676) */
+uint32_t orc_snappy_checksum(const uint8_t* p, size_t n) { return orc_mask_checksum(orc_crc32c(p, n)); }
+
+/* =====================================================================================
+ * Snappy raw block encoder — Snappy.java:82-313
+ * ===================================================================================== */
+static inline uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+
+/* hash (:177-179): in.getInt(index) * 0x1e35a7bd >>> shift */
+static inline uint32_t snappy_hash(const uint8_t* in, int32_t idx, int shift) {
+    return (be32(in + idx) * 0x1e35a7bdu) >> shift;
+}
+
+static inline int nlz32(uint32_t v) { return v ? __builtin_clz(v) : 32; }
+
+/* MathUtil.findNextPositivePowerOfTwo (common/.../MathUtil.java:34-37) — Java masks shift by 31 */
+static inline uint32_t next_pow2(int32_t value) {
+    int sh = 32 - nlz32((uint32_t)(value - 1));
+    return 1u << (sh & 31);
+}
+
+/* findMatchingLength (:224-239) */
+static int32_t find_matching_length(const uint8_t* in, int32_t minIndex, int32_t inIndex,
+                                    int32_t maxIndex) {
+    int32_t matched = 0;
+    while (inIndex <= maxIndex - 4 && be32(in + inIndex) == be32(in + minIndex + matched)) {
+        inIndex += 4;
+        matched += 4;
+    }
+    while (inIndex < maxIndex && in[minIndex + matched] == in[inIndex]) {
+        ++inIndex;
+        ++matched;
+    }
+    return matched;
+}
+
+/* bitsToEncode (:249-257) = floor(log2(value)) for value > 0 */
+static int bits_to_encode(int32_t value) {
+    uint32_t hob = value ? (1u << (31 - nlz32((uint32_t)value))) : 0;
+    int bl = 0;
+    while ((hob >>= 1) != 0) bl++;
+    return bl;
+}
+
+/* encodeLiteral (:268-281); in points at the literal's first byte */
+static size_t encode_literal(const uint8_t* in, uint8_t* out, size_t op, int32_t length) {
+    if (length < 61) {
+        out[op++] = (uint8_t)((length - 1) << 2);
+    } else {
+        int bitLength = bits_to_encode(length - 1);
+        int bytesToEncode = 1 + bitLength / 8;
+        out[op++] = (uint8_t)((59 + bytesToEncode) << 2);
+        for (int i = 0; i < bytesToEncode; i++) out[op++] = (uint8_t)(((length - 1) >> (i * 8)) & 0xff);
+    }
+    memcpy(out + op, in, (size_t)length);
+    return op + (size_t)length;
+}
+
+/* encodeCopyWithOffset (:283-292) */
+static size_t encode_copy_with_offset(uint8_t* out, size_t op, int32_t offset, int32_t length) {
+    if (length < 12 && offset < 2048) {
+        out[op++] = (uint8_t)(1 | ((length - 4) << 2) | ((offset >> 8) << 5));
+        out[op++] = (uint8_t)(offset & 0xff);
+    } else {
+        out[op++] = (uint8_t)(2 | ((length - 1) << 2));
+        out[op++] = (uint8_t)(offset & 0xff);
+        out[op++] = (uint8_t)((offset >> 8) & 0xff);
+    }
+    return op;
+}
+
+/* encodeCopy (:301-313) */
+static size_t encode_copy(uint8_t* out, size_t op, int32_t offset, int32_t length) {
+    while (length >= 68) {
+        op = encode_copy_with_offset(out, op, offset, 64);
+        length -= 64;
+    }
+    if (length > 64) {
+        op = encode_copy_with_offset(out, op, offset, 60);
+        length -= 60;
+    }
+    return encode_copy_with_offset(out, op, offset, length);
+}
+
+size_t orc_snappy_max_compressed_length(size_t n) { return 32 + n + n / 6; }
+
+/* Snappy.encode (:82-165) with in.readerIndex() == 0 (baseIndex = 0) */
+size_t orc_snappy_encode(const uint8_t* in, int32_t length, uint8_t* out) {
+    size_t op = 0;
+    /* preamble: LE base-128 varint (:84-92); `length >>> i*7` */
+    for (int i = 0;; i++) {
+        uint32_t b = (uint32_t)length >> (i * 7);
+        if ((b & 0xFFFFFF80u) != 0) {
+            out[op++] = (uint8_t)((b & 0x7f) | 0x80);
+        } else {
+            out[op++] = (uint8_t)b;
+            break;
+        }
+    }
+    int32_t inIndex = 0;
+    const int32_t baseIndex = 0;
+    uint32_t hashTableSize = next_pow2(length);
+    if (hashTableSize > (1u << 14)) hashTableSize = 1u << 14; /* MAX_HT_SIZE (:33,98) */
+    uint16_t* table = (uint16_t*)calloc(hashTableSize, sizeof(uint16_t)); /* new short[] (:191) */
+    const int shift = nlz32(hashTableSize) + 1;                           /* (:100) */
+    int32_t nextEmit = inIndex;
+
+    if (length - inIndex >= 15) { /* MIN_COMPRESSIBLE_BYTES (:34,104) */
+        uint32_t nextHash = snappy_hash(in, ++inIndex, shift);
+        for (;;) { /* outer: */
+            int32_t skip = 32;
+            int32_t candidate;
+            int32_t nextIndex = inIndex;
+            do {
+                inIndex = nextIndex;
+                uint32_t hash = nextHash;
+                int32_t bytesBetweenHashLookups = skip++ >> 5;
+                nextIndex = inIndex + bytesBetweenHashLookups;
+                if (nextIndex > length - 4) goto done_outer;
+                nextHash = snappy_hash(in, nextIndex, shift);
+                candidate = baseIndex + table[hash];
+                table[hash] = (uint16_t)(inIndex - baseIndex);
+            } while (be32(in + inIndex) != be32(in + candidate));
+
+            op = encode_literal(in + nextEmit, out, op, inIndex - nextEmit);
+
+            int32_t insertTail;
+            do {
+                int32_t base = inIndex;
+                int32_t matched = 4 + find_matching_length(in, candidate + 4, inIndex + 4, length);
+                inIndex += matched;
+                int32_t offset = base - candidate;
+                op = encode_copy(out, op, offset, matched);
+                insertTail = inIndex - 1;
+                nextEmit = inIndex;
+                if (inIndex >= length - 4) goto done_outer;
+                uint32_t prevHash = snappy_hash(in, insertTail, shift);
+                table[prevHash] = (uint16_t)(inIndex - baseIndex - 1);
+                uint32_t currentHash = snappy_hash(in, insertTail + 1, shift);
+                candidate = baseIndex + table[currentHash];
+                table[currentHash] = (uint16_t)(inIndex - baseIndex);
+            } while (be32(in + insertTail + 1) == be32(in + candidate));
+
+            nextHash = snappy_hash(in, insertTail + 2, shift);
+            ++inIndex;
+        }
+    }
+done_outer:
+    if (nextEmit < length) op = encode_literal(in + nextEmit, out, op, length - nextEmit);
+    free(table);
+    return op;
+}
+
+/* =====================================================================================
+ * Snappy raw block decoder — Snappy.java:315-650, driven once per complete chunk as
+ * SnappyFrameDecoder.java:205-216 does.  NOT_ENOUGH_INPUT → silent return (partial).
+ * ===================================================================================== */
+int64_t orc_snappy_get_preamble(const uint8_t* in, size_t in_len) {
+    /* readPreamble (:404-420) */
+    uint32_t length = 0;
+    int byteIndex = 0;
+    size_t ip = 0;
+    while (ip < in_len) {
+        uint32_t current = in[ip++];
+        length |= (current & 0x7f) << (byteIndex++ * 7);
+        if ((current & 0x80) == 0) return (int64_t)length;
+        if (byteIndex >= 4) return NX_ERR_SNAPPY_PREAMBLE_TOO_LONG;
+    }
+    return 0;
+}
+
+int32_t orc_snappy_decode(const uint8_t* in, size_t in_len, uint8_t* out, size_t out_cap,
+                          size_t* out_len, size_t* consumed) {
+    size_t ip = 0, op = 0;
+    int32_t st = NX_OK;
+    *out_len = 0;
+    *consumed = 0;
+    if (in_len == 0) return NX_OK;
+    /* READING_PREAMBLE (:318-330) */
+    uint32_t ulen = 0;
+    {
+        int byteIndex = 0;
+        int complete = 0;
+        while (ip < in_len) {
+            uint32_t current = in[ip++];
+            ulen |= (current & 0x7f) << (byteIndex++ * 7);
+            if ((current & 0x80) == 0) { complete = 1; break; }
+            if (byteIndex >= 4) { *consumed = ip; return NX_ERR_SNAPPY_PREAMBLE_TOO_LONG; }
+        }
+        if (!complete || ulen == 0) { *consumed = ip; return NX_OK; }
+        /* out.ensureWritable(uncompressedLength) against the max capacity */
+        if ((size_t)ulen > out_cap) { *consumed = ip; return NX_ERR_SNAPPY_OUTPUT_OVERFLOW; }
+    }
+    size_t written = 0; /* Snappy.written */
+    while (ip < in_len) {
+        /* READING_TAG (:331-346) */
+        uint8_t tag = in[ip++];
+        size_t after_tag = ip;
+        uint32_t type = tag & 3u;
+        if (type == 0) {
+            /* decodeLiteral (:454-494) */
+            uint32_t code = (tag >> 2) & 0x3Fu;
+            int64_t length;
+            if (code < 60) {
+                length = code;
+            } else {
+                uint32_t nb = code - 59; /* 60→1, 61→2, 62→3, 63→4 */
+                if (in_len - ip < nb) { ip = after_tag; goto partial; }
+                uint32_t v = 0;
+                for (uint32_t k = 0; k < nb; ++k) v |= (uint32_t)in[ip + k] << (8 * k);
+                ip += nb;
+                length = (nb == 4) ? (int64_t)(int32_t)v : (int64_t)v; /* readIntLE is signed */
+            }
+            /* `length += 1` in Java int */
+            int32_t jlen = (int32_t)(uint32_t)((uint32_t)length + 1u);
+            if (jlen >= 0 && in_len - ip < (size_t)jlen) { ip = after_tag; goto partial; }
+            if (jlen < 0) { st = NX_ERR_SNAPPY_LITERAL_LEN_INVALID; goto fail; }
+            if (op + (size_t)jlen > out_cap) { st = NX_ERR_SNAPPY_OUTPUT_OVERFLOW; goto fail; }
+            memcpy(out + op, in + ip, (size_t)jlen);
+            ip += (size_t)jlen;
+            op += (size_t)jlen;
+            written += (size_t)jlen;
+        } else {
+            int64_t length, offset;
+            if (type == 1) { /* decodeCopyWith1ByteOffset (:509-538) */
+                if (in_len - ip < 1) goto partial;
+                length = 4 + ((tag & 0x1c) >> 2);
+                offset = ((int64_t)(tag & 0xe0) << 3) | in[ip];
+                ip += 1;
+            } else if (type == 2) { /* decodeCopyWith2ByteOffset (:553-582) */
+                if (in_len - ip < 2) goto partial;
+                length = 1 + ((tag >> 2) & 0x3f);
+                offset = (int64_t)in[ip] | ((int64_t)in[ip + 1] << 8);
+                ip += 2;
+            } else { /* decodeCopyWith4ByteOffset (:597-626) */
+                if (in_len - ip < 4) goto partial;
+                length = 1 + ((tag >> 2) & 0x3f);
+                uint32_t v = (uint32_t)in[ip] | ((uint32_t)in[ip + 1] << 8) | ((uint32_t)in[ip + 2] << 16) |
+                             ((uint32_t)in[ip + 3] << 24);
+                offset = (int64_t)(int32_t)v;
+                ip += 4;
+            }
+            /* validateOffset (:637-650) */
+            if (offset == 0) { st = NX_ERR_SNAPPY_OFFSET_ZERO; goto fail; }
+            if (offset < 0) { st = NX_ERR_SNAPPY_OFFSET_NEGATIVE; goto fail; }
+            if ((size_t)offset > written) { st = NX_ERR_SNAPPY_OFFSET_BEYOND; goto fail; }
+            if (op + (size_t)length > out_cap) { st = NX_ERR_SNAPPY_OUTPUT_OVERFLOW; goto fail; }
+            /* the piecewise readBytes loops (:521-534) equal a byte-serial LZ77 copy */
+            for (int64_t k = 0; k < length; ++k) out[op + k] = out[op + k - offset];
+            op += (size_t)length;
+            written += (size_t)length;
+        }
+        continue;
+    partial:
+        /* NOT_ENOUGH_INPUT: tag consumed, its operands left unread */
+        *out_len = op;
+        *consumed = ip;
+        return NX_OK;
+    }
+    *out_len = op;
+    *consumed = ip;
+    return NX_OK;
+fail:
+    *out_len = op;
+    *consumed = ip;
+    return st;
+}
+
+/* =====================================================================================
+ * Snappy framing encoder — SnappyFrameEncoder.java:79-152
+ * ===================================================================================== */
+static const uint8_t STREAM_START[10] = {0xff, 0x06, 0x00, 0x00, 0x73, 0x4e, 0x61, 0x50, 0x70, 0x59};
+
+size_t orc_snappy_frame_max_encoded(size_t n) { return 10 + (n / 32767 + 2) * 8 + orc_snappy_max_compressed_length(n); }
+
+static size_t write_unencoded_chunk(const uint8_t* in, size_t n, uint8_t* out, size_t op) {
+    /* writeUnencodedChunk (:119-124) */
+    out[op++] = 1;
+    uint32_t cl = (uint32_t)n + 4;
+    out[op++] = (uint8_t)cl;
+    out[op++] = (uint8_t)(cl >> 8);
+    out[op++] = (uint8_t)(cl >> 16);
+    uint32_t crc = orc_snappy_checksum(in, n);
+    memcpy(out + op, &crc, 4); /* writeIntLE */
+    op += 4;
+    memcpy(out + op, in, n);
+    return op + n;
+}
+
+size_t orc_snappy_frame_encode(const uint8_t* in, size_t n, int jumbo, int* started, uint8_t* out) {
+    const int32_t sliceSize = jumbo ? 65535 : 32767; /* (:31,39) */
+    size_t op = 0, ip = 0;
+    if (n == 0) return 0; /* !in.isReadable() */
+    if (!*started) {
+        *started = 1;
+        memcpy(out, STREAM_START, 10);
+        op = 10;
+    }
+    int64_t dataLength = (int64_t)n;
+    if (dataLength > 18) { /* MIN_COMPRESSIBLE_LENGTH (:46) */
+        for (;;) {
+            size_t lengthIdx = op + 1;
+            if (dataLength < 18) {
+                op = write_unencoded_chunk(in + ip, (size_t)dataLength, out, op);
+                break;
+            }
+            memset(out + op, 0, 4); /* out.writeInt(0) */
+            op += 4;
+            int32_t len = dataLength > sliceSize ? sliceSize : (int32_t)dataLength;
+            uint32_t crc = orc_snappy_checksum(in + ip, (size_t)len);
+            memcpy(out + op, &crc, 4);
+            op += 4;
+            op += orc_snappy_encode(in + ip, len, out + op);
+            /* setChunkLength (:126-132) */
+            uint32_t chunkLength = (uint32_t)(op - lengthIdx - 3);
+            out[lengthIdx] = (uint8_t)chunkLength;
+            out[lengthIdx + 1] = (uint8_t)(chunkLength >> 8);
+            out[lengthIdx + 2] = (uint8_t)(chunkLength >> 16);
+            ip += (size_t)len;
+            if (dataLength > sliceSize) {
+                dataLength -= sliceSize;
+            } else {
+                break;
+            }
+        }
+    } else {
+        op = write_unencoded_chunk(in, n, out, op);
+    }
+    return op;
+}
+
+/* =====================================================================================
+ * FastLZ — FastLz.java:96-557
+ * ===================================================================================== */
+#define FLZ_MAX_DISTANCE 8191
+#define FLZ_MAX_FARDISTANCE (65535 + FLZ_MAX_DISTANCE - 1)
+#define FLZ_HASH_LOG 13
+#define FLZ_HASH_SIZE (1 << FLZ_HASH_LOG)
+#define FLZ_HASH_MASK (FLZ_HASH_SIZE - 1)
+#define FLZ_MAX_COPY 32
+#define FLZ_MAX_LEN (256 + 8)
+
+/* readU16 (:552-557): absolute-index quirk expressed relative to the chunk start */
+static inline int32_t flz_read_u16(const uint8_t* in, int32_t o, int32_t u16_limit) {
+    if (o + 1 >= u16_limit) return in[o];
+    return ((int32_t)in[o + 1] << 8) | in[o];
+}
+
+/* hashFunction (:545-550) */
+static inline int32_t flz_hash(const uint8_t* in, int32_t o, int32_t lim) {
+    int32_t v = flz_read_u16(in, o, lim);
+    v ^= flz_read_u16(in, o + 1, lim) ^ (v >> (16 - FLZ_HASH_LOG));
+    v &= FLZ_HASH_MASK;
+    return v;
+}
+
+int32_t orc_fastlz_compress(const uint8_t* in, int32_t inLength, uint8_t* out, int32_t proposedLevel,
+                            int32_t lim) {
+    const int32_t level = proposedLevel == 0 ? (inLength < 65536 ? 1 : 2) : proposedLevel; /* (:98-103) */
+    int32_t ip = 0;
+    int32_t ipBound = ip + inLength - 2;
+    int32_t ipLimit = ip + inLength - 12;
+    int32_t op = 0;
+    int32_t copy;
+    if (inLength < 4) { /* (:123-135) */
+        if (inLength != 0) {
+            out[op++] = (uint8_t)(inLength - 1);
+            ipBound++;
+            while (ip <= ipBound) out[op++] = in[ip++];
+            return inLength + 1;
+        }
+        return 0;
+    }
+    int32_t* htab = (int32_t*)malloc(sizeof(int32_t) * FLZ_HASH_SIZE);
+    for (int32_t h = 0; h < FLZ_HASH_SIZE; h++) htab[h] = ip; /* (:139-142) */
+    copy = 2;
+    out[op++] = FLZ_MAX_COPY - 1;
+    out[op++] = in[ip++];
+    out[op++] = in[ip++];
+    while (ip < ipLimit) { /* main loop (:151) */
+        int32_t ref = 0;
+        int64_t distance = 0;
+        int32_t len = 3;
+        int32_t anchor = ip;
+        int matchLabel = 0;
+        if (level == 2) { /* check for a run (:167-180) */
+            if (in[ip] == in[ip - 1] && flz_read_u16(in, ip - 1, lim) == flz_read_u16(in, ip + 1, lim)) {
+                distance = 1;
+                ip += 3;
+                ref = anchor + (3 - 1);
+                matchLabel = 1;
+            }
+        }
+        if (!matchLabel) {
+            int32_t hval = flz_hash(in, ip, lim);
+            ref = htab[hval];
+            distance = anchor - ref;
+            htab[hval] = anchor;
+            int lit = 0;
+            if (distance == 0 || (level == 1 ? distance >= FLZ_MAX_DISTANCE : distance >= FLZ_MAX_FARDISTANCE)) {
+                lit = 1;
+            } else if (in[ref++] != in[ip++]) {
+                lit = 1;
+            } else if (in[ref++] != in[ip++]) {
+                lit = 1;
+            } else if (in[ref++] != in[ip++]) {
+                lit = 1;
+            }
+            if (!lit && level == 2 && distance >= FLZ_MAX_DISTANCE) { /* far match (:216-235) */
+                if (in[ip++] != in[ref++]) {
+                    lit = 1;
+                } else if (in[ip++] != in[ref++]) {
+                    lit = 1;
+                } else {
+                    len += 2;
+                }
+            }
+            if (lit) { /* literal: (:206-212) */
+                out[op++] = in[anchor++];
+                ip = anchor;
+                copy++;
+                if (copy == FLZ_MAX_COPY) {
+                    copy = 0;
+                    out[op++] = FLZ_MAX_COPY - 1;
+                }
+                continue;
+            }
+        }
+        /* match: (:240-358) */
+        ip = anchor + len;
+        distance--;
+        if (distance == 0) {
+            uint8_t x = in[ip - 1];
+            while (ip < ipBound) {
+                if (in[ref++] != x) break;
+                ip++;
+            }
+        } else {
+            int missMatch = 0;
+            for (int i = 0; i < 8; i++) {
+                if (in[ref++] != in[ip++]) { missMatch = 1; break; }
+            }
+            if (!missMatch) {
+                while (ip < ipBound) {
+                    if (in[ref++] != in[ip++]) break;
+                }
+            }
+        }
+        if (copy != 0) {
+            out[op - copy - 1] = (uint8_t)(copy - 1);
+        } else {
+            op--;
+        }
+        copy = 0;
+        ip -= 3;
+        len = ip - anchor;
+        if (level == 2) {
+            if (distance < FLZ_MAX_DISTANCE) {
+                if (len < 7) {
+                    out[op++] = (uint8_t)((len << 5) + (int32_t)(distance >> 8));
+                    out[op++] = (uint8_t)(distance & 255);
+                } else {
+                    out[op++] = (uint8_t)((7 << 5) + (int32_t)(distance >> 8));
+                    for (len -= 7; len >= 255; len -= 255) out[op++] = 255;
+                    out[op++] = (uint8_t)len;
+                    out[op++] = (uint8_t)(distance & 255);
+                }
+            } else {
+                distance -= FLZ_MAX_DISTANCE;
+                if (len < 7) {
+                    out[op++] = (uint8_t)((len << 5) + 31);
+                    out[op++] = 255;
+                    out[op++] = (uint8_t)(distance >> 8);
+                    out[op++] = (uint8_t)(distance & 255);
+                } else {
+                    out[op++] = (uint8_t)((7 << 5) + 31);
+                    for (len -= 7; len >= 255; len -= 255) out[op++] = 255;
+                    out[op++] = (uint8_t)len;
+                    out[op++] = 255;
+                    out[op++] = (uint8_t)(distance >> 8);
+                    out[op++] = (uint8_t)(distance & 255);
+                }
+            }
+        } else {
+            if (len > FLZ_MAX_LEN - 2) {
+                while (len > FLZ_MAX_LEN - 2) {
+                    out[op++] = (uint8_t)((7 << 5) + (int32_t)(distance >> 8));
+                    out[op++] = (uint8_t)(FLZ_MAX_LEN - 2 - 7 - 2);
+                    out[op++] = (uint8_t)(distance & 255);
+                    len -= FLZ_MAX_LEN - 2;
+                }
+            }
+            if (len < 7) {
+                out[op++] = (uint8_t)((len << 5) + (int32_t)(distance >> 8));
+                out[op++] = (uint8_t)(distance & 255);
+            } else {
+                out[op++] = (uint8_t)((7 << 5) + (int32_t)(distance >> 8));
+                out[op++] = (uint8_t)(len - 7);
+                out[op++] = (uint8_t)(distance & 255);
+            }
+        }
+        int32_t hv = flz_hash(in, ip, lim);
+        htab[hv] = ip++;
+        hv = flz_hash(in, ip, lim);
+        htab[hv] = ip++;
+        out[op++] = FLZ_MAX_COPY - 1;
+    }
+    /* left-over as literal copy (:375-391) */
+    ipBound++;
+    while (ip <= ipBound) {
+        out[op++] = in[ip++];
+        copy++;
+        if (copy == FLZ_MAX_COPY) {
+            copy = 0;
+            out[op++] = FLZ_MAX_COPY - 1;
+        }
+    }
+    if (copy != 0) {
+        out[op - copy - 1] = (uint8_t)(copy - 1);
+    } else {
+        op--;
+    }
+    if (level == 2) out[0] |= 1 << 5; /* (:393-396) */
+    free(htab);
+    return op;
+}
+
+int32_t orc_fastlz_decompress(const uint8_t* in, int32_t inLength, int32_t in_avail, uint8_t* out,
+                              int32_t outLength) {
+#define FLZ_IN(i) ((i) < in_avail ? (int32_t)in[(i)] : (oob = 1, 0))
+    int oob = 0;
+    if (in_avail < 1) return NX_ERR_FASTLZ_INPUT_OOB;
+    const int32_t level = ((int8_t)in[0] >> 5) + 1; /* getByte is signed (:412) */
+    if (level != 1 && level != 2) return NX_ERR_FASTLZ_BAD_LEVEL;
+    int32_t ip = 0, op = 0;
+    int64_t ctrl = in[ip++] & 31;
+    int loop = 1;
+    do {
+        int64_t ref = op;
+        int64_t len = ctrl >> 5;
+        int64_t ofs = (ctrl & 31) << 8;
+        if (ctrl >= 32) {
+            len--;
+            ref -= ofs;
+            int32_t code;
+            if (len == 6) {
+                if (level == 1) {
+                    len += FLZ_IN(ip); ip++;
+                } else {
+                    do {
+                        code = FLZ_IN(ip); ip++;
+                        if (oob) return NX_ERR_FASTLZ_INPUT_OOB;
+                        len += code;
+                    } while (code == 255);
+                }
+            }
+            if (level == 1) {
+                ref -= FLZ_IN(ip); ip++;
+            } else {
+                code = FLZ_IN(ip); ip++;
+                ref -= code;
+                if (code == 255 && ofs == (31 << 8)) {
+                    ofs = (int64_t)FLZ_IN(ip) << 8; ip++;
+                    ofs += FLZ_IN(ip); ip++;
+                    ref = (int32_t)(op - ofs - FLZ_MAX_DISTANCE);
+                }
+            }
+            if (oob) return NX_ERR_FASTLZ_INPUT_OOB;
+            if (op + len + 3 > outLength) return 0;
+            if (ref - 1 < 0) return 0;
+            if (ip < inLength) {
+                ctrl = FLZ_IN(ip); ip++;
+                if (oob) return NX_ERR_FASTLZ_INPUT_OOB;
+            } else {
+                loop = 0;
+            }
+            if (ref == op) {
+                uint8_t b = out[ref - 1];
+                out[op++] = b;
+                out[op++] = b;
+                out[op++] = b;
+                while (len != 0) { out[op++] = b; --len; }
+            } else {
+                ref--;
+                out[op++] = out[ref++];
+                out[op++] = out[ref++];
+                out[op++] = out[ref++];
+                while (len != 0) { out[op++] = out[ref++]; --len; }
+            }
+        } else {
+            ctrl++;
+            if (op + ctrl > outLength) return 0;
+            if (ip + ctrl > inLength) return 0;
+            out[op++] = in[ip++];
+            for (--ctrl; ctrl != 0; ctrl--) out[op++] = in[ip++];
+            loop = ip < inLength ? 1 : 0;
+            if (loop) ctrl = in[ip++];
+        }
+    } while (loop != 0);
+    return op;
+#undef FLZ_IN
+}
+
+/* java.util.zip.Adler32 (zlib adler32) */
+uint32_t orc_adler32(const uint8_t* p, size_t n) {
+    uint32_t a = 1, b = 0;
+    for (size_t i = 0; i < n; ++i) {
+        a = (a + p[i]) % 65521u;
+        b = (b + a) % 65521u;
+    }
+    return (b << 16) | a;
+}
+
+size_t orc_fastlz_frame_max_encoded(size_t n) { return (n / 65535 + 1) * (12 + 66) + n + n / 16; }
+
+/* FastLzFrameEncoder.encode (FastLzFrameEncoder.java:111-172).  buf[r0 .. r0+n) is readable. */
+size_t orc_fastlz_frame_encode(const uint8_t* buf, size_t r0, size_t n, int level, int checksum, uint8_t* out) {
+    size_t op = 0;
+    size_t r = r0;
+    const size_t w = r0 + n;
+    while (r < w) {
+        const int32_t length = (int32_t)((w - r) < 65535 ? (w - r) : 65535);
+        const size_t outputIdx = op;
+        out[op + 0] = 'F'; out[op + 1] = 'L'; out[op + 2] = 'Z';
+        size_t outputOffset = outputIdx + 4 + (checksum ? 4 : 0);
+        uint8_t blockType;
+        int32_t chunkLength;
+        if (checksum) {
+            uint32_t c = orc_adler32(buf + r, (size_t)length);
+            out[outputIdx + 4] = (uint8_t)(c >> 24); out[outputIdx + 5] = (uint8_t)(c >> 16);
+            out[outputIdx + 6] = (uint8_t)(c >> 8);  out[outputIdx + 7] = (uint8_t)c;
+        }
+        if (length < 32) { /* MIN_LENGTH_TO_COMPRESSION */
+            blockType = 0;
+            memcpy(out + outputOffset + 2, buf + r, (size_t)length);
+            chunkLength = length;
+        } else {
+            /* readU16 limit: readableBytes() - inOffset = (w - r) - r */
+            int64_t lim64 = (int64_t)(w - r) - (int64_t)r;
+            int32_t lim = lim64 < -0x40000000 ? -0x40000000 : (int32_t)lim64;
+            int32_t clen = orc_fastlz_compress(buf + r, length, out + outputOffset + 4, level, lim);
+            if (clen < length) {
+                blockType = 1;
+                chunkLength = clen;
+                out[outputOffset] = (uint8_t)(chunkLength >> 8);
+                out[outputOffset + 1] = (uint8_t)chunkLength;
+                outputOffset += 2;
+            } else {
+                blockType = 0;
+                memcpy(out + outputOffset + 2, buf + r, (size_t)length);
+                chunkLength = length;
+            }
+        }
+        out[outputOffset] = (uint8_t)(length >> 8);
+        out[outputOffset + 1] = (uint8_t)length;
+        out[outputIdx + 3] = (uint8_t)(blockType | (checksum ? 0x10 : 0));
+        op = outputOffset + 2 + (size_t)chunkLength;
+        r += (size_t)length;
+    }
+    return op;
+}
+
+/* =====================================================================================
+ * LZF — format restated from liblzf / com.ning:compress-lzf 1.0.3 (third party, not in
+ * /root/reference).  Decoder: ChunkDecoder.decodeChunk semantics as called from
+ * LzfDecoder.java:205 (loop until outPos == outEnd; overrun/underrun/bad ref → error).
+ * Encoder: the build's own greedy hash encoder (PARITY UNPINNED — no reference bytes).
+ * ===================================================================================== */
+int32_t orc_lzf_decode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out, int32_t out_len) {
+    int32_t ip = 0, op = 0;
+    do {
+        if (ip >= in_len) return NX_ERR_LZF_CORRUPT;
+        int32_t ctrl = in[ip++];
+        if (ctrl < 32) { /* literal run of ctrl+1 */
+            int32_t n = ctrl + 1;
+            if (ip + n > in_len || op + n > out_len) return NX_ERR_LZF_CORRUPT;
+            memcpy(out + op, in + ip, (size_t)n);
+            ip += n;
+            op += n;
+            continue;
+        }
+        int32_t len = ctrl >> 5;
+        int32_t ref = op - ((ctrl & 0x1f) << 8) - 1;
+        if (len == 7) {
+            if (ip >= in_len) return NX_ERR_LZF_CORRUPT;
+            len += in[ip++];
+        }
+        if (ip >= in_len) return NX_ERR_LZF_CORRUPT;
+        ref -= in[ip++];
+        len += 2;
+        if (ref < 0 || op + len > out_len) return NX_ERR_LZF_CORRUPT;
+        for (int32_t k = 0; k < len; ++k) out[op + k] = out[ref + k];
+        op += len;
+    } while (op < out_len);
+    return op == out_len ? NX_OK : NX_ERR_LZF_CORRUPT;
+}
+
+#define LZF_HLOG 14
+#define LZF_MAX_OFF 8192
+#define LZF_MAX_REF 264
+#define LZF_MAX_LIT 32
+
+static inline uint32_t lzf_hash(uint32_t v) { return ((v * 2654435761u) >> (32 - LZF_HLOG)) & ((1u << LZF_HLOG) - 1); }
+
+int32_t orc_lzf_compress_body(const uint8_t* in, int32_t n, uint8_t* out) {
+    int32_t* htab = (int32_t*)malloc(sizeof(int32_t) << LZF_HLOG);
+    for (int i = 0; i < (1 << LZF_HLOG); ++i) htab[i] = -1;
+    int32_t ip = 0, op = 0, lit = 0;
+    op++; /* literal-length placeholder */
+    while (ip + 2 < n) {
+        uint32_t seq = ((uint32_t)in[ip] << 16) | ((uint32_t)in[ip + 1] << 8) | in[ip + 2];
+        uint32_t h = lzf_hash(seq);
+        int32_t ref = htab[h];
+        htab[h] = ip;
+        int32_t off = ip - ref - 1;
+        if (ref >= 0 && off < LZF_MAX_OFF && in[ref] == in[ip] && in[ref + 1] == in[ip + 1] &&
+            in[ref + 2] == in[ip + 2]) {
+            int32_t maxlen = n - ip;
+            if (maxlen > LZF_MAX_REF) maxlen = LZF_MAX_REF;
+            int32_t len = 3;
+            while (len < maxlen && in[ref + len] == in[ip + len]) len++;
+            if (lit) {
+                out[op - lit - 1] = (uint8_t)(lit - 1);
+            } else {
+                op--;
+            }
+            lit = 0;
+            int32_t l2 = len - 2;
+            if (l2 < 7) {
+                out[op++] = (uint8_t)((off >> 8) + (l2 << 5));
+            } else {
+                out[op++] = (uint8_t)((off >> 8) + (7 << 5));
+                out[op++] = (uint8_t)(l2 - 7);
+            }
+            out[op++] = (uint8_t)off;
+            op++; /* next literal placeholder */
+            ip += len;
+            if (ip + 2 < n) {
+                uint32_t s1 = ((uint32_t)in[ip - 1] << 16) | ((uint32_t)in[ip] << 8) | in[ip + 1];
+                htab[lzf_hash(s1)] = ip - 1;
+            }
+            continue;
+        }
+        out[op++] = in[ip++];
+        if (++lit == LZF_MAX_LIT) {
+            out[op - lit - 1] = (uint8_t)(lit - 1);
+            lit = 0;
+            op++;
+        }
+    }
+    while (ip < n) {
+        out[op++] = in[ip++];
+        if (++lit == LZF_MAX_LIT) {
+            out[op - lit - 1] = (uint8_t)(lit - 1);
+            lit = 0;
+            op++;
+        }
+    }
+    if (lit) {
+        out[op - lit - 1] = (uint8_t)(lit - 1);
+    } else {
+        op--;
+    }
+    free(htab);
+    return op;
+}
+
+/* One LZFChunk: compressed "ZV 01 clen ulen body" if it beats "ZV 00 len data", else the latter. */
+size_t orc_lzf_encode_chunk(const uint8_t* in, int32_t n, uint8_t* out) {
+    if (n >= 16) {
+        int32_t clen = orc_lzf_compress_body(in, n, out + 7);
+        if (clen + 7 < n + 5) {
+            out[0] = 'Z'; out[1] = 'V'; out[2] = 1;
+            out[3] = (uint8_t)(clen >> 8); out[4] = (uint8_t)clen;
+            out[5] = (uint8_t)(n >> 8); out[6] = (uint8_t)n;
+            return (size_t)clen + 7;
+        }
+    }
+    out[0] = 'Z'; out[1] = 'V'; out[2] = 0;
+    out[3] = (uint8_t)(n >> 8); out[4] = (uint8_t)n;
+    memcpy(out + 5, in, (size_t)n);
+    return (size_t)n + 5;
+}
+
+size_t orc_lzf_frame_max_encoded(size_t n) { return (n / 65535 + 1) * 7 + n + n / 32 + 64 + 66; }
+
+/* LzfEncoder.encode (LzfEncoder.java:169-216): split into 65535-byte chunks
+ * (LZFEncoder.appendEncoded), or non-compressed chunks below compressThreshold (:197-203). */
+size_t orc_lzf_frame_encode(const uint8_t* in, size_t n, int32_t compress_threshold, uint8_t* out) {
+    size_t op = 0, ip = 0;
+    /* an empty message still yields one empty non-compressed chunk (lzfEncodeNonCompress :223-239) */
+    do {
+        int32_t len = (int32_t)((n - ip) < 65535 ? (n - ip) : 65535);
+        if ((int64_t)n >= compress_threshold) {
+            op += orc_lzf_encode_chunk(in + ip, len, out + op);
+        } else {
+            out[op] = 'Z'; out[op + 1] = 'V'; out[op + 2] = 0;
+            out[op + 3] = (uint8_t)(len >> 8); out[op + 4] = (uint8_t)len;
+            memcpy(out + op + 5, in + ip, (size_t)len);
+            op += (size_t)len + 5;
+        }
+        ip += (size_t)len;
+    } while (ip < n);
+    return op;
+}
+
+/* =====================================================================================
+ * java.util.Random (nextBytes / nextLong) — used to regenerate the reference's seeded inputs
+ * (SnappyIntegrationTest.java:105-108, AbstractIntegrationTest.java:106-112).
+ * ===================================================================================== */
+#define JR_MULT 0x5DEECE66DLL
+#define JR_MASK ((1LL << 48) - 1)
+
+int64_t orc_java_random_scramble(int64_t seed) { return (seed ^ JR_MULT) & JR_MASK; }
+
+static int32_t jr_next(int64_t* s, int bits) {
+    *s = (*s * JR_MULT + 0xBLL) & JR_MASK;
+    return (int32_t)((uint64_t)*s >> (48 - bits));
+}
+
+int64_t orc_java_random_next_long(int64_t* s) {
+    int64_t hi = (int64_t)jr_next(s, 32);
+    int64_t lo = (int64_t)jr_next(s, 32);
+    return (int64_t)((uint64_t)hi << 32) + lo;
+}
+
+void orc_java_random_bytes(int64_t seed, uint8_t* out, size_t n) {
+    int64_t s = orc_java_random_scramble(seed);
+    for (size_t i = 0; i < n;) {
+        int32_t rnd = jr_next(&s, 32);
+        size_t k = n - i < 4 ? n - i : 4;
+        for (; k-- > 0; rnd >>= 8) out[i++] = (uint8_t)rnd;
+    }
+}
+
+/* =====================================================================================
+ * Text-like generator (shared definition in include/netty_amd_textgen.h)
+ * ===================================================================================== */
+static nx_textgen_tables* g_tg = NULL;
+
+void orc_textgen_init(void) {
+    if (g_tg) return;
+    g_tg = (nx_textgen_tables*)malloc(sizeof(nx_textgen_tables));
+    nx_textgen_build(g_tg);
+}
+
+void orc_textgen_chunk(uint64_t chunk_index, uint8_t* out, size_t n) {
+    orc_textgen_init();
+    nx_tg_chunk(g_tg, chunk_index, out, n);
+}
+
+const uint8_t* orc_textgen_vocab(uint32_t* n_words, const uint32_t** offsets, const uint32_t** cdf) {
+    orc_textgen_init();
+    *n_words = NX_TG_WORDS;
+    *offsets = g_tg->off;
+    *cdf = g_tg->cdf;
+    return g_tg->chars;
+}

@@ -1,0 +1,88 @@
+/*
+ * netty_oracle.h — CPU restatement of Netty's codec-compression hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity oracle: only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it, and only as the checker / the CPU baseline.
+ * The product path (netty_amd/) never links or calls it.
+ *
+ * Pinned by the reference's own known-answer vectors (tests/test_oracle_kat.py); see
+ * oracle/netty_oracle.c for the file:line each function follows.
+ */
+#ifndef NETTY_ORACLE_H
+#define NETTY_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+#include "../include/netty_amd_status.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- CRC32C (Crc32c.java) + Snappy mask (Snappy.java:658-722) ---- */
+uint32_t orc_crc32c(const uint8_t* p, size_t n);
+uint32_t orc_crc32c_update(uint32_t state, const uint8_t* p, size_t n); /* raw state, init 0xFFFFFFFF */
+uint32_t orc_mask_checksum(uint32_t crc);
+uint32_t orc_snappy_checksum(const uint8_t* p, size_t n);
+
+/* ---- Snappy raw block (Snappy.java:82-393) ---- */
+size_t orc_snappy_max_compressed_length(size_t n);
+/* encode(in, out, length) with in.readerIndex()==0 (the framing encoder's readSlice). Returns bytes written. */
+size_t orc_snappy_encode(const uint8_t* in, int32_t length, uint8_t* out);
+/* One-shot decode of a complete chunk payload, as SnappyFrameDecoder drives Snappy.decode.
+ * out_cap = output ByteBuf max capacity (65536 in the frame decoder).
+ * Returns status (NX_OK or NX_ERR_*); *out_len = bytes produced (partial on silent truncation);
+ * *consumed = input bytes consumed by the state machine (differs from in_len on truncation). */
+int32_t orc_snappy_decode(const uint8_t* in, size_t in_len, uint8_t* out, size_t out_cap,
+                          size_t* out_len, size_t* consumed);
+/* Snappy.getPreamble: returns the varint (0 if incomplete), or NX_ERR_SNAPPY_PREAMBLE_TOO_LONG. */
+int64_t orc_snappy_get_preamble(const uint8_t* in, size_t in_len);
+
+/* ---- Snappy framing (SnappyFrameEncoder.java:79-152) ---- */
+size_t orc_snappy_frame_max_encoded(size_t n);
+/* One encode(ctx,in,out) call.  *started is the per-encoder 'started' flag. */
+size_t orc_snappy_frame_encode(const uint8_t* in, size_t n, int jumbo, int* started, uint8_t* out);
+
+/* ---- FastLZ (FastLz.java:96-557) ---- */
+/* compress(input, inOffset, inLength, output, outOffset, level).
+ * in points at the chunk start; readU16's readableBytes() quirk is expressed as
+ * u16_limit = readableBytes() - inOffset (relative to the chunk start; may be <= 0):
+ * readU16(o) returns only in[o] when o + 1 >= u16_limit.  Bytes in[inLength .. u16_limit)
+ * must be readable (they are the rest of the message). */
+int32_t orc_fastlz_compress(const uint8_t* in, int32_t in_len, uint8_t* out, int32_t level,
+                            int32_t u16_limit);
+/* decompress(input, inOffset, inLength, output, outOffset, outLength).  in_avail = readable bytes
+ * from the chunk start (>= in_len; reads beyond it raise NX_ERR_FASTLZ_INPUT_OOB). Returns the
+ * Java return value (>= 0, 0 on overflow/underflow) or a negative status. */
+int32_t orc_fastlz_decompress(const uint8_t* in, int32_t in_len, int32_t in_avail, uint8_t* out,
+                              int32_t out_len);
+uint32_t orc_adler32(const uint8_t* p, size_t n);
+/* FastLzFrameEncoder.encode over one message buffer; reader index r0, writer index r0+n.
+ * level 0/1/2; checksum 0/1 (Adler32).  Returns bytes written. */
+size_t orc_fastlz_frame_encode(const uint8_t* buf, size_t r0, size_t n, int level, int checksum,
+                               uint8_t* out);
+size_t orc_fastlz_frame_max_encoded(size_t n);
+
+/* ---- LZF (LzfEncoder/LzfDecoder framing; chunk codec restates the LZF format) ---- */
+/* Encode one chunk (<= 65535 bytes) to an LZF "ZV" block (compressed if it saves bytes). */
+size_t orc_lzf_encode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out);
+/* LZF compressed-chunk body decoder (ChunkDecoder.decodeChunk semantics). Returns NX_OK or
+ * NX_ERR_LZF_CORRUPT; writes exactly out_len bytes on success. */
+int32_t orc_lzf_decode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out, int32_t out_len);
+/* Raw LZF body compressor used by orc_lzf_encode_chunk; returns body length (may exceed in_len). */
+int32_t orc_lzf_compress_body(const uint8_t* in, int32_t in_len, uint8_t* out);
+size_t orc_lzf_frame_encode(const uint8_t* in, size_t n, int32_t compress_threshold, uint8_t* out);
+size_t orc_lzf_frame_max_encoded(size_t n);
+
+/* ---- Test data: java.util.Random restatement and the text-like generator ---- */
+void orc_java_random_bytes(int64_t seed, uint8_t* out, size_t n);
+int64_t orc_java_random_next_long(int64_t* state_seed); /* state already scrambled */
+int64_t orc_java_random_scramble(int64_t seed);
+/* Text-like chunk generator (BASELINE config 2/3); must equal the device generator. */
+void orc_textgen_init(void);
+void orc_textgen_chunk(uint64_t chunk_index, uint8_t* out, size_t n);
+const uint8_t* orc_textgen_vocab(uint32_t* n_words, const uint32_t** offsets, const uint32_t** cdf);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

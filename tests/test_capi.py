@@ -1,0 +1,60 @@
+"""CPU-side checks of the drop-in boundary: libnetty_amd.so loads and exports every entry point
+include/netty_amd.h declares (no compute calls: there is no GPU here)."""
+import os
+import re
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "netty_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b(nx_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    for must in ("nx_snappy_encode_batch", "nx_snappy_decode_batch", "nx_crc32c_masked_batch", "nx_fastlz_compress_batch",
+                 "nx_fastlz_decompress_batch", "nx_lzf_encode_batch", "nx_lzf_decode_batch",
+                 "nx_snappy_frame_encoder_encode", "nx_snappy_frame_decoder_decode"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from netty_amd import _lib
+    L = _lib.load()
+    missing = [n for n in _declared() if not hasattr(L, n)]
+    assert not missing, missing
+    # every ctypes signature in _lib.py is a declared symbol too
+    assert set(_lib.EXPORTED) <= set(_declared())
+
+
+def test_exports_are_c_abi_symbols():
+    so = os.path.join(ROOT, "netty_amd", "libnetty_amd.so")
+    out = subprocess.check_output(["nm", "-D", "--defined-only", so], text=True)
+    syms = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    for n in _declared():
+        assert n in syms, n  # unmangled extern "C"
+
+
+def test_host_only_calls_without_gpu():
+    from netty_amd import _lib
+    L = _lib.load()
+    assert L.nx_snappy_max_compressed_length(65536) == 32 + 65536 + 65536 // 6
+    assert _lib.status_string(-2) == "Offset is less than minimum permissible value"
+    assert b"gfx950" in L.nx_version()
+
+
+def test_product_has_no_oracle_dependency():
+    # the product package must never import or link the oracle (checker only)
+    pkg = os.path.join(ROOT, "netty_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".hpp", ".h")):
+                txt = open(os.path.join(dirpath, f), errors="ignore").read()
+                assert not re.search(r"^\s*(import|from)\s+oracle|pyoracle|#\s*include\s*[<\"].*oracle|liboracle", txt,
+                                     flags=re.M), f
+    out = subprocess.check_output(["ldd", os.path.join(pkg, "libnetty_amd.so")], text=True)
+    assert "oracle" not in out

@@ -1,0 +1,113 @@
+"""GPU parity of the FastLZ / LZF / Adler32 batch kernels vs the CPU oracle (config 4:
+mixed 4–64 KiB chunks, 50 % text-like / 50 % random)."""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def B():
+    from netty_amd import batch
+    return batch
+
+
+def _mixed(oracle, n, seed):
+    rng = random.Random(seed)
+    out = []
+    for i in range(n):
+        L = rng.randint(4096, 65535)
+        out.append(oracle.textgen_chunk(seed * 100000 + i, L) if i % 2 == 0 else oracle.java_random_bytes(i + seed, L))
+    out += [bytes(5), bytes(31), bytes(32), b"abc", b"", oracle.textgen_chunk(3, 100), bytes(70) + b"x" * 40]
+    return out
+
+
+@pytest.mark.parametrize("level", [1, 2])
+def test_fastlz_compress_parity(dev, B, oracle, level):
+    chunks = _mixed(oracle, 64, level)
+    rng = random.Random(level)
+    # u16 limits: standalone (= len), degenerate (<= 0), and partial
+    lims = [len(c) if i % 3 else (0 if i % 2 else max(len(c) // 2, 1)) for i, c in enumerate(chunks)]
+    inp, off, ln = B.pack(chunks, dev)
+    cap = [len(c) + len(c) // 16 + 96 for c in chunks]
+    out, ooff = B.out_slots(cap, dev)
+    lv = torch.full((len(chunks),), level, dtype=torch.int32, device=dev)
+    lim = torch.tensor(lims, dtype=torch.int32, device=dev)
+    olen, st = B.fastlz_compress(inp, off, ln, out, ooff, level=lv, u16_limit=lim)
+    torch.cuda.synchronize()
+    olen, st, oo, h = olen.cpu().tolist(), st.cpu().tolist(), ooff.cpu().tolist(), out.cpu().numpy().tobytes()
+    for i, c in enumerate(chunks):
+        assert st[i] == 0
+        want = oracle.fastlz_compress(c, level, u16_limit=lims[i])
+        assert h[oo[i]:oo[i] + olen[i]] == want, (i, len(c), lims[i])
+    _ = rng
+
+
+def test_fastlz_decompress_parity(dev, B, oracle):
+    chunks = _mixed(oracle, 64, 7)
+    comp = [oracle.fastlz_compress(c, 1 + (i % 2)) for i, c in enumerate(chunks)]
+    # corrupt a few: wrong level bits, truncated
+    comp.append(bytes([0x60]) + comp[0][1:])
+    comp.append(comp[2][: len(comp[2]) // 2])
+    olimits = [len(c) for c in chunks] + [len(chunks[0]), len(chunks[2])]
+    inp, off, ln = B.pack(comp, dev)
+    out, ooff = B.out_slots(olimits, dev)
+    lim = torch.tensor(olimits, dtype=torch.int32, device=dev)
+    res = B.fastlz_decompress(inp, off, ln, out, ooff, lim).cpu().tolist()
+    h, oo = out.cpu().numpy().tobytes(), ooff.cpu().tolist()
+    for i, c in enumerate(comp):
+        wr, wout = oracle.fastlz_decompress(c, olimits[i])
+        assert res[i] == wr, (i, res[i], wr)
+        if wr > 0:
+            assert h[oo[i]:oo[i] + wr] == wout
+
+
+def test_adler32_batch(dev, B, oracle):
+    import zlib
+    chunks = _mixed(oracle, 20, 3)
+    inp, off, ln = B.pack(chunks, dev, align=1)
+    got = [x & 0xFFFFFFFF for x in B.adler32(inp, off, ln).cpu().tolist()]
+    assert got == [zlib.adler32(c) for c in chunks]
+
+
+def test_lzf_encode_decode_parity(dev, B, oracle):
+    chunks = [c for c in _mixed(oracle, 64, 5)]
+    inp, off, ln = B.pack(chunks, dev)
+    cap = [len(c) + len(c) // 32 + 80 for c in chunks]
+    out, ooff = B.out_slots(cap, dev)
+    olen, st = B.lzf_encode(inp, off, ln, out, ooff)
+    torch.cuda.synchronize()
+    olen, oo, h = olen.cpu().tolist(), ooff.cpu().tolist(), out.cpu().numpy().tobytes()
+    blocks = []
+    for i, c in enumerate(chunks):
+        blk = h[oo[i]:oo[i] + olen[i]]
+        assert blk == oracle.lzf_encode_chunk(c), i
+        blocks.append(blk)
+    # decode the compressed bodies on the GPU
+    bodies, ulens, idx = [], [], []
+    for i, blk in enumerate(blocks):
+        if blk[2] == 1:
+            clen = int.from_bytes(blk[3:5], "big")
+            bodies.append(blk[7:7 + clen])
+            ulens.append(int.from_bytes(blk[5:7], "big"))
+            idx.append(i)
+    bodies.append(bytes([0x20, 0x05]))  # corrupt: reference before the output start
+    ulens.append(3)
+    inp2, off2, ln2 = B.pack(bodies, dev)
+    out2, ooff2 = B.out_slots(ulens, dev)
+    ul = torch.tensor(ulens, dtype=torch.int32, device=dev)
+    st2 = B.lzf_decode(inp2, off2, ln2, out2, ooff2, ul).cpu().tolist()
+    h2, oo2 = out2.cpu().numpy().tobytes(), ooff2.cpu().tolist()
+    for k, i in enumerate(idx):
+        assert st2[k] == 0
+        assert h2[oo2[k]:oo2[k] + ulens[k]] == chunks[i]
+    assert st2[-1] == -30

@@ -1,0 +1,196 @@
+"""GPU tests of the handler layer — the reference's own handler-level tests restated:
+SnappyFrameEncoderTest / SnappyFrameDecoderTest KATs, AbstractIntegrationTest round trips
+(EmbeddedChannel identity), FastLzIntegrationTest's random small writes, LZF round trips, and
+frame-level byte parity with the oracle's restatement of the Java encoders."""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def nx():
+    import netty_amd
+    return netty_amd
+
+
+def _corpus(oracle, kat):
+    rnd1m = oracle.java_random_bytes(42, 1 << 20)
+    part = bytearray(oracle.java_random_bytes(7, 10240))
+    part[:1024] = b"\x02" * 1024
+    comp = bytearray(10240)
+    r = oracle.java_random_bytes(9, 10240)
+    for i in range(0, 10240, 4):
+        comp[i] = r[i]
+    return {
+        "empty": b"", "one": b"A", "two": b"BA",
+        "regular": bytes.fromhex(kat["identity_inputs"]["regular"]),
+        "large_random": rnd1m, "part_random": bytes(part), "compressible": bytes(comp),
+        "long_blank": bytes(102400), "long_same": bytes([123]) * 102400,
+        "sequential": bytes(i & 0xFF for i in range(1024)),
+        "issue_1002": bytes.fromhex(kat["identity_inputs"]["issue_1002"]),
+        "text": oracle.textgen_chunk(5, 300000),
+    }
+
+
+def _identity(nx, enc, dec, data):
+    """AbstractIntegrationTest.testIdentity (AbstractIntegrationTest.java:160-189)."""
+    ech = nx.EmbeddedChannel(enc)
+    assert ech.write_outbound(data)
+    compressed = b""
+    while (m := ech.read_outbound()) is not None:
+        compressed += m
+    dch = nx.EmbeddedChannel(dec)
+    dch.write_inbound(compressed)
+    assert dec.readable_bytes() == 0  # assertFalse(compressed.isReadable())
+    out = b""
+    while (m := dch.read_inbound()) is not None:
+        out += m
+    assert out == data
+    return compressed
+
+
+def test_snappy_frame_encoder_kats(nx, kat):
+    for v in kat["snappy_frame_encode"]:
+        ch = nx.EmbeddedChannel(nx.SnappyFrameEncoder())
+        for m in v["msgs"]:
+            ch.write_outbound(bytes.fromhex(m))
+        got = b""
+        while (m := ch.read_outbound()) is not None:
+            got += m
+        assert got.hex() == v["out"], v["src"]
+
+
+def test_snappy_frame_decoder_kats(nx, kat):
+    for v in kat["snappy_frame_decode"]:
+        ch = nx.EmbeddedChannel(nx.SnappyFrameDecoder(v.get("validate", False)))
+        if v.get("error"):
+            with pytest.raises(nx.DecompressionException):
+                ch.write_inbound(bytes.fromhex(v["in"]))
+        else:
+            ch.write_inbound(bytes.fromhex(v["in"]))
+            got = []
+            while (m := ch.read_inbound()) is not None:
+                got.append(m.hex())
+            assert got == v["msgs"], v["src"]
+
+
+def test_snappy_decoder_corrupted_is_sticky(nx):
+    d = nx.SnappyFrameDecoder()
+    ch = nx.EmbeddedChannel(d)
+    with pytest.raises(nx.DecompressionException):
+        ch.write_inbound(bytes([0x03, 0x01, 0x00, 0x00, 0x00]))
+    # SnappyFrameDecoder.java:86-89: once corrupted, all input is skipped
+    assert not ch.write_inbound(bytes.fromhex("ff060000734e61507059010900006f982eb96e65747479"))
+
+
+@pytest.mark.parametrize("jumbo", [False, True])
+def test_snappy_identity_and_parity(nx, oracle, kat, jumbo):
+    for name, data in _corpus(oracle, kat).items():
+        comp = _identity(nx, nx.SnappyFrameEncoder(jumbo=jumbo), nx.SnappyFrameDecoder(), data)
+        want, _ = oracle.snappy_frame_encode(data, jumbo=jumbo)
+        assert comp == want, name
+        # and the validating decoder accepts it
+        d = nx.SnappyFrameDecoder(True)
+        assert b"".join(d.channel_read(comp)) == data
+
+
+def test_snappy_seeded_regressions(nx, oracle, kat):
+    # SnappyIntegrationTest.java:73-108 (16 MiB java.util.Random(seed).nextBytes)
+    for seed in kat["identity_inputs"]["snappy_seeds"]:
+        data = oracle.java_random_bytes(seed, 16 << 20)
+        comp = _identity(nx, nx.SnappyFrameEncoder(), nx.SnappyFrameDecoder(), data)
+        assert comp == oracle.snappy_frame_encode(data)[0]
+
+
+def test_snappy_streaming_partial_writes(nx, oracle):
+    # AbstractDecoderTest/FastLzIntegrationTest style: inbound bytes arrive in random small pieces
+    data = oracle.textgen_chunk(21, 200000)
+    comp = oracle.snappy_frame_encode(data)[0]
+    rng = random.Random(3)
+    for validate in (False, True):
+        d = nx.SnappyFrameDecoder(validate)
+        out, p = b"", 0
+        while p < len(comp):
+            k = rng.randint(1, 4000)
+            out += b"".join(d.channel_read(comp[p:p + k]))
+            p += k
+        assert out == data and d.readable_bytes() == 0
+
+
+def test_snappy_decoder_skippable_split(nx):
+    # RESERVED_SKIPPABLE whose body arrives in pieces (numBytesToSkip, SnappyFrameDecoder.java:91-99,137-150)
+    stream = bytes.fromhex("ff060000734e61507059") + bytes([0x80, 10, 0, 0]) + b"0123456789" + \
+        bytes.fromhex("010900006f982eb96e65747479")
+    d = nx.SnappyFrameDecoder(True)
+    got = []
+    for piece in (stream[:16], stream[16:20], stream[20:]):
+        got += d.channel_read(piece)
+    assert got == [b"netty"]
+
+
+@pytest.mark.parametrize("level,checksum", [(0, False), (1, False), (2, False), (0, True), (2, True)])
+def test_fastlz_identity(nx, oracle, kat, level, checksum):
+    for name, data in _corpus(oracle, kat).items():
+        comp = _identity(nx, nx.FastLzFrameEncoder(level, checksum), nx.FastLzFrameDecoder(checksum), data)
+        assert comp == oracle.fastlz_frame_encode(data, level=level, checksum=checksum), name
+
+
+def test_fastlz_reader_index_quirk_parity(nx, oracle):
+    # FastLz.readU16 uses readableBytes() of the message (FastLz.java:552-557): encode the same bytes
+    # at different reader indices and with multi-chunk messages; bytes must match the restatement.
+    data = oracle.textgen_chunk(8, 140000)
+    for r0 in (0, 1, 1000):
+        prefix = bytes(r0)
+        for level in (1, 2):
+            got = nx.FastLzFrameEncoder(level).encode(b"", reader_index=r0, buffer=prefix + data)
+            assert got == oracle.fastlz_frame_encode(data, level=level, r0=r0), (r0, level)
+
+
+def test_fastlz_random_small_writes(nx, oracle):
+    # FastLzIntegrationTest.java:64-113: encoder input and decoder input split into random pieces
+    rng = random.Random(11)
+    data = oracle.textgen_chunk(2, 50000)
+    enc = nx.FastLzFrameEncoder(0, True)
+    comp = b""
+    p = 0
+    while p < len(data):
+        k = rng.randint(1, 99)
+        comp += enc.encode(data[p:p + k])
+        p += k
+    dec = nx.FastLzFrameDecoder(True)
+    out, p = b"", 0
+    while p < len(comp):
+        k = rng.randint(1, 99)
+        out += b"".join(dec.channel_read(comp[p:p + k]))
+        p += k
+    assert out == data
+
+
+def test_fastlz_decoder_errors(nx, oracle):
+    with pytest.raises(nx.DecompressionException, match="unexpected block identifier"):
+        nx.FastLzFrameDecoder().channel_read(b"XYZ\x00\x00\x01a")
+    good = oracle.fastlz_frame_encode(oracle.textgen_chunk(1, 5000), level=1, checksum=True)
+    bad = bytearray(good)
+    bad[4] ^= 0xFF  # checksum byte
+    with pytest.raises(nx.DecompressionException, match="mismatching checksum"):
+        nx.FastLzFrameDecoder(True).channel_read(bytes(bad))
+    # the checksum is ignored by a decoder built without one (FastLzFrameDecoder.java:171)
+    assert b"".join(nx.FastLzFrameDecoder(False).channel_read(bytes(bad))) == oracle.textgen_chunk(1, 5000)
+
+
+@pytest.mark.parametrize("threshold", [16, 1000])
+def test_lzf_identity(nx, oracle, kat, threshold):
+    for name, data in _corpus(oracle, kat).items():
+        comp = _identity(nx, nx.LzfEncoder(threshold), nx.LzfDecoder(), data)
+        assert comp == oracle.lzf_frame_encode(data, threshold), name
+
+
+def test_lzf_decoder_errors(nx):
+    with pytest.raises(nx.DecompressionException, match="unexpected block identifier"):
+        nx.LzfDecoder().channel_read(b"AB\x00\x00\x01x")
+    with pytest.raises(nx.DecompressionException, match="unknown type of chunk"):
+        nx.LzfDecoder().channel_read(b"ZV\x07\x00\x01x")
+    with pytest.raises(nx.DecompressionException):
+        nx.LzfDecoder().channel_read(b"ZV\x01\x00\x02\x00\x05" + bytes([0x20, 0x05]))
