@@ -32,6 +32,7 @@ namespace nx {
 namespace dec {
 
 constexpr int kWaves = 8;                 // waves per workgroup
+constexpr int32_t kGuardTrip = -99;       // an internal loop bound tripped (never expected)
 constexpr int kTabBytes = (8 * 256 + 7 * 1024) * 4;  // CRC tables in LDS (36 KiB)
 
 __device__ __forceinline__ uint32_t shift_tab(const uint32_t* __restrict__ S, uint32_t c) {
@@ -150,7 +151,10 @@ __device__ void decode_frame(WaveLds<RING>& L, const uint8_t* __restrict__ src, 
     }
 
     bool stop = !go;
+    uint32_t windows = 0;
+    bool trip = false;
     while (!stop && W < in_len) {
+        if (++windows > in_len + 2) { st = kGuardTrip; break; }  // -99
         // ---------------- parse: speculative tag decode at W + lane
         const uint32_t p = W + lane;
         const uint32_t avail = p < in_len ? in_len - p : 0u;
@@ -218,7 +222,8 @@ __device__ void decode_frame(WaveLds<RING>& L, const uint8_t* __restrict__ src, 
         // ---------------- chain walk from lane 0 (scalar)
         uint64_t chain = 0;
         uint32_t t = 0, exitrel = 0;
-        for (;;) {
+        for (int guard = 0;; ++guard) {
+            if (guard > 64) { st = kGuardTrip + 1; stop = true; exitrel = 1; break; }
             if (W + t >= in_len) { exitrel = t; break; }
             chain |= 1ull << t;
             uint32_t n2 = (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)t);
@@ -274,7 +279,7 @@ __device__ void decode_frame(WaveLds<RING>& L, const uint8_t* __restrict__ src, 
         if (ntags) {
             int32_t jcur = -1;
             uint32_t S = O & ~63u;
-            for (; S < E; S += 64) {
+            for (; S < E && !trip; S += 64) {
                 if (lane == 0) L.bmask = 0ull;
                 const int32_t jj = jcur + 1 + lane;
                 if (jj < (int32_t)ntags) {
@@ -306,7 +311,8 @@ __device__ void decode_frame(WaveLds<RING>& L, const uint8_t* __restrict__ src, 
                         }
                     }
                 }
-                while (__any(!res)) {
+                for (int guard = 0; __any(!res); ++guard) {
+                    if (guard > 64) { st = kGuardTrip + 2; stop = trip = true; break; }
                     const uint32_t v2 = (uint32_t)__shfl((int)v, (int)sl);
                     const int r2 = __shfl((int)res, (int)sl);
                     const uint32_t sl2 = (uint32_t)__shfl((int)sl, (int)sl);
@@ -321,7 +327,8 @@ __device__ void decode_frame(WaveLds<RING>& L, const uint8_t* __restrict__ src, 
                 }
                 if (act) L.ring[pp & (RING - 1)] = (uint8_t)v;
                 const uint32_t front = (S + 64u < E) ? S + 64u : E;
-                while (front - flushed >= 1024u) {
+                for (int guard = 0; front >= flushed + 1024u; ++guard) {
+                    if (guard > 64) { st = kGuardTrip + 3; stop = trip = true; break; }
                     crc = flush_block<RING>(L, dst, flushed, dst16, sT, sSH, crc, do_crc, lane);
                     flushed += 1024u;
                 }
@@ -369,7 +376,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_snappy_decode(const uint8_t* __
                                                                uint32_t* __restrict__ out_len, uint32_t* __restrict__ consumed,
                                                                int32_t* __restrict__ status, const uint32_t* __restrict__ expect,
                                                                uint32_t* __restrict__ crc_out, uint32_t n, uint32_t* __restrict__ ticket,
-                                                               const CrcTables* __restrict__ tabs) {
+                                                               const CrcTables* __restrict__ tabs, int dbg_mode) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* sT = reinterpret_cast<uint32_t*>(smem);
     uint32_t* sSH = sT + 8 * 256;
@@ -381,14 +388,19 @@ __global__ void __launch_bounds__(kWaves * 64) k_snappy_decode(const uint8_t* __
         for (int i = threadIdx.x; i < 7 * 1024; i += blockDim.x) sSH[i] = gS[i];
     }
     __syncthreads();
+    if (dbg_mode == 1) return;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     WaveLds<RING>& L = *reinterpret_cast<WaveLds<RING>*>(smem + kTabBytes + wave * sizeof(WaveLds<RING>));
-    for (;;) {
-        uint32_t c = 0;
-        if (lane == 0) c = atomicAdd(ticket, 1u);
-        c = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)c, 0));
-        if (c >= n) break;
+    // static wave -> frame assignment (interleaved so that neighbouring waves take neighbouring frames)
+    const uint32_t gw = blockIdx.x * kWaves + (uint32_t)wave;
+    const uint32_t nw = gridDim.x * kWaves;
+    (void)ticket;
+    for (uint32_t c = gw; c < n; c += nw) {
+        if (dbg_mode == 2) {
+            if (lane == 0) status[c] = 7;
+            continue;
+        }
         const uint32_t cap = out_cap ? out_cap[c] : 65536u;
         decode_frame<RING>(L, in + in_off[c], in_len[c], out + out_off[c], cap, sT, sSH, do_crc, expect ? expect[c] : 0u,
                            expect != nullptr, &out_len[c], consumed ? &consumed[c] : nullptr, &status[c],
@@ -400,11 +412,34 @@ __global__ void __launch_bounds__(kWaves * 64) k_snappy_decode(const uint8_t* __
 }  // namespace nx
 
 #include <mutex>
+#include <stdlib.h>
 namespace {
 std::mutex g_tk_mu;
 uint32_t* g_ticket = nullptr;
 int g_ticket_dev = -1;
 constexpr int kRing = 4096;
+template <int R>
+int32_t launch_decode(int dbg, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                      const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len, uint32_t* consumed, int32_t* status,
+                      const uint32_t* expected_masked_crc, uint32_t* crc_out, uint32_t n, hipStream_t stream, int cus) {
+    using namespace nx::dec;
+    const size_t lds = kTabBytes + kWaves * sizeof(WaveLds<R>);
+    static bool attr_done = false;
+    if (!attr_done) {
+        NX_HIP_CHECK(hipFuncSetAttribute((const void*)k_snappy_decode<R>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_done = true;
+    }
+    NX_HIP_CHECK(hipMemsetAsync(g_ticket, 0, 16, stream));
+    unsigned blocks_per_cu = (unsigned)(160 * 1024 / lds);
+    if (blocks_per_cu < 1) blocks_per_cu = 1;
+    uint64_t want = (uint64_t)cus * blocks_per_cu;
+    uint64_t need = (n + kWaves - 1) / kWaves;
+    unsigned grid = (unsigned)(need < want ? need : want);
+    hipLaunchKernelGGL(k_snappy_decode<R>, dim3(grid), dim3(kWaves * 64), lds, stream, in, in_off, in_len, out, out_off, out_cap,
+                       out_len, consumed, status, expected_masked_crc, crc_out, n, g_ticket, nx::crc_tables_dev(), dbg);
+    NX_HIP_CHECK(hipGetLastError());
+    return NX_OK;
+}
 }  // namespace
 
 extern "C" int32_t nx_snappy_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
@@ -418,29 +453,17 @@ extern "C" int32_t nx_snappy_decode_batch(const uint8_t* in, const uint64_t* in_
     int dev = 0, cus = 256;
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const size_t lds = kTabBytes + kWaves * sizeof(WaveLds<kRing>);
     {
         std::lock_guard<std::mutex> lk(g_tk_mu);
         if (!g_ticket || g_ticket_dev != dev) {
             NX_HIP_CHECK(hipMalloc(&g_ticket, 256 * sizeof(uint32_t)));
             g_ticket_dev = dev;
-            static bool attr_done = false;
-            if (!attr_done) {
-                NX_HIP_CHECK(hipFuncSetAttribute((const void*)k_snappy_decode<kRing>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)lds));
-                attr_done = true;
-            }
         }
     }
-    NX_HIP_CHECK(hipMemsetAsync(g_ticket, 0, 16, (hipStream_t)stream));
-    unsigned blocks_per_cu = (unsigned)(160 * 1024 / lds);
-    if (blocks_per_cu < 1) blocks_per_cu = 1;
-    uint64_t want = (uint64_t)cus * blocks_per_cu;
-    uint64_t need = (n + kWaves - 1) / kWaves;
-    unsigned grid = (unsigned)(need < want ? need : want);
-    hipLaunchKernelGGL(k_snappy_decode<kRing>, dim3(grid), dim3(kWaves * 64), lds, (hipStream_t)stream, in, in_off, in_len, out,
-                       out_off, out_cap, out_len, consumed, status, expected_masked_crc, crc_out, n, g_ticket,
-                       nx::crc_tables_dev());
-    NX_HIP_CHECK(hipGetLastError());
-    return NX_OK;
+    static const int dbg = getenv("NX_DEC_DEBUG") ? atoi(getenv("NX_DEC_DEBUG")) : 0;
+    if (dbg == 3)
+        return launch_decode<1024>(0, in, in_off, in_len, out, out_off, out_cap, out_len, consumed, status, expected_masked_crc,
+                                   crc_out, n, (hipStream_t)stream, cus);
+    return launch_decode<kRing>(dbg, in, in_off, in_len, out, out_off, out_cap, out_len, consumed, status, expected_masked_crc,
+                                crc_out, n, (hipStream_t)stream, cus);
 }

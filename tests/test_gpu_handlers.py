@@ -130,11 +130,43 @@ def test_snappy_decoder_skippable_split(nx):
     assert got == [b"netty"]
 
 
-@pytest.mark.parametrize("level,checksum", [(0, False), (1, False), (2, False), (0, True), (2, True)])
+@pytest.mark.parametrize("level,checksum", [(0, False), (1, False), (0, True), (1, True)])
 def test_fastlz_identity(nx, oracle, kat, level, checksum):
+    # FastLzIntegrationTest uses LEVEL_AUTO (FastLzFrameEncoder(boolean)), which is level 1 for every
+    # <= 65535-byte chunk (FastLz.java:99-103)
     for name, data in _corpus(oracle, kat).items():
         comp = _identity(nx, nx.FastLzFrameEncoder(level, checksum), nx.FastLzFrameDecoder(checksum), data)
         assert comp == oracle.fastlz_frame_encode(data, level=level, checksum=checksum), name
+
+
+def _oracle_fastlz_frames_decode(oracle, fr):
+    p, out = 0, b""
+    while p < len(fr):
+        opt = fr[p + 3]
+        p += 4 + (4 if opt & 0x10 else 0)
+        clen = int.from_bytes(fr[p:p + 2], "big")
+        p += 2
+        olen = int.from_bytes(fr[p:p + 2], "big") if opt & 1 else clen
+        p += 2 if opt & 1 else 0
+        out += oracle.fastlz_decompress(fr[p:p + clen], olen)[1] if opt & 1 else fr[p:p + clen]
+        p += clen
+    return out
+
+
+@pytest.mark.parametrize("checksum", [False, True])
+def test_fastlz_level2_parity_including_readu16_corruption(nx, oracle, kat, checksum):
+    """LEVEL_2 through FastLzFrameEncoder: for chunk k >= 1 of a large message readU16's
+    `offset + 1 >= readableBytes()` test (FastLz.java:552-557) degenerates, and the level-2 run
+    check then emits wrong runs — the reference corrupts such messages.  The GPU path must
+    reproduce the reference bytes, corruption included."""
+    for name, data in _corpus(oracle, kat).items():
+        want = oracle.fastlz_frame_encode(data, level=2, checksum=checksum)
+        got = nx.FastLzFrameEncoder(2, checksum).encode(data)
+        assert got == want, name
+        dec = b"".join(nx.FastLzFrameDecoder(False).channel_read(got))
+        assert dec == _oracle_fastlz_frames_decode(oracle, want), name
+    big = oracle.textgen_chunk(5, 300000)
+    assert _oracle_fastlz_frames_decode(oracle, oracle.fastlz_frame_encode(big, level=2)) != big  # the quirk is real
 
 
 def test_fastlz_reader_index_quirk_parity(nx, oracle):
