@@ -16,7 +16,8 @@
 //   tags   — the current window's tag list.
 // Steps per window (64 bytes of compressed stream that start at a tag):
 //   parse   — lane l speculatively decodes "a tag at W+l" (2 ds_read_b32 + funnel shift); the real
-//             tag chain is walked from lane 0 with v_readlane → a 64-bit tag mask;
+//             tag chain is found by pointer doubling over ds_bpermute, which also compacts it
+//             (lane m = m-th tag);
 //   order   — the Java checks (NOT_ENOUGH_INPUT → silent stop, validateOffset, buffer capacity) run
 //             per tag with bytes-written-so-far from a wave prefix sum; the first failing tag in
 //             stream order decides, exactly as the serial state machine;
@@ -37,7 +38,7 @@
 namespace nx {
 namespace dec {
 
-constexpr int kWaves = 10;        // waves per workgroup (2 workgroups per CU → 20 waves/CU at <= 96 VGPRs)
+constexpr int kWaves = 12;        // waves per workgroup (2 workgroups per CU → 24 waves/CU at <= 80 VGPRs)
 constexpr int kRing = 4096;       // decoded-output history per wave
 constexpr int kStage = 1024;      // compressed-input ring per wave
 constexpr int kFB = 512;          // flush block (64 lanes x 8 B)
@@ -252,67 +253,78 @@ __device__ void decode_frame(WaveLds& L, const Frame& f, const uint32_t* __restr
             if (off64 == 0) err = NX_ERR_SNAPPY_OFFSET_ZERO;
             else if (off64 < 0) err = NX_ERR_SNAPPY_OFFSET_NEGATIVE;
         }
-        const uint32_t nxt = (uint32_t)lane + size;
+        const uint32_t nxt = (uint32_t)lane + size;  // relative position of the following tag
 
-        // ---------------- chain walk from lane 0 (scalar unit)
-        uint64_t chain = 0;
-        uint32_t t = 0, exitrel = 0;
-        for (int guard = 0;; ++guard) {
-            if (guard > 64) {
-                st = kGuardTrip + 1;
-                stop = true;
-                exitrel = 1;
-                break;
-            }
-            if (W + t >= in_len) {
-                exitrel = t;
-                break;
-            }
-            chain |= 1ull << t;
-            const uint32_t n2 = uni((uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)t));
-            if (n2 >= 64u) {
-                exitrel = n2;
-                break;
-            }
-            t = n2;
+        // ---------------- tag chain by pointer doubling (no scalar walk)
+        // J0[l] = next tag position if a tag starts at l (64 = leaves the window); positions at or
+        // past the end of the input are fixed points.  Jk = J0^(2^k); lane m then composes the Jk
+        // selected by the bits of m, so lane m ends on the position of the m-th tag: the chain comes
+        // out compacted (lanes 0..T-1 = tags in stream order).
+        const uint32_t lim = uni((in_len - W) < 64u ? (in_len - W) : 64u);
+        uint32_t Jk[6];
+        Jk[0] = (uint32_t)lane >= lim ? (uint32_t)lane : (nxt < 64u ? nxt : 64u);
+#pragma unroll
+        for (int k = 1; k < 6; ++k) {
+            const uint32_t prev = Jk[k - 1];
+            const uint32_t g = (uint32_t)__shfl((int)prev, (int)(prev & 63u));
+            Jk[k] = prev >= 64u ? 64u : g;
         }
-        const bool is_tag = (chain >> lane) & 1ull;
+        uint32_t pos = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t g = (uint32_t)__shfl((int)Jk[k], (int)(pos & 63u));
+            if (((uint32_t)lane >> k) & 1u) pos = pos >= 64u ? 64u : g;
+        }
+        const bool tv = pos < lim;  // lane m holds tag m
+        const uint32_t T = (uint32_t)__popcll(__ballot(tv));
+        // gather tag m's fields from lane pos
+        const uint32_t src_l = (uint32_t)(pos & 63u);
+        const uint32_t flags = (is_copy ? 1u : 0u) | (nei ? 2u : 0u) | ((uint32_t)(-err) << 8);
+        const uint32_t xv = is_copy ? (off64 > 0x7FFFFFFFll ? 0x7FFFFFFFu : (uint32_t)(off64 < 0 ? 0 : off64)) : x;
+        const uint32_t m_olen = (uint32_t)__shfl((int)olen, (int)src_l);
+        const uint32_t m_flags = (uint32_t)__shfl((int)flags, (int)src_l);
+        const uint32_t m_x = (uint32_t)__shfl((int)xv, (int)src_l);
+        const bool m_copy = (m_flags & 1u) != 0;
+        const bool m_nei = (m_flags & 2u) != 0;
+        int32_t m_err = -(int32_t)(m_flags >> 8);
+        // the window's exit: the position after the last tag
+        const uint32_t lastpos = uni((uint32_t)__builtin_amdgcn_readlane((int)pos, (int)(T - 1)));
+        const uint32_t exitrel = uni((uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)lastpos));
 
-        // ---------------- ordering: bytes written before each tag, per-tag checks
-        const uint32_t mylen = is_tag ? olen : 0u;
+        // ---------------- ordering: bytes written before each tag, per-tag checks (stream order = lane order)
+        const uint32_t mylen = tv ? m_olen : 0u;
         const uint32_t ostart = O + excl_scan(mylen, lane);
-        if (is_tag && is_copy && !nei && err == 0 && (uint64_t)off64 > ostart) err = NX_ERR_SNAPPY_OFFSET_BEYOND;
-        if (is_tag && !nei && err == 0 && (uint64_t)ostart + olen > cap) err = NX_ERR_SNAPPY_OUTPUT_OVERFLOW;
-        const uint64_t badm = __ballot(is_tag && (nei || err != 0));
-        uint64_t valid = chain;
+        if (tv && m_copy && !m_nei && m_err == 0 && m_x > ostart) m_err = NX_ERR_SNAPPY_OFFSET_BEYOND;
+        if (tv && !m_nei && m_err == 0 && (uint64_t)ostart + m_olen > cap) m_err = NX_ERR_SNAPPY_OUTPUT_OVERFLOW;
+        const uint64_t badm = __ballot(tv && (m_nei || m_err != 0));
+        uint32_t nv = T;  // tags that execute
         const uint32_t Wnext = uni(W + exitrel);
         if (badm) {
-            const int fb = __ffsll((long long)badm) - 1;
-            valid = chain & ((1ull << fb) - 1ull);
-            const int32_t e = __shfl(err, fb);
-            const uint32_t pf0 = W + (uint32_t)fb;
+            const uint32_t fb = (uint32_t)(__ffsll((long long)badm) - 1);
+            nv = fb;
+            const int32_t e = __builtin_amdgcn_readlane(m_err, (int)fb);
+            const uint32_t fpos = uni((uint32_t)__builtin_amdgcn_readlane((int)pos, (int)fb));
             if (e != 0) {
                 st = e;
-                consumed = pf0 + (uint32_t)__shfl((int)size, fb);
+                consumed = W + uni((uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)fpos));
             } else {
-                consumed = pf0 + 1;  // NOT_ENOUGH_INPUT: tag byte consumed, operands left unread
+                consumed = W + fpos + 1;  // NOT_ENOUGH_INPUT: tag byte consumed, operands left unread
             }
             stop = true;
         } else {
             consumed = Wnext < in_len ? Wnext : in_len;
         }
-        const bool vt = (valid >> lane) & 1ull;
-        const uint64_t outm = __ballot(vt && olen > 0);
+        const bool mine = (uint32_t)lane < nv && m_olen > 0;  // an output-producing tag
+        const uint64_t outm = __ballot(mine);
         const uint32_t ntags = (uint32_t)__popcll(outm);
         uint32_t E = O;
         if (ntags) {
-            const int lastl = 63 - __clzll((long long)outm);
-            E = uni((uint32_t)__shfl((int)(ostart + olen), lastl));
-            if ((outm >> lane) & 1ull) {
+            E = uni((uint32_t)__builtin_amdgcn_readlane((int)(ostart + mylen), (int)(nv - 1)));
+            if (mine) {
                 const uint32_t idx = (uint32_t)__popcll(outm & ((1ull << lane) - 1ull));
                 Tag tg;
                 tg.start = ostart;
-                tg.x = is_copy ? (0x80000000u | (uint32_t)off64) : x;
+                tg.x = m_copy ? (0x80000000u | m_x) : m_x;
                 L.tags[idx] = tg;
             }
         }
@@ -322,11 +334,7 @@ __device__ void decode_frame(WaveLds& L, const Frame& f, const uint32_t* __restr
             const uint32_t s_lo = sbase, s_hi = sbase + (uint32_t)kStage;  // stage window (aligned coords)
             for (uint32_t S = O & ~63u; S < E && !trip; S += 64) {
                 if (lane == 0) L.bmask = 0ull;
-                const int32_t jj = jcur + 1 + lane;
-                if (jj < (int32_t)ntags) {
-                    const uint32_t s = L.tags[jj].start;
-                    if (s < S + 64u) atomicOr(&L.bmask, 1ull << (s - S));
-                }
+                if (mine && ostart >= S && ostart < S + 64u) atomicOr(&L.bmask, 1ull << (ostart - S));
                 const uint64_t B = L.bmask;
                 const uint32_t pp = S + lane;
                 const bool act = pp >= O && pp < E;
@@ -438,7 +446,7 @@ __device__ void decode_frame(WaveLds& L, const Frame& f, const uint32_t* __restr
     }
 }
 
-__global__ void __launch_bounds__(kWaves * 64, 5) k_snappy_decode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+__global__ void __launch_bounds__(kWaves * 64, 6) k_snappy_decode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                                const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                                const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                                                                uint32_t* __restrict__ out_len, uint32_t* __restrict__ consumed,

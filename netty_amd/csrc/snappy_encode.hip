@@ -1,0 +1,309 @@
+// snappy_encode.hip — Snappy block encoder, bit-exact with Netty's Snappy.encode (Snappy.java:82-313).
+//
+// Netty's greedy matcher is a serial state machine whose output depends on the exact probe order
+// (the `skip++ >> 5` heuristic, :107-115) and on an evolving 16384-entry hash table (:97-100,
+// 126-128, 148-152).  There is no safe intra-chunk speculation, so each chunk is one lane's serial
+// state machine and the parallelism is the thousands of independent chunks of a batch (16 waves
+// per CU → 262 144 chunks in flight on 256 CUs).  What the kernel optimises is the memory side of
+// each lane's dependency chain:
+//   * every 4-byte window is one unaligned dword load (Java's big-endian getInt = bswap), and the
+//     bytes at the probe position are reused from the hash computation that loaded them;
+//   * the next probe's table load is issued before the current candidate compare resolves
+//     (a same-hash collision is forwarded in registers), so a probe costs one memory round trip;
+//   * match extension compares 4 bytes per step and finds the first mismatch with ctz;
+//   * output bytes are packed into dwords and written with aligned 4-byte stores; literal runs
+//     are copied 4 bytes at a time with a funnel shift.
+// Hash table: Java allocates a zeroed short[min(nextPow2(len),16384)] per call (:97-99,191).
+// Each resident lane owns a 16384-entry uint32 slot in a device workspace; an entry is
+// (stamp << 16) | position, and a stamp mismatch reads as 0 — exactly a freshly zeroed table,
+// without a 32 KiB clear per chunk.
+#include <stdlib.h>
+#include <mutex>
+#include "nx_common.hpp"
+
+namespace nx {
+namespace enc {
+
+typedef uint32_t __attribute__((aligned(1))) u32u;
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const u32u*>(p); }  // LE, unaligned
+__device__ __forceinline__ uint32_t hash_of(uint32_t le, int shift) {
+    return (__builtin_bswap32(le) * 0x1e35a7bdu) >> shift;  // hash (:177-179) on the BIG-endian getInt
+}
+
+// Output writer: bytes are packed into `acc` and leave as aligned dword stores.
+struct Writer {
+    uint32_t* w;   // next aligned dword to store
+    uint32_t acc;  // pending bytes (little-endian order)
+    uint32_t na;   // number of pending bytes (0..3)
+    uint32_t nw;   // dwords stored
+    __device__ __forceinline__ void put(uint32_t b) {
+        acc |= b << (8 * na);
+        if (++na == 4) {
+            w[nw++] = acc;
+            acc = 0;
+            na = 0;
+        }
+    }
+    // append `n` bytes starting at p (unaligned source)
+    __device__ __forceinline__ void copy(const uint8_t* p, int32_t n) {
+        while (n >= 4) {
+            const uint32_t v = ld32(p);
+            if (na == 0) {
+                w[nw++] = v;
+            } else {
+                w[nw++] = acc | (v << (8 * na));
+                acc = v >> (32 - 8 * na);
+            }
+            p += 4;
+            n -= 4;
+        }
+        while (n-- > 0) put(*p++);
+    }
+    __device__ __forceinline__ uint32_t pos() const { return nw * 4 + na; }
+    __device__ __forceinline__ void finish() {
+        uint8_t* t = reinterpret_cast<uint8_t*>(w + nw);
+        for (uint32_t i = 0; i < na; ++i) t[i] = (uint8_t)(acc >> (8 * i));
+    }
+};
+
+// Byte-store writer for unaligned destinations (same interface).
+struct ByteWriter {
+    uint8_t* o;
+    uint32_t n;
+    __device__ __forceinline__ void put(uint32_t b) { o[n++] = (uint8_t)b; }
+    __device__ __forceinline__ void copy(const uint8_t* p, int32_t k) {
+        for (int32_t i = 0; i < k; ++i) o[n + i] = p[i];
+        n += (uint32_t)k;
+    }
+    __device__ __forceinline__ uint32_t pos() const { return n; }
+    __device__ __forceinline__ void finish() {}
+};
+
+template <class Wr>
+__device__ __forceinline__ void enc_literal(const uint8_t* in, Wr& w, int32_t length) {
+    // encodeLiteral (:268-281)
+    if (length < 61) {
+        w.put((uint32_t)((length - 1) << 2));
+    } else {
+        const int32_t v = length - 1;
+        const int bitLength = 31 - __clz((uint32_t)v);  // bitsToEncode (:249-257), v >= 60
+        const int bytesToEncode = 1 + bitLength / 8;
+        w.put((uint32_t)((59 + bytesToEncode) << 2));
+        for (int i = 0; i < bytesToEncode; i++) w.put((uint32_t)((v >> (i * 8)) & 0xff));
+    }
+    w.copy(in, length);
+}
+
+template <class Wr>
+__device__ __forceinline__ void enc_copy_off(Wr& w, int32_t offset, int32_t length) {
+    // encodeCopyWithOffset (:283-292)
+    if (length < 12 && offset < 2048) {
+        w.put((uint32_t)(1 | ((length - 4) << 2) | ((offset >> 8) << 5)));
+        w.put((uint32_t)(offset & 0xff));
+    } else {
+        w.put((uint32_t)(2 | ((length - 1) << 2)));
+        w.put((uint32_t)(offset & 0xff));
+        w.put((uint32_t)((offset >> 8) & 0xff));
+    }
+}
+
+template <class Wr>
+__device__ __forceinline__ void enc_copy(Wr& w, int32_t offset, int32_t length) {
+    // encodeCopy (:301-313)
+    while (length >= 68) {
+        enc_copy_off(w, offset, 64);
+        length -= 64;
+    }
+    if (length > 64) {
+        enc_copy_off(w, offset, 60);
+        length -= 60;
+    }
+    enc_copy_off(w, offset, length);
+}
+
+// 4 + findMatchingLength(in, candidate + 4, inIndex + 4, length)  (:224-239): the common-prefix
+// length bounded by the bytes left, computed 4 bytes per step.
+__device__ __forceinline__ int32_t match_len(const uint8_t* in, int32_t a, int32_t b, int32_t length) {
+    int32_t m = 0;
+    while (b + m <= length - 4) {
+        const uint32_t x = ld32(in + a + m) ^ ld32(in + b + m);
+        if (x) return m + (int32_t)(__builtin_ctz(x) >> 3);
+        m += 4;
+    }
+    while (b + m < length && in[a + m] == in[b + m]) ++m;
+    return m;
+}
+
+template <class Wr>
+__device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length, Wr& w, uint32_t* __restrict__ table, uint32_t stamp) {
+    for (int i = 0;; i++) {  // preamble (:84-92)
+        const uint32_t b = (uint32_t)length >> (i * 7);
+        if ((b & 0xFFFFFF80u) != 0) {
+            w.put((b & 0x7f) | 0x80);
+        } else {
+            w.put(b);
+            break;
+        }
+    }
+    uint32_t hts = length <= 1 ? 1u : (1u << (32 - __clz((uint32_t)(length - 1))));
+    if (hts > 16384u) hts = 16384u;
+    const int shift = __clz(hts) + 1;
+    const uint32_t stag = stamp << 16;
+#define TBL_DEC(e) ((((e) & 0xFFFF0000u) == stag) ? (int32_t)((e) & 0xFFFFu) : 0)
+    int32_t nextEmit = 0;
+    if (length >= 15) {  // MIN_COMPRESSIBLE_BYTES (:34,104)
+        int32_t inIndex = 1;
+        uint32_t nextWord = ld32(in + 1);
+        uint32_t nextHash = hash_of(nextWord, shift);
+        for (;;) {  // outer: (:106)
+            // ---- probe run (:107-130), software-pipelined by one probe
+            int32_t skip = 32;
+            int32_t nextIndex = inIndex;
+            int32_t candidate;
+            uint32_t curWord;
+            // first probe of the run
+            inIndex = nextIndex;
+            uint32_t hash = nextHash;
+            curWord = nextWord;
+            nextIndex = inIndex + (skip++ >> 5);
+            if (nextIndex > length - 4) goto done;
+            nextWord = ld32(in + nextIndex);
+            nextHash = hash_of(nextWord, shift);
+            candidate = TBL_DEC(table[hash]);
+            table[hash] = stag | (uint32_t)inIndex;
+            for (;;) {
+                // speculative: the next probe's position, bytes and table entry
+                const int32_t pIndex = nextIndex;
+                const uint32_t pHash = nextHash;
+                const uint32_t pWord = nextWord;
+                const int32_t pNext = pIndex + (skip >> 5);
+                const bool pValid = pNext <= length - 4;
+                uint32_t pEntry = 0, pNextWord = 0;
+                if (pValid) {
+                    pEntry = table[pHash];
+                    pNextWord = ld32(in + pNext);
+                }
+                const uint32_t candWord = ld32(in + candidate);
+                if (curWord == candWord) break;  // match at inIndex
+                // advance to the next probe (:111-128)
+                skip++;
+                inIndex = pIndex;
+                hash = pHash;
+                curWord = pWord;
+                nextIndex = pNext;
+                if (!pValid) goto done;
+                nextWord = pNextWord;
+                nextHash = hash_of(pNextWord, shift);
+                candidate = TBL_DEC(pEntry);
+                table[hash] = stag | (uint32_t)inIndex;
+            }
+
+            enc_literal(in + nextEmit, w, inIndex - nextEmit);  // (:132)
+
+            int32_t insertTail;
+            for (;;) {  // (:135-154)
+                const int32_t base = inIndex;
+                const int32_t matched = 4 + match_len(in, candidate + 4, inIndex + 4, length);
+                inIndex += matched;
+                enc_copy(w, base - candidate, matched);
+                insertTail = inIndex - 1;
+                nextEmit = inIndex;
+                if (inIndex >= length - 4) goto done;
+                const uint32_t wTail = ld32(in + insertTail);
+                const uint32_t wCur = ld32(in + inIndex);
+                const uint32_t prevHash = hash_of(wTail, shift);
+                table[prevHash] = stag | (uint32_t)(inIndex - 1);
+                const uint32_t currentHash = hash_of(wCur, shift);
+                candidate = TBL_DEC(table[currentHash]);
+                table[currentHash] = stag | (uint32_t)inIndex;
+                if (wCur != ld32(in + candidate)) break;
+            }
+            nextWord = ld32(in + insertTail + 2);
+            nextHash = hash_of(nextWord, shift);  // (:156)
+            ++inIndex;
+        }
+    }
+done:
+#undef TBL_DEC
+    if (nextEmit < length) enc_literal(in + nextEmit, w, length - nextEmit);  // (:162-164)
+    w.finish();
+    return w.pos();
+}
+
+__global__ void __launch_bounds__(256) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                       const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                       const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
+                                                       int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
+                                                       uint32_t stamp_base) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    uint32_t* table = workspace + (size_t)tid * 16384u;
+    uint32_t iter = 0;
+    for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
+        const uint32_t len = in_len[c];
+        if (len > 65536u) {
+            status[c] = NX_ERR_INVALID_ARG;
+            out_len[c] = 0;
+            continue;
+        }
+        const uint32_t stamp = ((stamp_base + iter) % 65535u) + 1u;
+        uint8_t* o = out + out_off[c];
+        uint32_t olen;
+        if ((((uintptr_t)o) & 3u) == 0) {
+            Writer w{reinterpret_cast<uint32_t*>(o), 0, 0, 0};
+            olen = encode_chunk(in + in_off[c], (int32_t)len, w, table, stamp);
+        } else {
+            ByteWriter w{o, 0};
+            olen = encode_chunk(in + in_off[c], (int32_t)len, w, table, stamp);
+        }
+        out_len[c] = olen;
+        status[c] = NX_OK;
+    }
+}
+
+}  // namespace enc
+}  // namespace nx
+
+namespace {
+std::mutex g_ws_mu;
+uint32_t* g_ws = nullptr;
+size_t g_ws_threads = 0;
+uint32_t g_stamp = 0;
+int g_ws_dev = -1;
+constexpr unsigned kEncBlock = 256;
+constexpr unsigned kEncWavesPerCU = 16;
+}  // namespace
+
+extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                          const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream) {
+    if (n == 0) return NX_OK;
+    if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
+    int dev = 0, cus = 256;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    static const unsigned waves_per_cu = getenv("NX_ENC_WAVES") ? (unsigned)atoi(getenv("NX_ENC_WAVES")) : kEncWavesPerCU;
+    const size_t want = (size_t)cus * waves_per_cu * 64;
+    const size_t threads = n < want ? ((n + kEncBlock - 1) / kEncBlock) * kEncBlock : want;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    const size_t per = 16384u * sizeof(uint32_t);
+    if (g_ws == nullptr || g_ws_threads < threads || g_ws_dev != dev) {
+        if (g_ws) (void)hipFree(g_ws);
+        g_ws = nullptr;
+        NX_HIP_CHECK(hipMalloc(&g_ws, threads * per));
+        NX_HIP_CHECK(hipMemsetAsync(g_ws, 0, threads * per, (hipStream_t)stream));
+        g_ws_threads = threads;
+        g_ws_dev = dev;
+        g_stamp = 0;
+    }
+    const uint32_t iters = (uint32_t)((n + threads - 1) / threads);
+    if ((uint64_t)g_stamp + iters >= 65535u) {
+        NX_HIP_CHECK(hipMemsetAsync(g_ws, 0, g_ws_threads * per, (hipStream_t)stream));
+        g_stamp = 0;
+    }
+    hipLaunchKernelGGL(nx::enc::k_snappy_encode, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, (hipStream_t)stream, in,
+                       in_off, in_len, out, out_off, out_len, status, n, g_ws, g_stamp);
+    NX_HIP_CHECK(hipGetLastError());
+    g_stamp += iters;
+    return NX_OK;
+}
