@@ -331,52 +331,64 @@ __device__ void decode_frame(WaveLds& L, const Frame& f, const uint32_t* __restr
         // ---------------- expand [O, E) 64 bytes at a time
         if (ntags) {
             int32_t jcur = -1;
-            const uint32_t s_lo = sbase, s_hi = sbase + (uint32_t)kStage;  // stage window (aligned coords)
+            const uint32_t s_lo = sbase;  // stage window [sbase, sbase + kStage) in aligned coordinates
+            const uint8_t* lds_bytes = L.ring;  // ring at [0, kRing), stage at [kRing, kRing + kStage)
             for (uint32_t S = O & ~63u; S < E && !trip; S += 64) {
                 if (lane == 0) L.bmask = 0ull;
                 if (mine && ostart >= S && ostart < S + 64u) atomicOr(&L.bmask, 1ull << (ostart - S));
                 const uint64_t B = L.bmask;
+                const uint32_t Blo = uni((uint32_t)B), Bhi = uni((uint32_t)(B >> 32));
                 const uint32_t pp = S + lane;
                 const bool act = pp >= O && pp < E;
-                const int32_t idx = jcur + (int32_t)__popcll(B & lanemask_le(lane));
-                jcur += (int32_t)__popcll(B);
+                // tag covering byte pp = (number of tag starts <= pp) - 1
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi(Bhi, __builtin_amdgcn_mbcnt_lo(Blo, 0u));
+                const uint32_t own = (uint32_t)((lane < 32 ? (Blo >> lane) : (Bhi >> (lane - 32))) & 1u);
+                const int32_t idx = jcur + (int32_t)(below + own);
+                jcur += (int32_t)(__builtin_popcount(Blo) + __builtin_popcount(Bhi));
                 const uint32_t Oeff = S > O ? S : O;
                 uint32_t v = 0;
                 bool res = true;
                 uint32_t sl = 0;
                 if (act) {
                     const Tag tg = L.tags[idx];
-                    if ((tg.x & 0x80000000u) == 0u) {
-                        const uint32_t pos = (tg.x & 0x7FFFFFFFu) + (pp - tg.start);
-                        const uint32_t pa = pos + a;
-                        v = (pa >= s_lo && pa < s_hi) ? (uint32_t)L.stage[pa & (kStage - 1)] : (uint32_t)src[pos];
-                    } else {
-                        const uint32_t q = pp - (tg.x & 0x7FFFFFFFu);
-                        if (q >= Oeff) {
-                            res = false;
-                            sl = q - S;
-                        } else if (q + (uint32_t)kRing >= Oeff) {
-                            v = L.ring[q & (kRing - 1)];
-                        } else {
-                            v = dst[q];
-                        }
+                    const bool lit = (tg.x & 0x80000000u) == 0u;
+                    const uint32_t xo = tg.x & 0x7FFFFFFFu;
+                    const uint32_t pos = xo + (pp - tg.start);  // literal: input position
+                    const uint32_t pa = pos + a;
+                    const uint32_t q = pp - xo;                   // copy: source output position
+                    const bool lit_stage = (pa - s_lo) < (uint32_t)kStage;
+                    const bool intra = !lit && q >= Oeff;
+                    const bool near = !lit && !intra && q + (uint32_t)kRing >= Oeff;
+                    // one LDS byte read serves literals in the stage and copies in the history ring
+                    const uint32_t loff = lit ? ((uint32_t)kRing + (pa & (kStage - 1))) : (q & (kRing - 1));
+                    v = lds_bytes[loff];
+                    const bool needg = lit ? !lit_stage : (!intra && !near);
+                    if (needg) {  // rare: literal beyond the stage / far copy (global, not flat)
+                        const uint8_t* gp = lit ? src + pos : dst + q;
+                        v = *(const __attribute__((address_space(1))) uint8_t*)(gp);
                     }
+                    res = !intra;
+                    sl = q - S;
                 }
-                for (int guard = 0; __any(!res); ++guard) {
-                    if (guard > 64) {
-                        st = kGuardTrip + 2;
-                        stop = trip = true;
-                        break;
-                    }
-                    const uint32_t v2 = (uint32_t)__shfl((int)v, (int)sl);
-                    const int r2 = __shfl((int)res, (int)sl);
-                    const uint32_t sl2 = (uint32_t)__shfl((int)sl, (int)sl);
-                    if (!res) {
-                        if (r2) {
-                            v = v2;
-                            res = true;
-                        } else {
-                            sl = sl2;
+                // overlapping copies inside this 64-byte group: pointer jumping, one ds_bpermute per
+                // step carrying (value | resolved << 8 | source lane << 16)
+                if (__any(!res)) {
+                    uint32_t word = (v & 0xFFu) | (res ? 0x100u : 0u) | ((sl & 63u) << 16);
+                    for (int guard = 0; __any(!res); ++guard) {
+                        if (guard > 8) {
+                            st = kGuardTrip + 2;
+                            stop = trip = true;
+                            break;
+                        }
+                        const uint32_t g = (uint32_t)__shfl((int)word, (int)sl);
+                        if (!res) {
+                            if (g & 0x100u) {
+                                v = g & 0xFFu;
+                                res = true;
+                            } else {
+                                sl = (g >> 16) & 63u;
+                            }
+                            word = (v & 0xFFu) | (res ? 0x100u : 0u) | (sl << 16);
                         }
                     }
                 }
