@@ -15,9 +15,15 @@
 //     are copied 4 bytes at a time with a funnel shift.
 // Hash table: Java allocates a zeroed short[min(nextPow2(len),16384)] per call (:97-99,191).
 // Each resident lane owns a 16384-entry uint32 slot in a device workspace; an entry is
-// (stamp << 16) | position, and a stamp mismatch reads as 0 — exactly a freshly zeroed table,
-// without a 32 KiB clear per chunk.
+//   stamp[31:28] | check[27:16] | position[15:0]
+// A stamp mismatch reads as position 0 — exactly a freshly zeroed table, without a clear per
+// chunk.  `check` is 12 bits folded from the 4 bytes at `position`: when it differs from the
+// probe word's fold, getInt(ip) != getInt(candidate) is already decided and the random read of
+// the candidate bytes is skipped (most probes of a literal run end this way).  The candidate
+// position — and with it the emitted stream — is unchanged; only the memory traffic drops.
 #include <stdlib.h>
+#include <algorithm>
+#include <map>
 #include <mutex>
 #include "nx_common.hpp"
 
@@ -149,8 +155,16 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
     uint32_t hts = length <= 1 ? 1u : (1u << (32 - __clz((uint32_t)(length - 1))));
     if (hts > 16384u) hts = 16384u;
     const int shift = __clz(hts) + 1;
-    const uint32_t stag = stamp << 16;
-#define TBL_DEC(e) ((((e) & 0xFFFF0000u) == stag) ? (int32_t)((e) & 0xFFFFu) : 0)
+    const uint32_t stag = stamp << 28;
+    const uint32_t word0 = length >= 4 ? ld32(in) : 0u;  // getInt(base + 0): an empty slot's candidate
+#define TLD(ptr) (*(ptr))
+#define TST(ptr, v) (*(ptr) = (v))
+#define CHK(wd) (((wd) ^ ((wd) >> 12) ^ ((wd) >> 24)) & 0xFFFu)
+#define MK(pos, wd) (stag | (CHK(wd) << 16) | (uint32_t)(pos))
+#define LIVE(e) (((e) & 0xF0000000u) == stag)
+#define TBL_DEC(e) (LIVE(e) ? (int32_t)((e) & 0xFFFFu) : 0)
+    // may getInt(ip) == getInt(candidate)?  false is exact, true needs the candidate bytes
+#define MAYBE(e, wd) (LIVE(e) ? ((((e) >> 16) & 0xFFFu) == CHK(wd)) : ((wd) == word0))
     int32_t nextEmit = 0;
     if (length >= 15) {  // MIN_COMPRESSIBLE_BYTES (:34,104)
         int32_t inIndex = 1;
@@ -170,8 +184,10 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
             if (nextIndex > length - 4) goto done;
             nextWord = ld32(in + nextIndex);
             nextHash = hash_of(nextWord, shift);
-            candidate = TBL_DEC(table[hash]);
-            table[hash] = stag | (uint32_t)inIndex;
+            uint32_t entry = TLD(table + hash);
+            candidate = TBL_DEC(entry);
+            bool maybe = MAYBE(entry, curWord);
+            TST(table + hash, MK(inIndex, curWord));
             for (;;) {
                 // speculative: the next probe's position, bytes and table entry
                 const int32_t pIndex = nextIndex;
@@ -181,11 +197,10 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
                 const bool pValid = pNext <= length - 4;
                 uint32_t pEntry = 0, pNextWord = 0;
                 if (pValid) {
-                    pEntry = table[pHash];
+                    pEntry = TLD(table + pHash);
                     pNextWord = ld32(in + pNext);
                 }
-                const uint32_t candWord = ld32(in + candidate);
-                if (curWord == candWord) break;  // match at inIndex
+                if (maybe && curWord == ld32(in + candidate)) break;  // match at inIndex
                 // advance to the next probe (:111-128)
                 skip++;
                 inIndex = pIndex;
@@ -196,7 +211,8 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
                 nextWord = pNextWord;
                 nextHash = hash_of(pNextWord, shift);
                 candidate = TBL_DEC(pEntry);
-                table[hash] = stag | (uint32_t)inIndex;
+                maybe = MAYBE(pEntry, curWord);
+                TST(table + hash, MK(inIndex, curWord));
             }
 
             enc_literal(in + nextEmit, w, inIndex - nextEmit);  // (:132)
@@ -213,11 +229,12 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
                 const uint32_t wTail = ld32(in + insertTail);
                 const uint32_t wCur = ld32(in + inIndex);
                 const uint32_t prevHash = hash_of(wTail, shift);
-                table[prevHash] = stag | (uint32_t)(inIndex - 1);
+                TST(table + prevHash, MK(inIndex - 1, wTail));
                 const uint32_t currentHash = hash_of(wCur, shift);
-                candidate = TBL_DEC(table[currentHash]);
-                table[currentHash] = stag | (uint32_t)inIndex;
-                if (wCur != ld32(in + candidate)) break;
+                const uint32_t e = TLD(table + currentHash);
+                candidate = TBL_DEC(e);
+                TST(table + currentHash, MK(inIndex, wCur));
+                if (!MAYBE(e, wCur) || wCur != ld32(in + candidate)) break;
             }
             nextWord = ld32(in + insertTail + 2);
             nextHash = hash_of(nextWord, shift);  // (:156)
@@ -226,6 +243,12 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
     }
 done:
 #undef TBL_DEC
+#undef MAYBE
+#undef LIVE
+#undef MK
+#undef CHK
+#undef TLD
+#undef TST
     if (nextEmit < length) enc_literal(in + nextEmit, w, length - nextEmit);  // (:162-164)
     w.finish();
     return w.pos();
@@ -247,15 +270,16 @@ __global__ void __launch_bounds__(256) k_snappy_encode(const uint8_t* __restrict
             out_len[c] = 0;
             continue;
         }
-        const uint32_t stamp = ((stamp_base + iter) % 65535u) + 1u;
+        const uint32_t stamp = stamp_base + iter + 1u;  // 1..15, host re-zeroes the workspace before wrap
         uint8_t* o = out + out_off[c];
         uint32_t olen;
+        const uint8_t* src = in + in_off[c];
         if ((((uintptr_t)o) & 3u) == 0) {
             Writer w{reinterpret_cast<uint32_t*>(o), 0, 0, 0};
-            olen = encode_chunk(in + in_off[c], (int32_t)len, w, table, stamp);
+            olen = encode_chunk(src, (int32_t)len, w, table, stamp);
         } else {
             ByteWriter w{o, 0};
-            olen = encode_chunk(in + in_off[c], (int32_t)len, w, table, stamp);
+            olen = encode_chunk(src, (int32_t)len, w, table, stamp);
         }
         out_len[c] = olen;
         status[c] = NX_OK;
@@ -266,13 +290,18 @@ __global__ void __launch_bounds__(256) k_snappy_encode(const uint8_t* __restrict
 }  // namespace nx
 
 namespace {
+// Encoder hash-table workspace, one per (device, stream): launches on one stream are ordered, so
+// they may share a workspace; launches on different streams may overlap and must not.
+struct Workspace {
+    uint32_t* ws = nullptr;
+    size_t threads = 0;
+    uint32_t stamp = 0;  // last stamp used; entries carry 4-bit stamps 1..15
+};
 std::mutex g_ws_mu;
-uint32_t* g_ws = nullptr;
-size_t g_ws_threads = 0;
-uint32_t g_stamp = 0;
-int g_ws_dev = -1;
+std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
 constexpr unsigned kEncBlock = 256;
 constexpr unsigned kEncWavesPerCU = 16;
+constexpr uint32_t kMaxStamp = 15;
 }  // namespace
 
 extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
@@ -283,27 +312,33 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     static const unsigned waves_per_cu = getenv("NX_ENC_WAVES") ? (unsigned)atoi(getenv("NX_ENC_WAVES")) : kEncWavesPerCU;
+    const hipStream_t st = (hipStream_t)stream;
     const size_t want = (size_t)cus * waves_per_cu * 64;
     const size_t threads = n < want ? ((n + kEncBlock - 1) / kEncBlock) * kEncBlock : want;
-    std::lock_guard<std::mutex> lk(g_ws_mu);
     const size_t per = 16384u * sizeof(uint32_t);
-    if (g_ws == nullptr || g_ws_threads < threads || g_ws_dev != dev) {
-        if (g_ws) (void)hipFree(g_ws);
-        g_ws = nullptr;
-        NX_HIP_CHECK(hipMalloc(&g_ws, threads * per));
-        NX_HIP_CHECK(hipMemsetAsync(g_ws, 0, threads * per, (hipStream_t)stream));
-        g_ws_threads = threads;
-        g_ws_dev = dev;
-        g_stamp = 0;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    Workspace& W = g_ws[{dev, st}];
+    if (W.ws == nullptr || W.threads < threads) {
+        if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
+        W.ws = nullptr;
+        NX_HIP_CHECK(hipMalloc(&W.ws, threads * per));
+        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, threads * per, st));
+        W.threads = threads;
+        W.stamp = 0;
     }
-    const uint32_t iters = (uint32_t)((n + threads - 1) / threads);
-    if ((uint64_t)g_stamp + iters >= 65535u) {
-        NX_HIP_CHECK(hipMemsetAsync(g_ws, 0, g_ws_threads * per, (hipStream_t)stream));
-        g_stamp = 0;
+    // Each launch gives a resident lane at most kMaxStamp - 1 chunks (one stamp each).
+    const size_t per_launch = threads * (kMaxStamp - 1);
+    for (size_t base = 0; base < n; base += per_launch) {
+        const uint32_t m = (uint32_t)std::min<size_t>(per_launch, n - base);
+        const uint32_t iters = (uint32_t)((m + threads - 1) / threads);
+        if (W.stamp + iters >= kMaxStamp) {
+            NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.threads * per, st));
+            W.stamp = 0;
+        }
+        hipLaunchKernelGGL(nx::enc::k_snappy_encode, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
+                           in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp);
+        NX_HIP_CHECK(hipGetLastError());
+        W.stamp += iters;
     }
-    hipLaunchKernelGGL(nx::enc::k_snappy_encode, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, (hipStream_t)stream, in,
-                       in_off, in_len, out, out_off, out_len, status, n, g_ws, g_stamp);
-    NX_HIP_CHECK(hipGetLastError());
-    g_stamp += iters;
     return NX_OK;
 }
