@@ -105,6 +105,7 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
 
     from netty_amd import batch as B
+    from netty_amd import shard as S
 
     n = args.chunks
     # HBM budget: src + dec (n*64 KiB each) + encoded slots (n*cap) + encoder workspace (~8.6 GB)
@@ -161,26 +162,15 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = S.max_over_ranks(t1 - t0, device=dev)
 
     # verification (outside the timed region): statuses, lengths, identity
     ok = (int((est != 0).sum()) == 0 and int((dst != 0).sum()) == 0 and bool(torch.equal(dlen, ln))
           and bool(torch.equal(dec, src)))
     comp_bytes = int(elen.to(torch.int64).sum().item())
-    totals = torch.tensor([comp_bytes], dtype=torch.int64, device=dev)
-    if world > 1:
-        gathered = [torch.zeros_like(totals) for _ in range(world)]
-        dist.all_gather(gathered, totals)  # offset exchange for a single global stream layout
-        totals_all = [int(x.item()) for x in gathered]
-        okt = torch.tensor([1 if ok else 0], device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
-    else:
-        totals_all = [comp_bytes]
+    # offset exchange that lays the shards out as one stream (outside the timed region)
+    _, _, totals_all = S.exchange_offsets(comp_bytes, device=dev)
+    ok = S.all_true(ok, device=dev)
 
     def avg_ms(pairs):
         return sum(a.elapsed_time(b) for a, b in pairs) / max(1, len(pairs))
