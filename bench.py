@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--chunks", type=int, default=1 << 20, help="64 KiB chunks per GPU (configs[1]: 1M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (H2D/D2H) end-to-end measurement")
+    ap.add_argument("--e2e-chunks", type=int, default=131072, help="chunks through the host pipeline (8 GiB)")
+    ap.add_argument("--e2e-sub", type=int, default=65536, help="chunks per pipelined sub-batch")
     return ap.parse_args()
 
 
@@ -208,6 +211,12 @@ def main():
         "compression_ratio": round(C_ / U, 4), "compressed_bytes_per_rank": totals_all,
         "verified": ok,
     }
+    if rank == 0 and world == 1 and not args.no_e2e:
+        # host-memory path (pinned ByteBuf-like buffers, H2D → kernels → D2H, two streams); never `value`
+        del src, dec, enc
+        torch.cuda.empty_cache()
+        from netty_amd import pipeline as P
+        line["end_to_end"] = P.measure(dev, n=args.e2e_chunks, sub=args.e2e_sub)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

@@ -127,6 +127,12 @@ int32_t nx_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 int32_t nx_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int32_t nx_stream_sync(void* stream);
 
+/* Gather chunk i from src[src_off[i] .. +len[i]) to dst[dst_off[i] ..): packs fixed-capacity
+ * output slots into one contiguous stream so a batch returns to host memory in one D2H copy
+ * (the per-message `out` buffers of MessageToByteEncoder.write, MessageToByteEncoder.java:105-117). */
+int32_t nx_pack_batch(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, uint8_t* dst,
+                      const uint64_t* dst_off, uint32_t n, void* stream);
+
 /* ------------------------------------------------------------------ (2) host handler layer */
 /* Output list of one decode()/encode() call: messages are views into an arena owned by the
  * handle (valid until the next call on the same handle). */

@@ -43,6 +43,7 @@ _SIGS = {
     "nx_lzf_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_lzf_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_textgen_device": (i32, [vp, u64, u32, u32, vp]),
+    "nx_pack_batch": (i32, [vp, vp, vp, vp, vp, u32, vp]),
     "nx_device_alloc": (vp, [sz]),
     "nx_device_free": (i32, [vp]),
     "nx_memcpy_h2d": (i32, [vp, vp, sz, vp]),

@@ -114,6 +114,22 @@ def textgen(out, first_chunk: int, n_chunks: int, chunk_len: int):
     return out
 
 
+def gather(src, src_off, length, dst=None, dst_off=None):
+    """Pack chunk i = src[src_off[i] : +length[i]] contiguously (nx_pack_batch).  dst_off defaults
+    to the exclusive scan of length.  Returns (dst, dst_off)."""
+    n = length.numel()
+    if dst_off is None:
+        dst_off = torch.zeros(n, dtype=torch.int64, device=src.device)
+        if n > 1:
+            torch.cumsum(length[:-1].to(torch.int64), 0, out=dst_off[1:])
+    if dst is None:
+        total = int((dst_off[-1] + length[-1].to(torch.int64)).item()) if n else 0
+        dst = torch.empty(max(total, 1), dtype=torch.uint8, device=src.device)
+    _chk(_lib.load().nx_pack_batch(_ptr(src), _ptr(src_off), _ptr(length), _ptr(dst), _ptr(dst_off), n, _stream()),
+         "nx_pack_batch")
+    return dst, dst_off
+
+
 def pack(chunks: list[bytes], device, align: int = 16, pad: int = 0):
     """Pack host chunks into one device tensor; returns (data, off[int64], len[int32])."""
     offs, cur = [], 0

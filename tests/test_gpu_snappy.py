@@ -185,3 +185,25 @@ def test_device_roundtrip_many_chunks(dev, B, oracle):
     for k in (0, 1, 4095, 8191):
         e = enc[k * cap:k * cap + elh[k]].cpu().numpy().tobytes()
         assert e == oracle.snappy_encode(oracle.textgen_chunk(k, L))
+
+
+def test_pack_batch_gathers_slots():
+    """nx_pack_batch: variable-length slots → one contiguous stream (aligned and unaligned)."""
+    import torch
+    from netty_amd import batch as B
+    g = torch.Generator().manual_seed(5)
+    n = 300
+    lens = torch.randint(0, 3000, (n,), generator=g, dtype=torch.int32)
+    lens[:3] = torch.tensor([0, 1, 17], dtype=torch.int32)
+    src_off = torch.arange(n, dtype=torch.int64) * 3072 + torch.randint(0, 16, (n,), generator=g)
+    src = torch.randint(0, 256, (n * 3072 + 64,), generator=g, dtype=torch.uint8)
+    for shift in (0, 3):
+        d_src, d_off, d_len = src.cuda(), src_off.cuda(), lens.cuda()
+        dst_off = torch.zeros(n, dtype=torch.int64)
+        dst_off[1:] = torch.cumsum(lens[:-1].to(torch.int64), 0)
+        dst_off += shift
+        dst = torch.zeros(int(dst_off[-1] + lens[-1]) + 16, dtype=torch.uint8, device="cuda")
+        B.gather(d_src, d_off, d_len, dst, dst_off.cuda())
+        want = torch.cat([src[int(o):int(o) + int(l)] for o, l in zip(src_off, lens)])
+        got = dst.cpu()[shift:shift + want.numel()]
+        assert torch.equal(got, want)
