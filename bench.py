@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (H2D/D2H) end-to-end measurement")
     ap.add_argument("--e2e-chunks", type=int, default=131072, help="chunks through the host pipeline (8 GiB)")
     ap.add_argument("--e2e-sub", type=int, default=65536, help="chunks per pipelined sub-batch")
+    ap.add_argument("--no-alt", action="store_true", help="skip the FastLZ/LZF (configs[3]) measurement")
+    ap.add_argument("--alt-chunks", type=int, default=262144)
     return ap.parse_args()
 
 
@@ -89,6 +91,93 @@ def cpu_baseline(seconds: float):
             "sample": f"oracle/netty_oracle.c encode+CRC32C then decode+verify of text-like 64 KiB chunks, "
                       f"{sum(counts)} chunks on {threads} threads in {t1 - t0:.1f}s (+ {d1} chunks single-thread)",
             "single_thread_value": round(single, 4)}
+
+
+def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2):
+    """configs[3]: FastLZ (level 1 and 2) and LZF encode/decode of a mixed batch — sizes uniform in
+    [4096, 65535], half text-like, half random — device-resident.  GiB/s of uncompressed bytes."""
+    g = torch.Generator(device=dev).manual_seed(1234)
+    CH = CHUNK
+    src = torch.empty(n * CH, dtype=torch.uint8, device=dev)
+    B.textgen(src, 0, n, CH)
+    view = src.view(n, CH)
+    view[1::2] = torch.randint(0, 256, (len(range(1, n, 2)), CH), dtype=torch.uint8, device=dev, generator=g)
+    ln = torch.randint(4096, 65536, (n,), dtype=torch.int32, device=dev, generator=g)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * CH
+    U = int(ln.to(torch.int64).sum())
+    res = {"chunks": n, "bytes": U, "sizes": "uniform [4096, 65535]", "data": "50% text-like, 50% random"}
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        return min(ts)
+
+    fcap = (B.fastlz_max_compressed_length(CH) + 15) // 16 * 16
+    fout = torch.empty(n * fcap, dtype=torch.uint8, device=dev)
+    foff = torch.arange(n, dtype=torch.int64, device=dev) * fcap
+    dec = torch.empty_like(src)
+    for level in (1, 2):
+        lv = torch.full((n,), level, dtype=torch.int32, device=dev)
+        box = {}
+
+        def enc():
+            box["r"] = B.fastlz_compress(src, off, ln, fout, foff, level=lv)
+
+        te = timed(enc)
+        flen, fst = box["r"]
+
+        def dcm():
+            box["d"] = B.fastlz_decompress(fout, foff, flen, dec, off, ln)
+
+        td = timed(dcm)
+        ok = bool(torch.equal(box["d"], ln)) and int((fst != 0).sum()) == 0
+        if ok:
+            for i in (0, 1, n - 1):
+                m = int(ln[i])
+                ok = ok and bool(torch.equal(dec[i * CH:i * CH + m], src[i * CH:i * CH + m]))
+        res[f"fastlz_l{level}"] = {"encode_gib_s": round(U / te * 1e3 / 2**30, 3), "decode_gib_s": round(U / td * 1e3 / 2**30, 3),
+                                   "ratio": round(int(flen.to(torch.int64).sum()) / U, 4), "verified": ok}
+    del fout
+    lcap = (B.lzf_max_compressed_length(CH) + 15) // 16 * 16
+    lout = torch.empty(n * lcap, dtype=torch.uint8, device=dev)
+    loff = torch.arange(n, dtype=torch.int64, device=dev) * lcap
+    box = {}
+
+    def lenc():
+        box["r"] = B.lzf_encode(src, off, ln, lout, loff)
+
+    te = timed(lenc)
+    llen, lst = box["r"]
+    # compressed "ZV" blocks (type 1): body at +7, compressed length at +3 (big-endian)
+    typ = lout[loff + 2]
+    idx = torch.nonzero(typ == 1).flatten()
+    boff = loff[idx] + 7
+    blen = (lout[loff[idx] + 3].to(torch.int32) << 8) | lout[loff[idx] + 4].to(torch.int32)
+    uo = off[idx]
+    ul = ln[idx]
+    Ud = int(ul.to(torch.int64).sum())
+
+    def ldec():
+        box["d"] = B.lzf_decode(lout, boff, blen, dec, uo, ul)
+
+    td = timed(ldec)
+    ok = int((lst != 0).sum()) == 0 and int((box["d"] != 0).sum()) == 0
+    if ok and idx.numel():
+        i = int(idx[0])
+        m = int(ln[i])
+        ok = bool(torch.equal(dec[i * CH:i * CH + m], src[i * CH:i * CH + m]))
+    res["lzf"] = {"encode_gib_s": round(U / te * 1e3 / 2**30, 3),
+                  "decode_gib_s": round(Ud / td * 1e3 / 2**30, 3) if idx.numel() else None,
+                  "decoded_chunks": int(idx.numel()), "ratio": round(int(llen.to(torch.int64).sum()) / U, 4), "verified": ok}
+    return res
 
 
 def main():
@@ -211,6 +300,12 @@ def main():
         "compression_ratio": round(C_ / U, 4), "compressed_bytes_per_rank": totals_all,
         "verified": ok,
     }
+    if rank == 0 and world == 1 and not args.no_alt:
+        del src, dec, enc
+        torch.cuda.empty_cache()
+        src = dec = enc = None
+        line["alt_codecs"] = bench_alt_codecs(torch, B, dev, args.alt_chunks)
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_e2e:
         # host-memory path (pinned ByteBuf-like buffers, H2D → kernels → D2H, two streams); never `value`
         del src, dec, enc

@@ -28,6 +28,14 @@ def snappy_max_compressed_length(n: int) -> int:
     return _lib.load().nx_snappy_max_compressed_length(n)
 
 
+def fastlz_max_compressed_length(n: int) -> int:
+    return _lib.load().nx_fastlz_max_compressed_length(n)
+
+
+def lzf_max_compressed_length(n: int) -> int:
+    return _lib.load().nx_lzf_max_compressed_length(n)
+
+
 def snappy_encode(inp, in_off, in_len, out, out_off, out_len=None, status=None):
     """Snappy.encode per chunk (Snappy.java:82-165).  Returns (out_len, status) int tensors."""
     n = in_len.numel()

@@ -17,7 +17,13 @@ eoff = torch.arange(n, dtype=torch.int64, device=dev) * cap
 elen, est = B.snappy_encode(src, off, ln, enc, eoff)
 crc = B.crc32c_masked(src, off, ln)
 dec = torch.empty_like(src)
+ts = []
 for _ in range(R):
+    a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
+    a.record()
     r = B.snappy_decode(enc, eoff, elen, dec, off, expected_crc=crc)
-torch.cuda.synchronize()
+    b.record()
+    torch.cuda.synchronize()
+    ts.append(a.elapsed_time(b))
+print("decode ms", [round(t, 3) for t in ts], "GiB/s", round(n * L / min(ts) * 1e3 / 2**30, 2))
 print("ok", bool(torch.equal(dec, src)), int((r["status"] != 0).sum()), int(elen.sum()))
