@@ -128,12 +128,59 @@ __device__ __forceinline__ void enc_copy(Wr& w, int32_t offset, int32_t length) 
     enc_copy_off(w, offset, length);
 }
 
+// Register window over the lane's own input stream: 32 bytes from a 16-byte-aligned address.
+// The scan front moves 1-2 bytes per probe, so one refill (two 16-byte loads) serves the next
+// 10-25 stream reads that would otherwise each be a separate memory request; with 262 144 lanes
+// streaming at once, L2 cannot keep a lane's current line between its probes.  Dword i of the
+// window is picked by a 3-level select tree (dynamic register indexing would spill to scratch).
+// A 16-byte block that holds at least one byte of the chunk never crosses a page, so the loads
+// stay inside mapped memory; a second block wholly past the end is not loaded.
+struct StreamWin {
+    const uint8_t* origin;  // chunk start rounded down to 16 bytes
+    uint32_t pad;           // chunk start - origin
+    uint32_t end;           // chunk end, origin-relative
+    uint32_t wb;            // window base, origin-relative, multiple of 16
+    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
+    __device__ __forceinline__ void init(const uint8_t* in, int32_t length) {
+        origin = reinterpret_cast<const uint8_t*>((uintptr_t)in & ~(uintptr_t)15);
+        pad = (uint32_t)((uintptr_t)in & 15u);
+        end = pad + (uint32_t)length;
+        wb = 0x80000000u;  // empty: q - wb > 27 for every position
+    }
+    __device__ __forceinline__ static uint32_t sel(uint32_t i, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4,
+                                                   uint32_t a5, uint32_t a6, uint32_t a7) {
+        const bool b0 = i & 1u, b1 = i & 2u, b2 = i & 4u;
+        const uint32_t c0 = b0 ? a1 : a0, c1 = b0 ? a3 : a2, c2 = b0 ? a5 : a4, c3 = b0 ? a7 : a6;
+        const uint32_t d0 = b1 ? c1 : c0, d1 = b1 ? c3 : c2;
+        return b2 ? d1 : d0;
+    }
+    // the 4 bytes at chunk position p (p + 4 <= length), little-endian
+    __device__ __forceinline__ uint32_t get(int32_t p) {
+        const uint32_t q = (uint32_t)p + pad;
+        uint32_t off = q - wb;
+        if (off > 27u) {
+            wb = q & ~15u;
+            const uint4 x = *reinterpret_cast<const uint4*>(origin + wb);
+            w0 = x.x; w1 = x.y; w2 = x.z; w3 = x.w;
+            if (wb + 16u < end) {
+                const uint4 y = *reinterpret_cast<const uint4*>(origin + wb + 16u);
+                w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
+            }
+            off = q - wb;
+        }
+        const uint32_t i = off >> 2;
+        const uint32_t lo = sel(i, w0, w1, w2, w3, w4, w5, w6, w7);
+        const uint32_t hi = sel(i + 1u, w0, w1, w2, w3, w4, w5, w6, w7);
+        return __builtin_amdgcn_alignbyte(hi, lo, off & 3u);
+    }
+};
+
 // 4 + findMatchingLength(in, candidate + 4, inIndex + 4, length)  (:224-239): the common-prefix
-// length bounded by the bytes left, computed 4 bytes per step.
-__device__ __forceinline__ int32_t match_len(const uint8_t* in, int32_t a, int32_t b, int32_t length) {
+// length bounded by the bytes left, computed 4 bytes per step (the inIndex side from the window).
+__device__ __forceinline__ int32_t match_len(const uint8_t* in, StreamWin& win, int32_t a, int32_t b, int32_t length) {
     int32_t m = 0;
     while (b + m <= length - 4) {
-        const uint32_t x = ld32(in + a + m) ^ ld32(in + b + m);
+        const uint32_t x = ld32(in + a + m) ^ win.get(b + m);
         if (x) return m + (int32_t)(__builtin_ctz(x) >> 3);
         m += 4;
     }
@@ -167,8 +214,10 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
 #define MAYBE(e, wd) (LIVE(e) ? ((((e) >> 16) & 0xFFFu) == CHK(wd)) : ((wd) == word0))
     int32_t nextEmit = 0;
     if (length >= 15) {  // MIN_COMPRESSIBLE_BYTES (:34,104)
+        StreamWin win;
+        win.init(in, length);
         int32_t inIndex = 1;
-        uint32_t nextWord = ld32(in + 1);
+        uint32_t nextWord = win.get(1);
         uint32_t nextHash = hash_of(nextWord, shift);
         for (;;) {  // outer: (:106)
             // ---- probe run (:107-130), software-pipelined by one probe
@@ -182,7 +231,7 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
             curWord = nextWord;
             nextIndex = inIndex + (skip++ >> 5);
             if (nextIndex > length - 4) goto done;
-            nextWord = ld32(in + nextIndex);
+            nextWord = win.get(nextIndex);
             nextHash = hash_of(nextWord, shift);
             uint32_t entry = TLD(table + hash);
             candidate = TBL_DEC(entry);
@@ -198,7 +247,7 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
                 uint32_t pEntry = 0, pNextWord = 0;
                 if (pValid) {
                     pEntry = TLD(table + pHash);
-                    pNextWord = ld32(in + pNext);
+                    pNextWord = win.get(pNext);
                 }
                 if (maybe && curWord == ld32(in + candidate)) break;  // match at inIndex
                 // advance to the next probe (:111-128)
@@ -220,14 +269,14 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
             int32_t insertTail;
             for (;;) {  // (:135-154)
                 const int32_t base = inIndex;
-                const int32_t matched = 4 + match_len(in, candidate + 4, inIndex + 4, length);
+                const int32_t matched = 4 + match_len(in, win, candidate + 4, inIndex + 4, length);
                 inIndex += matched;
                 enc_copy(w, base - candidate, matched);
                 insertTail = inIndex - 1;
                 nextEmit = inIndex;
                 if (inIndex >= length - 4) goto done;
-                const uint32_t wTail = ld32(in + insertTail);
-                const uint32_t wCur = ld32(in + inIndex);
+                const uint32_t wTail = win.get(insertTail);
+                const uint32_t wCur = win.get(inIndex);
                 const uint32_t prevHash = hash_of(wTail, shift);
                 TST(table + prevHash, MK(inIndex - 1, wTail));
                 const uint32_t currentHash = hash_of(wCur, shift);
@@ -236,7 +285,7 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
                 TST(table + currentHash, MK(inIndex, wCur));
                 if (!MAYBE(e, wCur) || wCur != ld32(in + candidate)) break;
             }
-            nextWord = ld32(in + insertTail + 2);
+            nextWord = win.get(insertTail + 2);
             nextHash = hash_of(nextWord, shift);  // (:156)
             ++inIndex;
         }
@@ -254,7 +303,7 @@ done:
     return w.pos();
 }
 
-__global__ void __launch_bounds__(256) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+__global__ void __launch_bounds__(256, 8) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                        const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
                                                        int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
