@@ -36,6 +36,7 @@ _SIGS = {
     "nx_snappy_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_snappy_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_snappy_decode_batch_naive": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
+    "nx_snappy_decode_batch_fused": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_crc32c_masked_batch": (i32, [vp, vp, vp, vp, u32, vp]),
     "nx_fastlz_compress_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_fastlz_decompress_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),

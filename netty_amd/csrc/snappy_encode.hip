@@ -188,7 +188,7 @@ __device__ __forceinline__ int32_t match_len(const uint8_t* in, StreamWin& win, 
     return m;
 }
 
-template <class Wr>
+template <bool SWAP, class Wr>
 __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length, Wr& w, uint32_t* __restrict__ table, uint32_t stamp) {
     for (int i = 0;; i++) {  // preamble (:84-92)
         const uint32_t b = (uint32_t)length >> (i * 7);
@@ -204,8 +204,11 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
     const int shift = __clz(hts) + 1;
     const uint32_t stag = stamp << 28;
     const uint32_t word0 = length >= 4 ? ld32(in) : 0u;  // getInt(base + 0): an empty slot's candidate
-#define TLD(ptr) (*(ptr))
 #define TST(ptr, v) (*(ptr) = (v))
+    // read-and-insert of one table slot: a single atomic swap (one memory request instead of a
+    // load and a store; same-address order keeps Java's read-then-write semantics)
+#define XCH(ptr, v) (SWAP ? __hip_atomic_exchange((ptr), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) \
+                          : ({ const uint32_t o_ = *(ptr); *(ptr) = (v); o_; }))
 #define CHK(wd) (((wd) ^ ((wd) >> 12) ^ ((wd) >> 24)) & 0xFFFu)
 #define MK(pos, wd) (stag | (CHK(wd) << 16) | (uint32_t)(pos))
 #define LIVE(e) (((e) & 0xF0000000u) == stag)
@@ -233,10 +236,9 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
             if (nextIndex > length - 4) goto done;
             nextWord = win.get(nextIndex);
             nextHash = hash_of(nextWord, shift);
-            uint32_t entry = TLD(table + hash);
+            uint32_t entry = XCH(table + hash, MK(inIndex, curWord));
             candidate = TBL_DEC(entry);
             bool maybe = MAYBE(entry, curWord);
-            TST(table + hash, MK(inIndex, curWord));
             for (;;) {
                 // speculative: the next probe's position, bytes and table entry
                 const int32_t pIndex = nextIndex;
@@ -246,10 +248,14 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
                 const bool pValid = pNext <= length - 4;
                 uint32_t pEntry = 0, pNextWord = 0;
                 if (pValid) {
-                    pEntry = TLD(table + pHash);
+                    // the next probe's insert is made now; undone below if this probe matches
+                    pEntry = XCH(table + pHash, MK(pIndex, pWord));
                     pNextWord = win.get(pNext);
                 }
-                if (maybe && curWord == ld32(in + candidate)) break;  // match at inIndex
+                if (maybe && curWord == ld32(in + candidate)) {  // match at inIndex
+                    if (pValid) TST(table + pHash, pEntry);   // Java never probes pIndex: restore
+                    break;
+                }
                 // advance to the next probe (:111-128)
                 skip++;
                 inIndex = pIndex;
@@ -261,7 +267,6 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
                 nextHash = hash_of(pNextWord, shift);
                 candidate = TBL_DEC(pEntry);
                 maybe = MAYBE(pEntry, curWord);
-                TST(table + hash, MK(inIndex, curWord));
             }
 
             enc_literal(in + nextEmit, w, inIndex - nextEmit);  // (:132)
@@ -280,9 +285,8 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
                 const uint32_t prevHash = hash_of(wTail, shift);
                 TST(table + prevHash, MK(inIndex - 1, wTail));
                 const uint32_t currentHash = hash_of(wCur, shift);
-                const uint32_t e = TLD(table + currentHash);
+                const uint32_t e = XCH(table + currentHash, MK(inIndex, wCur));
                 candidate = TBL_DEC(e);
-                TST(table + currentHash, MK(inIndex, wCur));
                 if (!MAYBE(e, wCur) || wCur != ld32(in + candidate)) break;
             }
             nextWord = win.get(insertTail + 2);
@@ -296,21 +300,23 @@ done:
 #undef LIVE
 #undef MK
 #undef CHK
-#undef TLD
+#undef XCH
 #undef TST
     if (nextEmit < length) enc_literal(in + nextEmit, w, length - nextEmit);  // (:162-164)
     w.finish();
     return w.pos();
 }
 
+template <bool SWAP>
 __global__ void __launch_bounds__(256, 8) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                        const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
                                                        int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
-                                                       uint32_t stamp_base) {
+                                                       uint32_t stamp_base, uint32_t alias) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nthreads = gridDim.x * blockDim.x;
-    uint32_t* table = workspace + (size_t)tid * 16384u;
+    // alias != 0 is a timing experiment only (NX_ENC_ALIAS): lanes share tables, output is wrong
+    uint32_t* table = workspace + (size_t)(alias ? tid % alias : tid) * 16384u;
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
         const uint32_t len = in_len[c];
@@ -325,10 +331,10 @@ __global__ void __launch_bounds__(256, 8) k_snappy_encode(const uint8_t* __restr
         const uint8_t* src = in + in_off[c];
         if ((((uintptr_t)o) & 3u) == 0) {
             Writer w{reinterpret_cast<uint32_t*>(o), 0, 0, 0};
-            olen = encode_chunk(src, (int32_t)len, w, table, stamp);
+            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
         } else {
             ByteWriter w{o, 0};
-            olen = encode_chunk(src, (int32_t)len, w, table, stamp);
+            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
         }
         out_len[c] = olen;
         status[c] = NX_OK;
@@ -384,8 +390,10 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
             NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.threads * per, st));
             W.stamp = 0;
         }
-        hipLaunchKernelGGL(nx::enc::k_snappy_encode, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
-                           in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp);
+        static const uint32_t alias = getenv("NX_ENC_ALIAS") ? (uint32_t)atoi(getenv("NX_ENC_ALIAS")) : 0u;
+        static const bool swap = getenv("NX_ENC_SWAP") ? atoi(getenv("NX_ENC_SWAP")) != 0 : true;
+        hipLaunchKernelGGL(swap ? nx::enc::k_snappy_encode<true> : nx::enc::k_snappy_encode<false>, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
+                           in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp, alias);
         NX_HIP_CHECK(hipGetLastError());
         W.stamp += iters;
     }

@@ -65,14 +65,14 @@ def test_snappy_encode_parity(dev, B, oracle, kat):
         assert got == want, (i, len(c))
 
 
-@pytest.mark.parametrize("naive", [False, True])
-def test_snappy_decode_parity(dev, B, oracle, kat, naive):
+@pytest.mark.parametrize("variant,align", [("auto", 16), ("auto", 1), ("fused", 16), ("fused", 1), ("naive", 16)])
+def test_snappy_decode_parity(dev, B, oracle, kat, variant, align):
     chunks = _corpus(oracle, kat)
     enc = [oracle.snappy_encode(c) for c in chunks]
-    inp, off, ln = B.pack(enc, dev)
+    inp, off, ln = B.pack(enc, dev, align=align)
     out, ooff = B.out_slots([65536] * len(enc), dev)
     crcs = torch.tensor([oracle.snappy_checksum(c) for c in chunks], dtype=torch.int64).to(torch.int32).to(dev)
-    r = B.snappy_decode(inp, off, ln, out, ooff, expected_crc=crcs, want_crc=True, consumed=True, naive=naive)
+    r = B.snappy_decode(inp, off, ln, out, ooff, expected_crc=crcs, want_crc=True, consumed=True, variant=variant)
     torch.cuda.synchronize()
     st, olen, cons = r["status"].cpu().tolist(), r["out_len"].cpu().tolist(), r["consumed"].cpu().tolist()
     crc = [x & 0xFFFFFFFF for x in r["crc"].cpu().tolist()]
@@ -109,12 +109,12 @@ def _crafted_streams(oracle, kat):
     return cases
 
 
-@pytest.mark.parametrize("naive", [False, True])
-def test_snappy_decode_edge_cases(dev, B, oracle, kat, naive):
+@pytest.mark.parametrize("variant", ["auto", "fused", "naive"])
+def test_snappy_decode_edge_cases(dev, B, oracle, kat, variant):
     cases = _crafted_streams(oracle, kat)
     inp, off, ln = B.pack(cases, dev)
     out, ooff = B.out_slots([65536] * len(cases), dev)
-    r = B.snappy_decode(inp, off, ln, out, ooff, consumed=True, naive=naive)
+    r = B.snappy_decode(inp, off, ln, out, ooff, consumed=True, variant=variant)
     torch.cuda.synchronize()
     st, olen, cons = r["status"].cpu().tolist(), r["out_len"].cpu().tolist(), r["consumed"].cpu().tolist()
     outh, ooff_h = out.cpu().numpy().tobytes(), ooff.cpu().tolist()
@@ -124,6 +124,39 @@ def test_snappy_decode_edge_cases(dev, B, oracle, kat, naive):
         if wst == 0:
             assert outh[ooff_h[i]:ooff_h[i] + olen[i]] == wout, i
             assert cons[i] == wcons, (i, cons[i], wcons)
+
+
+def _copy_run(n_out, length, offset=1):
+    """A raw Snappy block: preamble n_out, literal 'a', then COPY_2 tags of `length` at `offset`."""
+    pre, v = bytearray(), n_out
+    while v >= 0x80:
+        pre.append((v & 0x7F) | 0x80)
+        v >>= 7
+    pre.append(v)
+    tag = bytes([0x02 | ((length - 1) << 2), offset & 0xFF, offset >> 8])
+    return bytes(pre) + bytes([0x00]) + b"a" + tag * ((n_out - 1) // length)
+
+
+def test_snappy_decode_record_overflow_falls_back(dev, B, oracle):
+    """Frames with more output-producing tags than a record slot holds (16384) are decoded by the
+    single-kernel path inside nx_snappy_decode_batch; results stay bit-exact with the oracle."""
+    cases = [_copy_run(65536, 1), _copy_run(16385, 1), _copy_run(16384, 1), _copy_run(16386, 1)[:-1],
+             _copy_run(40000, 2)[:-3] + bytes([0x02 | (3 << 2), 0xFF, 0xFF]),  # ends on an offset-beyond error
+             oracle.snappy_encode(oracle.textgen_chunk(5, 65536))]
+    inp, off, ln = B.pack(cases, dev, align=1)
+    out, ooff = B.out_slots([65536] * len(cases), dev)
+    r = B.snappy_decode(inp, off, ln, out, ooff, consumed=True, want_crc=True)
+    torch.cuda.synchronize()
+    st, olen, cons = r["status"].cpu().tolist(), r["out_len"].cpu().tolist(), r["consumed"].cpu().tolist()
+    crc = [x & 0xFFFFFFFF for x in r["crc"].cpu().tolist()]
+    outh, ooff_h = out.cpu().numpy().tobytes(), ooff.cpu().tolist()
+    for i, c in enumerate(cases):
+        wst, wout, wcons = oracle.snappy_decode(c, 65536)
+        assert st[i] == wst, (i, st[i], wst)
+        assert olen[i] == len(wout), i
+        assert outh[ooff_h[i]:ooff_h[i] + olen[i]] == wout, i
+        assert cons[i] == wcons, (i, cons[i], wcons)
+        assert crc[i] == oracle.snappy_checksum(wout), i
 
 
 def test_snappy_decode_detects_crc_corruption(dev, B, oracle):
