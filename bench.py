@@ -93,6 +93,20 @@ def cpu_baseline(seconds: float):
             "single_thread_value": round(single, 4)}
 
 
+def load_traffic():
+    """Per-chunk HBM bytes per kernel from the newest committed PMC summary (scripts/pmc_traffic.sh:
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench's workload)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        return {k: v["hbm_bytes_per_chunk"] for k, v in d["kernels"].items()}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2):
     """configs[3]: FastLZ (level 1 and 2) and LZF encode/decode of a mixed batch — sizes uniform in
     [4096, 65535], half text-like, half random — device-resident.  GiB/s of uncompressed bytes."""
@@ -259,6 +273,23 @@ def main():
     # verification (outside the timed region): statuses, lengths, identity
     ok = (int((est != 0).sum()) == 0 and int((dst != 0).sum()) == 0 and bool(torch.equal(dlen, ln))
           and bool(torch.equal(dec, src)))
+    # configs[2]: a 2 % subset with corrupted expected CRCs must be flagged, and nothing else
+    g = torch.Generator(device=dev).manual_seed(77 + rank)
+    bad = torch.rand(n, device=dev, generator=g) < 0.02
+    crc_bad = torch.where(bad, crc ^ 1, crc)
+    B.snappy_decode(enc, eoff, elen, dec, off, expected_crc=crc_bad, out_len=dlen, status=dst)
+    crc_detect = bool(torch.equal(dst != 0, bad)) and bool(torch.equal(dst[bad], torch.full_like(dst[bad], -7)))
+    ok = ok and crc_detect
+    # achievable HBM bandwidth on this device: a plain device-to-device copy (read + write bytes)
+    cb = []
+    for _ in range(3):
+        a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a_.record()
+        dec.copy_(src)
+        b_.record()
+        torch.cuda.synchronize()
+        cb.append(a_.elapsed_time(b_))
+    copy_gbs = 2 * src.numel() / (min(cb) / 1e3) / 1e9
     comp_bytes = int(elen.to(torch.int64).sum().item())
     # offset exchange that lays the shards out as one stream (outside the timed region)
     _, _, totals_all = S.exchange_offsets(comp_bytes, device=dev)
@@ -271,14 +302,21 @@ def main():
     U = n * CHUNK
     C_ = comp_bytes
 
-    def roof(algo_bytes, ms):
-        a = algo_bytes / (ms / 1e3) / 1e9
-        return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None}
+    traffic = load_traffic()
 
-    r_dec = roof(C_ + U, t_dec)       # decode: C_in + U_out per chunk
-    r_enc = roof(U + C_, t_enc)       # encode: U_in + C_out per chunk
-    r_dec["kernel"], r_enc["kernel"] = "nx::dec::k_snappy_decode", "nx::enc::k_snappy_encode"
+    def roof(algo_bytes, ms, kernels):
+        a = algo_bytes / (ms / 1e3) / 1e9
+        per_chunk = sum(traffic.get(k, 0.0) for k in kernels) if traffic else None
+        return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(a / HBM_PEAK_GBS, 4),
+                "traffic": round(per_chunk * n) if per_chunk else None,
+                "traffic_per_chunk": round(per_chunk) if per_chunk else None,
+                "algorithmic_per_chunk": round(algo_bytes / n),
+                "achievable_copy_gbs": round(copy_gbs, 1), "frac_of_achievable": round(a / copy_gbs, 4),
+                "kernel": " + ".join(kernels)}
+
+    r_dec = roof(C_ + U, t_dec, ["nx::dec::k_parse", "nx::dec::k_expand"])  # decode: C_in + U_out per chunk
+    r_enc = roof(U + C_, t_enc, ["nx::enc::k_snappy_encode<true>"])           # encode: U_in + C_out per chunk
     dominant = r_enc if t_enc >= t_dec else r_dec
 
     value = world * U / elapsed * args.steps / 2**30
@@ -298,6 +336,7 @@ def main():
         "decode_gib_s": round(U / (t_dec / 1e3) / 2**30, 3),
         "kernel_ms": {"crc32c": round(t_crc, 3), "encode": round(t_enc, 3), "decode_crc": round(t_dec, 3)},
         "compression_ratio": round(C_ / U, 4), "compressed_bytes_per_rank": totals_all,
+        "crc_corruption_subset_detected": crc_detect,
         "verified": ok,
     }
     if rank == 0 and world == 1 and not args.no_alt:

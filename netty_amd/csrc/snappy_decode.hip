@@ -347,6 +347,46 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
                 need = (pb >= 63u ? ~0ull : ((2ull << pb) - 1ull)) & ~((1ull << (pa & 63u)) - 1ull);
             }
         }
+        // Sources that do not depend on this pass, fetched once before the rounds: far copies (the
+        // frame's own flushed output) and literal bytes outside the stage, from HBM.  (Guarded by
+        // wave-uniform branches so that passes without such pieces skip them entirely.)
+        uint32_t gval = 0;
+        if (__ballot(valid && gl)) {
+            if (valid && gl) {
+                if (!lit) {
+                    gval = g_ld32u(io.dst + sp);  // flushed and drained output of this frame
+                } else if (pin + 4u <= io.in_len) {
+                    gval = g_ld32u(io.src + pin);
+                } else {
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i)
+                        if (pin + i < io.in_len) gval |= g_ld8(io.src + pin + i) << (8 * i);
+                }
+            }
+        }
+        // Overlapping copies (offset < length): out[x] = out[tstart - xo + ((x - tstart) mod xo)],
+        // xo < tlen <= 64; the four ring byte addresses, packed 4 x 12 bits into two dwords.
+        const bool has_ov = __ballot(valid && overlap) != 0ull;
+        uint32_t ova = 0, ovb = 0;
+        if (has_ov) {
+            if (valid && overlap) {
+                const uint32_t n0 = x0 - tstart;
+                const uint32_t inv = (uint32_t)(__builtin_amdgcn_rcpf((float)xo) * 65536.0f) + 1u;  // floor(n0/xo) exact for n0, xo < 64
+                const uint32_t m0 = n0 - xo * ((n0 * inv) >> 16);
+                const uint32_t q = tstart - xo;
+                uint32_t ad[4];
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i) {
+                    uint32_t mi = m0 + i;
+                    mi -= mi >= xo ? xo : 0u;
+                    mi -= mi >= xo ? xo : 0u;
+                    mi -= mi >= xo ? xo : 0u;
+                    ad[i] = (q + mi) & (kRing - 1);
+                }
+                ova = ad[0] | (ad[1] << 16);
+                ovb = ad[2] | (ad[3] << 16);
+            }
+        }
         uint64_t pending = __ballot(valid);
         uint64_t done = ~pending;
         for (int round = 0; pending; ++round) {
@@ -356,37 +396,11 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
             const uint32_t w = sp >> 2;
             const uint32_t lo = lds32[lbase + (w & lmask)];
             const uint32_t hi = lds32[lbase + ((w + 1u) & lmask)];
-            uint32_t val = __builtin_amdgcn_alignbyte(hi, lo, sp & 3u);
-            if (__ballot(ready && gl)) {
-                if (ready && gl) {
-                    if (!lit) {
-                        val = g_ld32u(io.dst + sp);  // flushed and drained output of this frame
-                    } else if (pin + 4u <= io.in_len) {
-                        val = g_ld32u(io.src + pin);
-                    } else {
-                        val = 0;
-#pragma unroll
-                        for (uint32_t i = 0; i < 4; ++i)
-                            if (pin + i < io.in_len) val |= g_ld8(io.src + pin + i) << (8 * i);
-                    }
-                }
-            }
-            if (__ballot(ready && overlap)) {
+            uint32_t val = gl ? gval : __builtin_amdgcn_alignbyte(hi, lo, sp & 3u);
+            if (has_ov && __ballot(ready && overlap)) {
                 if (ready && overlap) {
-                    // out[x] = out[tstart - xo + ((x - tstart) mod xo)]; xo < tlen <= 64
-                    const uint32_t n0 = x0 - tstart;
-                    const uint32_t inv = (uint32_t)(65536.0f / (float)xo) + 1u;
-                    const uint32_t m0 = n0 - xo * ((n0 * inv) >> 16);
-                    const uint32_t q = tstart - xo;
-                    val = 0;
-#pragma unroll
-                    for (uint32_t i = 0; i < 4; ++i) {
-                        uint32_t mi = m0 + i;
-                        mi -= mi >= xo ? xo : 0u;
-                        mi -= mi >= xo ? xo : 0u;
-                        mi -= mi >= xo ? xo : 0u;
-                        val |= (uint32_t)ring8[(q + mi) & (kRing - 1)] << (8 * i);
-                    }
+                    val = (uint32_t)ring8[ova & 0xFFFFu] | ((uint32_t)ring8[ova >> 16] << 8) | ((uint32_t)ring8[ovb & 0xFFFFu] << 16) |
+                          ((uint32_t)ring8[ovb >> 16] << 24);
                 }
             }
             // one masked atomic write per lane: the piece's bytes, or nothing (mask 0)
@@ -755,88 +769,59 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
         if (!__any(run)) break;
         if (run && !win.has(ip)) win.load(ip);  // burst reload: one wait for the whole wave
         while (run && win.has(ip)) {
+            // one tag, branch-free: both interpretations are computed and selected by the type
             const uint64_t v = win.get8(ip);
             const uint32_t tag = (uint32_t)v & 0xFFu;
             const uint32_t ops = (uint32_t)(v >> 8);  // operand bytes (valid where < in_len)
             const uint32_t after_tag = ip + 1u;
             const uint32_t avail = in_len - after_tag;
             const uint32_t type = tag & 3u;
-            run = false;  // set again by a tag that completes
-            if (type == 0u) {
-                const uint32_t code = tag >> 2;
-                uint32_t nb = 0, lj;
-                if (code < 60u) {
-                    lj = code + 1u;
-                } else {
-                    nb = code - 59u;
-                    if (avail < nb) {  // NOT_ENOUGH_INPUT: silent stop, tag byte consumed
-                        ip = after_tag;
-                        continue;
-                    }
-                    lj = (nb == 4u ? ops : (ops & ((1u << (8u * nb)) - 1u))) + 1u;  // Java int length + 1
-                }
-                const uint32_t dpos = after_tag + nb;
-                ip = dpos;
-                if ((int32_t)lj >= 0 && in_len - dpos < lj) {
-                    ip = after_tag;
-                    continue;
-                }
-                if ((int32_t)lj < 0) {
-                    st = NX_ERR_SNAPPY_LITERAL_LEN_INVALID;
-                    continue;
-                }
-                if ((uint64_t)op + lj > cap) {
-                    st = NX_ERR_SNAPPY_OUTPUT_OVERFLOW;
-                    continue;
-                }
-                bool fit = true;
-                for (uint32_t k = 0; k < lj && fit; k += 64u) {
+            const bool isl = type == 0u;
+            const uint32_t code = tag >> 2;
+            // literal (decodeLiteral): nb length bytes after the tag, Java int length + 1
+            const uint32_t nb = (isl && code >= 60u) ? code - 59u : 0u;
+            const uint32_t fmask = nb >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
+            const uint32_t lj = nb == 0u ? code + 1u : (ops & fmask) + 1u;
+            // copy (decodeCopyWith{1,2,4}ByteOffset)
+            const uint32_t csize = type == 1u ? 1u : (type == 2u ? 2u : 4u);
+            const uint32_t clen = type == 1u ? 4u + (code & 7u) : 1u + code;
+            const uint32_t coff = type == 1u ? (((tag & 0xe0u) << 3) | (ops & 0xFFu)) : (type == 2u ? (ops & 0xFFFFu) : ops);
+            const uint32_t hdr = isl ? nb : csize;
+            const uint32_t dpos = after_tag + hdr;
+            const bool lneg = isl && (int32_t)lj < 0;
+            // NOT_ENOUGH_INPUT (silent stop, the tag byte consumed): operands, or the literal's bytes
+            const bool nei = avail < hdr || (isl && !lneg && in_len - dpos < lj);
+            const uint32_t len = isl ? lj : clen;
+            int32_t err = 0;
+            if (isl) {
+                err = lneg ? NX_ERR_SNAPPY_LITERAL_LEN_INVALID : 0;
+            } else {
+                err = coff == 0u ? NX_ERR_SNAPPY_OFFSET_ZERO
+                                 : ((int32_t)coff < 0 ? NX_ERR_SNAPPY_OFFSET_NEGATIVE : (coff > op ? NX_ERR_SNAPPY_OFFSET_BEYOND : 0));
+            }
+            if (err == 0 && (uint64_t)op + len > cap) err = NX_ERR_SNAPPY_OUTPUT_OVERFLOW;
+            if (nei || err != 0) {  // rare: the frame stops here
+                ip = nei ? after_tag : dpos;
+                st = nei ? NX_OK : err;
+                run = false;
+                continue;
+            }
+            const uint32_t m0 = lj < 64u ? lj : 64u;
+            const uint32_t r = isl ? (((m0 - 1u) << 25) | dpos) : (0x80000000u | ((clen - 1u) << 25) | coff);
+            bool fit = (isl && lj == 0u) || rw.put(r);  // a zero-length literal (field 0xFFFFFFFF) emits nothing
+            if (isl && lj > 64u) {  // literals longer than 64 bytes: one record per 64 bytes
+                for (uint32_t k = 64u; k < lj && fit; k += 64u) {
                     const uint32_t m = lj - k < 64u ? lj - k : 64u;
                     fit = rw.put(((m - 1u) << 25) | (dpos + k));
                 }
-                if (!fit) {
-                    st = kNeedFused;
-                    continue;
-                }
-                ip = dpos + lj;
-                op += lj;
-            } else {
-                const uint32_t csize = type == 1u ? 1u : (type == 2u ? 2u : 4u);
-                if (avail < csize) {
-                    ip = after_tag;
-                    continue;
-                }
-                uint32_t length, offset;
-                if (type == 1u) {
-                    length = 4u + ((tag >> 2) & 7u);
-                    offset = ((tag & 0xe0u) << 3) | (ops & 0xFFu);
-                } else {
-                    length = 1u + (tag >> 2);
-                    offset = type == 2u ? (ops & 0xFFFFu) : ops;
-                }
-                ip = after_tag + csize;
-                if (offset == 0u) {
-                    st = NX_ERR_SNAPPY_OFFSET_ZERO;
-                    continue;
-                }
-                if ((int32_t)offset < 0) {
-                    st = NX_ERR_SNAPPY_OFFSET_NEGATIVE;
-                    continue;
-                }
-                if (offset > op) {
-                    st = NX_ERR_SNAPPY_OFFSET_BEYOND;
-                    continue;
-                }
-                if (op + length > cap) {
-                    st = NX_ERR_SNAPPY_OUTPUT_OVERFLOW;
-                    continue;
-                }
-                if (!rw.put(0x80000000u | ((length - 1u) << 25) | offset)) {
-                    st = kNeedFused;
-                    continue;
-                }
-                op += length;
             }
+            if (!fit) {
+                st = kNeedFused;
+                run = false;
+                continue;
+            }
+            ip = dpos + (isl ? lj : 0u);
+            op += len;
             run = ip < in_len;
         }
     }
