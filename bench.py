@@ -217,9 +217,11 @@ def main():
     # HBM budget: src + dec (n*64 KiB each) + encoded slots (n*cap) + encoder workspace (~8.6 GB)
     cap = (B.snappy_max_compressed_length(CHUNK) + 15) // 16 * 16
     free, total = torch.cuda.mem_get_info(dev)
-    need = n * (2 * CHUNK + cap) + (10 << 30)
+    # + encoder hash tables (16 GiB) and decoder record slots (16 GiB) allocated by the C-ABI, + slack
+    reserve = 40 << 30
+    need = n * (2 * CHUNK + cap) + reserve
     if need > free:
-        n = int((free - (10 << 30)) // (2 * CHUNK + cap))
+        n = int((free - reserve) // (2 * CHUNK + cap))
     first = rank * n  # contiguous shard of chunk indices per rank
 
     src = torch.empty(n * CHUNK, dtype=torch.uint8, device=dev)
@@ -271,8 +273,11 @@ def main():
     elapsed = S.max_over_ranks(t1 - t0, device=dev)
 
     # verification (outside the timed region): statuses, lengths, identity
+    def same(a, b, step=1 << 32):  # torch.equal in slices (it materialises a mask of the whole tensor)
+        return all(bool(torch.equal(a[i:i + step], b[i:i + step])) for i in range(0, a.numel(), step))
+
     ok = (int((est != 0).sum()) == 0 and int((dst != 0).sum()) == 0 and bool(torch.equal(dlen, ln))
-          and bool(torch.equal(dec, src)))
+          and same(dec, src))
     # configs[2]: a 2 % subset with corrupted expected CRCs must be flagged, and nothing else
     g = torch.Generator(device=dev).manual_seed(77 + rank)
     bad = torch.rand(n, device=dev, generator=g) < 0.02

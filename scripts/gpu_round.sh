@@ -16,7 +16,7 @@ if [[ $STAGE == all || $STAGE == smoke ]]; then
   run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 1
 fi
 if [[ $STAGE == all || $STAGE == test ]]; then
-  run timeout -k 10 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+  run timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
   rc=$?
   if [[ $rc -ge 2 ]]; then exit $rc; fi
 fi
@@ -26,6 +26,10 @@ fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
   export TMPDIR=/tmp
   cd /tmp && run timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-      python "$ROOT/bench.py" --chunks "$CHUNKS" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/prof.log" 2>&1 || exit 1
+      python "$ROOT/bench.py" --chunks "$CHUNKS" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-alt > "$OUT/prof.log" 2>&1 || exit 1
+  cd "$ROOT"
+fi
+if [[ $STAGE == all || $STAGE == pmc ]]; then
+  run env CHUNKS="$CHUNKS" bash scripts/pmc_traffic.sh || exit 1
 fi
 echo done >> "$OUT/steps.log"
