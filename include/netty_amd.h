@@ -83,6 +83,31 @@ int32_t nx_snappy_decode_batch_naive(const uint8_t* in, const uint64_t* in_off, 
                                      const uint32_t* expected_masked_crc, uint32_t* crc_out,
                                      uint32_t n, void* stream);
 
+/* Replaces the chunk walk of SnappyFrameDecoder.decode (SnappyFrameDecoder.java:85-231) as
+ * ByteToMessageDecoder.callDecode runs it over a cumulation (ByteToMessageDecoder.java:464-517),
+ * for n device-resident cumulations at once (one per stream/connection).
+ *   in[in_off[s] .. +in_len[s]) — stream s's readable bytes.
+ *   state[s]    (in/out) — started (bit 0) | corrupted (bit 1) | numBytesToSkip << 8; 0 for a new decoder.
+ *   consumed[s] — bytes read (the cumulation's new readerIndex).  On a frame error: the start of the
+ *                 failing chunk (the end of a stream identifier whose contents mismatch).
+ *   status[s]   — NX_OK; NX_SCAN_LIST_FULL (the list filled up before this stream's next data chunk:
+ *                 call again from consumed[s]); < 0 = NX_ERR_SNAPPY_* frame error (the decoder is now
+ *                 corrupted, as :227-230).
+ * Data chunks are listed in device arrays of `cap` entries: COMPRESSED_DATA at [0, counts[0]),
+ * UNCOMPRESSED_DATA at [cap - counts[1], cap).  Entry k: data_off[k] = absolute position in `in` of
+ * the payload (after the 4-byte checksum), data_len[k] = chunkLength - 4, masked_crc[k] = the stored
+ * checksum, chunk_stream[k] = s, chunk_seq[k] = the chunk's index among stream s's data chunks.
+ * The first counts[0] entries of data_off / data_len / masked_crc are nx_snappy_decode_batch's
+ * in_off / in_len / expected_masked_crc as they stand.  The call zeroes counts[0..2] (counts[2] counts
+ * claims, which may exceed cap).
+ * A compressed chunk's Snappy errors (and any checksum mismatch) surface in the decode batch; the
+ * caller drops the stream's chunks after the first failing one, as Java stops at the exception. */
+int32_t nx_snappy_frame_scan_batch(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                                   uint32_t* state, uint64_t* consumed, int32_t* status,
+                                   uint64_t* data_off, uint32_t* data_len, uint32_t* masked_crc,
+                                   uint32_t* chunk_stream, uint32_t* chunk_seq, uint32_t* counts,
+                                   uint32_t cap, uint32_t n, void* stream);
+
 /* Replaces Snappy.calculateChecksum(ByteBuf, off, len)  Snappy.java:668-676
  * (Crc32c.java:105-124 + maskChecksum :720-722).  masked_out[i] = mask(crc32c(chunk i)). */
 int32_t nx_crc32c_masked_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len,

@@ -47,6 +47,29 @@
  * LzfDecoder.java:120-122,134-137).  The handle's err_msg carries the reference message. */
 #define NX_ERR_FRAME_CORRUPT              (-40)
 
+/* Device frame scan (nx_snappy_frame_scan_batch), one code per SnappyFrameDecoder throw site: */
+/* :116-118  "Unexpected length of stream identifier: %d" */
+#define NX_ERR_SNAPPY_STREAM_ID_LENGTH        (-41)
+/* :128-133 → checkByte :233-238  "Unexpected stream identifier contents. Mismatched snappy protocol version?" */
+#define NX_ERR_SNAPPY_STREAM_ID_CONTENT       (-42)
+/* :181-183  "Received COMPRESSED_DATA tag before STREAM_IDENTIFIER" */
+#define NX_ERR_SNAPPY_COMPRESSED_BEFORE_ID    (-43)
+/* :159-161  "Received UNCOMPRESSED_DATA tag before STREAM_IDENTIFIER" */
+#define NX_ERR_SNAPPY_UNCOMPRESSED_BEFORE_ID  (-44)
+/* :138-140  "Received RESERVED_SKIPPABLE tag before STREAM_IDENTIFIER" */
+#define NX_ERR_SNAPPY_SKIPPABLE_BEFORE_ID     (-45)
+/* :162-165  "Received UNCOMPRESSED_DATA larger than 65540 bytes" */
+#define NX_ERR_SNAPPY_UNCOMPRESSED_TOO_LARGE  (-46)
+/* :198-201  "Received COMPRESSED_DATA that contains uncompressed data that exceeds 65536 bytes" */
+#define NX_ERR_SNAPPY_DECOMPRESSED_TOO_LARGE  (-47)
+/* chunk length < 4: the checksum read runs past the chunk (:171-177, :194-195 throw from ByteBuf) */
+#define NX_ERR_SNAPPY_CHUNK_TOO_SHORT         (-48)
+/* :152-157  "Found reserved unskippable chunk type: 0x%x" */
+#define NX_ERR_SNAPPY_UNSKIPPABLE             (-49)
+/* Not an error: the frame scan's chunk list is full; the stream stopped before a data chunk and
+ * continues from consumed[i] on the next call. */
+#define NX_SCAN_LIST_FULL                     1
+
 #define NX_ERR_INVALID_ARG                (-100)
 #define NX_ERR_HIP                        (-101)
 #define NX_ERR_NO_DEVICE                  (-102)

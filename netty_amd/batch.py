@@ -69,6 +69,31 @@ def snappy_decode(inp, in_off, in_len, out, out_off, out_cap=None, expected_crc=
     return {"out_len": out_len, "status": status, "consumed": cons, "crc": crc}
 
 
+def snappy_frame_scan(inp, in_off, in_len, state, cap: int):
+    """SnappyFrameDecoder's chunk walk over device cumulations (nx_snappy_frame_scan_batch).
+
+    in_off / in_len: int64 tensors (one cumulation per stream); state: int32 tensor, updated in place
+    (started | corrupted << 1 | numBytesToSkip << 8).  Returns a dict of tensors: consumed, status,
+    counts [compressed, uncompressed, claims], and the list arrays data_off, data_len, masked_crc,
+    stream, seq (compressed entries at [0, counts[0]), uncompressed at [cap - counts[1], cap))."""
+    n = in_len.numel()
+    dev = inp.device
+    c = max(int(cap), 1)
+    r = {"consumed": torch.empty(n, dtype=torch.int64, device=dev),
+         "status": torch.empty(n, dtype=torch.int32, device=dev),
+         "data_off": torch.empty(c, dtype=torch.int64, device=dev),
+         "data_len": torch.empty(c, dtype=torch.int32, device=dev),
+         "masked_crc": torch.empty(c, dtype=torch.int32, device=dev),
+         "stream": torch.empty(c, dtype=torch.int32, device=dev),
+         "seq": torch.empty(c, dtype=torch.int32, device=dev),
+         "counts": torch.empty(3, dtype=torch.int32, device=dev)}
+    _chk(_lib.load().nx_snappy_frame_scan_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(state), _ptr(r["consumed"]),
+                                                _ptr(r["status"]), _ptr(r["data_off"]), _ptr(r["data_len"]),
+                                                _ptr(r["masked_crc"]), _ptr(r["stream"]), _ptr(r["seq"]), _ptr(r["counts"]),
+                                                int(cap), n, _stream()), "nx_snappy_frame_scan_batch")
+    return r
+
+
 def crc32c_masked(inp, off, length, out=None):
     """Snappy.calculateChecksum per chunk (Snappy.java:668-676)."""
     n = length.numel()

@@ -20,6 +20,16 @@ extern "C" const char* nx_status_string(int32_t s) {
         case NX_ERR_FASTLZ_CRC_MISMATCH: return "stream corrupted: mismatching checksum";
         case NX_ERR_LZF_CORRUPT: return "Corrupt LZF data";
         case NX_ERR_FRAME_CORRUPT: return "corrupted frame";
+        case NX_ERR_SNAPPY_STREAM_ID_LENGTH: return "Unexpected length of stream identifier";
+        case NX_ERR_SNAPPY_STREAM_ID_CONTENT: return "Unexpected stream identifier contents. Mismatched snappy protocol version?";
+        case NX_ERR_SNAPPY_COMPRESSED_BEFORE_ID: return "Received COMPRESSED_DATA tag before STREAM_IDENTIFIER";
+        case NX_ERR_SNAPPY_UNCOMPRESSED_BEFORE_ID: return "Received UNCOMPRESSED_DATA tag before STREAM_IDENTIFIER";
+        case NX_ERR_SNAPPY_SKIPPABLE_BEFORE_ID: return "Received RESERVED_SKIPPABLE tag before STREAM_IDENTIFIER";
+        case NX_ERR_SNAPPY_UNCOMPRESSED_TOO_LARGE: return "Received UNCOMPRESSED_DATA larger than 65540 bytes";
+        case NX_ERR_SNAPPY_DECOMPRESSED_TOO_LARGE: return "Received COMPRESSED_DATA that contains uncompressed data that exceeds 65536 bytes";
+        case NX_ERR_SNAPPY_CHUNK_TOO_SHORT: return "Received a data chunk shorter than its checksum";
+        case NX_ERR_SNAPPY_UNSKIPPABLE: return "Found reserved unskippable chunk type";
+        case NX_SCAN_LIST_FULL: return "chunk list full (call again from consumed)";
         case NX_ERR_INVALID_ARG: return "invalid argument";
         case NX_ERR_HIP: return "HIP runtime error";
         case NX_ERR_NO_DEVICE: return "no GPU device";

@@ -212,3 +212,96 @@ def textgen_chunk(index: int, n: int = 65536) -> bytes:
     out = _buf(n)
     lib().orc_textgen_chunk(index, out, n)
     return bytes(out[:n])
+
+
+# ---------------------------------------------------------------- Snappy frame scan
+# Status codes of include/netty_amd_status.h used by the scan.
+SCAN_OK, SCAN_LIST_FULL = 0, 1
+SCAN_ERR = {"stream_id_length": -41, "stream_id_content": -42, "compressed_before_id": -43,
+            "uncompressed_before_id": -44, "skippable_before_id": -45, "uncompressed_too_large": -46,
+            "decompressed_too_large": -47, "chunk_too_short": -48, "unskippable": -49, "preamble_too_long": -1}
+
+
+def snappy_frame_scan(buf: bytes, state: int = 0, cap: int | None = None):
+    """Pure-Python restatement of SnappyFrameDecoder.decode's chunk walk (SnappyFrameDecoder.java:85-231)
+    under ByteToMessageDecoder.callDecode (ByteToMessageDecoder.java:464-517: decode() again while it
+    reads).  Small inputs only.  state = started | corrupted << 1 | numBytesToSkip << 8.
+    Returns (entries, consumed, state, status); entries = [(type, payload_off, payload_len, stored_crc)]
+    for the data chunks in stream order (type 0 compressed, 1 uncompressed).  `cap` bounds the entries
+    (status SCAN_LIST_FULL, stopping before the chunk that did not fit)."""
+    n = len(buf)
+    started, corrupted, skip = bool(state & 1), bool(state & 2), state >> 8
+    p, res, ents = 0, SCAN_OK, []
+    if corrupted:  # :86-89
+        p = n
+    while not corrupted and p < n:
+        if skip:  # :91-99
+            k = min(skip, n - p)
+            p, skip = p + k, skip - k
+            continue
+        avail = n - p
+        if avail < 4:  # :104-108
+            break
+        typ, clen = buf[p], int.from_bytes(buf[p + 1:p + 4], "little")
+        if typ == 0xFF:  # STREAM_IDENTIFIER :115-136
+            if clen != 6:
+                res = SCAN_ERR["stream_id_length"]
+                break
+            if avail < 10:
+                break
+            content = buf[p + 4:p + 10]
+            p += 10
+            if content != b"sNaPpY":
+                res = SCAN_ERR["stream_id_content"]
+                break
+            started = True
+            continue
+        if typ & 0x80:  # RESERVED_SKIPPABLE :137-151
+            if not started:
+                res = SCAN_ERR["skippable_before_id"]
+                break
+            p += 4
+            k = min(clen, n - p)
+            p, skip = p + k, clen - k
+            continue
+        if typ > 1:  # RESERVED_UNSKIPPABLE :152-157
+            res = SCAN_ERR["unskippable"]
+            break
+        if not started:
+            res = SCAN_ERR["uncompressed_before_id" if typ else "compressed_before_id"]
+            break
+        if typ == 1 and clen > 65540:  # :162-165
+            res = SCAN_ERR["uncompressed_too_large"]
+            break
+        if avail < 4 + clen:  # :167-169, :190-192
+            break
+        if clen < 4:
+            res = SCAN_ERR["chunk_too_short"]
+            break
+        if typ == 0:  # getPreamble over the cumulation (Snappy.java:404-441), :197-201
+            ulen, complete = 0, False
+            for i in range(4):
+                if p + 8 + i >= n:
+                    break
+                c = buf[p + 8 + i]
+                ulen |= (c & 0x7F) << (7 * i)
+                if not c & 0x80:
+                    complete = True
+                    break
+                if i == 3:
+                    res = SCAN_ERR["preamble_too_long"]
+            if res:
+                break
+            if not complete:
+                ulen = 0
+            if ulen > 65536:
+                res = SCAN_ERR["decompressed_too_large"]
+                break
+        if cap is not None and len(ents) >= cap:
+            res = SCAN_LIST_FULL
+            break
+        ents.append((typ, p + 8, clen - 4, int.from_bytes(buf[p + 4:p + 8], "little")))
+        p += 4 + clen
+    if res < 0:
+        corrupted = True  # :227-230
+    return ents, p, int(started) | (int(corrupted) << 1) | (skip << 8), res

@@ -187,3 +187,46 @@ def test_textgen_deterministic(oracle):
     assert a == oracle.textgen_chunk(0, 65536) and a != oracle.textgen_chunk(1, 65536)
     r = len(oracle.snappy_encode(a)) / 65536
     assert 0.40 < r < 0.52  # Netty ratio on the text-like chunks ≈ 0.46
+
+
+def test_snappy_frame_scan_kats(kat, oracle):
+    """The frame-scan restatement against SnappyFrameDecoderTest's streams: every expected exception
+    is a scan error or (validating decoders) a checksum mismatch; every expected message is a listed
+    chunk whose payload decodes to it."""
+    for v in kat["snappy_frame_decode"]:
+        buf = bytes.fromhex(v["in"])
+        ents, consumed, state, status = oracle.snappy_frame_scan(buf)
+        msgs, failed = [], status < 0
+        for typ, off, ln, crc in ents:
+            payload = buf[off:off + ln]
+            if typ == 0:
+                st, out, _ = oracle.snappy_decode(payload, 65536)
+                failed |= st < 0
+            else:
+                out = payload
+            if v.get("validate") and oracle.snappy_checksum(out) != crc:
+                failed = True
+            msgs.append(out.hex())
+        if v.get("error"):
+            assert failed, v["src"]
+        else:
+            assert not failed and status == 0 and consumed == len(buf), v["src"]
+            assert msgs == v["msgs"], v["src"]
+        assert bool(state & 2) == (status < 0)
+
+
+def test_snappy_frame_scan_partial_and_skip(oracle):
+    framed, _ = oracle.snappy_frame_encode(oracle.textgen_chunk(3, 70000))
+    skippable = bytes([0xFE, 10, 0, 0]) + bytes(10)
+    buf = framed + skippable + framed[10:]
+    full = oracle.snappy_frame_scan(buf)
+    per = len(oracle.snappy_frame_scan(framed)[0])
+    assert full[3] == 0 and full[1] == len(buf) and len(full[0]) == 2 * per > 2
+    for cut in (3, 10, 11, 25, len(framed) - 1, len(framed) + 6):
+        e1, c1, s1, r1 = oracle.snappy_frame_scan(buf[:cut])
+        assert r1 == 0 and c1 <= cut
+        e2, c2, s2, r2 = oracle.snappy_frame_scan(buf[c1:], s1)
+        assert r2 == 0 and c1 + c2 == len(buf)
+        assert [(t, o + c1, n, c) for t, o, n, c in e2] == [(t, o, n, c) for t, o, n, c in full[0][len(e1):]]
+    e, c, s, r = oracle.snappy_frame_scan(buf, cap=1)
+    assert r == oracle.SCAN_LIST_FULL and len(e) == 1 and not s & 2
