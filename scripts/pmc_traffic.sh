@@ -6,7 +6,7 @@ CHUNKS=${CHUNKS:-1048576}
 cd /tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d "$ROOT/gpurun_out/traffic_$c" -o p -- \
-      python "$ROOT/bench.py" --chunks "$CHUNKS" --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-alt \
+      python "$ROOT/bench.py" --chunks "$CHUNKS" --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-alt --no-frame-scan \
       > "$ROOT/gpurun_out/traffic_$c.log" 2>&1 || exit 1
 done
 cd "$ROOT" && python scripts/pmc_traffic.py gpurun_out "$CHUNKS" > gpurun_out/pmc_traffic.json
