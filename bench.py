@@ -365,7 +365,9 @@ def main():
 
     def roof(algo_bytes, ms, kernels):
         a = algo_bytes / (ms / 1e3) / 1e9
-        per_chunk = sum(traffic.get(k, 0.0) for k in kernels) if traffic else None
+        # PMC summaries name kernels with their template arguments; match on the name before them
+        per_chunk = (sum(v for k2, v in traffic.items() if any(k2.split("<")[0] == k.split("<")[0] for k in kernels))
+                     if traffic else None)
         return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(a / HBM_PEAK_GBS, 4),
                 "traffic": round(per_chunk * n) if per_chunk else None,
@@ -375,7 +377,7 @@ def main():
                 "kernel": " + ".join(kernels)}
 
     r_dec = roof(C_ + U, t_dec, ["nx::dec::k_parse", "nx::dec::k_expand"])  # decode: C_in + U_out per chunk
-    r_enc = roof(U + C_, t_enc, ["nx::enc::k_snappy_encode<true>"])           # encode: U_in + C_out per chunk
+    r_enc = roof(U + C_, t_enc, ["nx::enc::k_snappy_encode<true, false>"])           # encode: U_in + C_out per chunk
     dominant = r_enc if t_enc >= t_dec else r_dec
 
     value = world * U / elapsed * args.steps / 2**30

@@ -188,7 +188,7 @@ __device__ __forceinline__ int32_t match_len(const uint8_t* in, StreamWin& win, 
     return m;
 }
 
-template <bool SWAP, class Wr>
+template <bool SWAP, bool SPEC, class Wr>
 __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length, Wr& w, uint32_t* __restrict__ table, uint32_t stamp) {
     for (int i = 0;; i++) {  // preamble (:84-92)
         const uint32_t b = (uint32_t)length >> (i * 7);
@@ -228,6 +228,22 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
             int32_t nextIndex = inIndex;
             int32_t candidate;
             uint32_t curWord;
+            if constexpr (!SPEC) {
+                // Java's order: each probe's swap waits for the previous compare, so no probe is
+                // made and undone (fewer memory requests; the kernel is request-rate bound)
+                uint32_t entry;
+                do {
+                    inIndex = nextIndex;
+                    const uint32_t hash = nextHash;
+                    curWord = nextWord;
+                    nextIndex = inIndex + (skip++ >> 5);
+                    if (nextIndex > length - 4) goto done;
+                    nextWord = win.get(nextIndex);
+                    nextHash = hash_of(nextWord, shift);
+                    entry = XCH(table + hash, MK(inIndex, curWord));
+                    candidate = TBL_DEC(entry);
+                } while (!(MAYBE(entry, curWord) && curWord == ld32(in + candidate)));
+            } else {
             // first probe of the run
             inIndex = nextIndex;
             uint32_t hash = nextHash;
@@ -268,6 +284,7 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
                 candidate = TBL_DEC(pEntry);
                 maybe = MAYBE(pEntry, curWord);
             }
+            }
 
             enc_literal(in + nextEmit, w, inIndex - nextEmit);  // (:132)
 
@@ -307,7 +324,7 @@ done:
     return w.pos();
 }
 
-template <bool SWAP>
+template <bool SWAP, bool SPEC>
 __global__ void __launch_bounds__(256, 8) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                        const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
@@ -331,10 +348,10 @@ __global__ void __launch_bounds__(256, 8) k_snappy_encode(const uint8_t* __restr
         const uint8_t* src = in + in_off[c];
         if ((((uintptr_t)o) & 3u) == 0) {
             Writer w{reinterpret_cast<uint32_t*>(o), 0, 0, 0};
-            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
+            olen = encode_chunk<SWAP, SPEC>(src, (int32_t)len, w, table, stamp);
         } else {
             ByteWriter w{o, 0};
-            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
+            olen = encode_chunk<SWAP, SPEC>(src, (int32_t)len, w, table, stamp);
         }
         out_len[c] = olen;
         status[c] = NX_OK;
@@ -392,7 +409,10 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
         }
         static const uint32_t alias = getenv("NX_ENC_ALIAS") ? (uint32_t)atoi(getenv("NX_ENC_ALIAS")) : 0u;
         static const bool swap = getenv("NX_ENC_SWAP") ? atoi(getenv("NX_ENC_SWAP")) != 0 : true;
-        hipLaunchKernelGGL(swap ? nx::enc::k_snappy_encode<true> : nx::enc::k_snappy_encode<false>, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
+        static const bool spec = getenv("NX_ENC_SPEC") ? atoi(getenv("NX_ENC_SPEC")) != 0 : false;
+        auto kern = swap ? (spec ? nx::enc::k_snappy_encode<true, true> : nx::enc::k_snappy_encode<true, false>)
+                         : (spec ? nx::enc::k_snappy_encode<false, true> : nx::enc::k_snappy_encode<false, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
                            in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp, alias);
         NX_HIP_CHECK(hipGetLastError());
         W.stamp += iters;
