@@ -377,7 +377,7 @@ def main():
                 "kernel": " + ".join(kernels)}
 
     r_dec = roof(C_ + U, t_dec, ["nx::dec::k_parse", "nx::dec::k_expand"])  # decode: C_in + U_out per chunk
-    r_enc = roof(U + C_, t_enc, ["nx::enc::k_snappy_encode<true, false>"])           # encode: U_in + C_out per chunk
+    r_enc = roof(U + C_, t_enc, ["nx::enc::k_snappy_encode<true>"])           # encode: U_in + C_out per chunk
     dominant = r_enc if t_enc >= t_dec else r_dec
 
     value = world * U / elapsed * args.steps / 2**30

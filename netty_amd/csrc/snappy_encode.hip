@@ -32,7 +32,10 @@ namespace enc {
 
 typedef uint32_t __attribute__((aligned(1))) u32u;
 
+typedef uint64_t __attribute__((aligned(1))) u64u;
+
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const u32u*>(p); }  // LE, unaligned
+__device__ __forceinline__ uint64_t ld64(const uint8_t* p) { return *reinterpret_cast<const u64u*>(p); }
 __device__ __forceinline__ uint32_t hash_of(uint32_t le, int shift) {
     return (__builtin_bswap32(le) * 0x1e35a7bdu) >> shift;  // hash (:177-179) on the BIG-endian getInt
 }
@@ -175,20 +178,34 @@ struct StreamWin {
     }
 };
 
+// The 8 bytes at chunk position c, or its 4 when fewer than 8 remain: the candidate compare and the
+// first step of the match extension share one memory request.
+__device__ __forceinline__ uint64_t ld_cand(const uint8_t* in, int32_t c, int32_t length) {
+    return c + 8 <= length ? ld64(in + c) : (uint64_t)ld32(in + c);
+}
+
 // 4 + findMatchingLength(in, candidate + 4, inIndex + 4, length)  (:224-239): the common-prefix
 // length bounded by the bytes left, computed 4 bytes per step (the inIndex side from the window).
-__device__ __forceinline__ int32_t match_len(const uint8_t* in, StreamWin& win, int32_t a, int32_t b, int32_t length) {
+// `first` = the 4 bytes at a, already read with the candidate compare; b <= length - 4 implies
+// a + 4 <= length (a < b), which is when ld_cand read them.
+__device__ __forceinline__ int32_t match_len(const uint8_t* in, StreamWin& win, int32_t a, int32_t b, int32_t length,
+                                             uint32_t first) {
     int32_t m = 0;
-    while (b + m <= length - 4) {
-        const uint32_t x = ld32(in + a + m) ^ win.get(b + m);
-        if (x) return m + (int32_t)(__builtin_ctz(x) >> 3);
-        m += 4;
+    if (b <= length - 4) {
+        const uint32_t x0 = first ^ win.get(b);
+        if (x0) return (int32_t)(__builtin_ctz(x0) >> 3);
+        m = 4;
+        while (b + m <= length - 4) {
+            const uint32_t x = ld32(in + a + m) ^ win.get(b + m);
+            if (x) return m + (int32_t)(__builtin_ctz(x) >> 3);
+            m += 4;
+        }
     }
     while (b + m < length && in[a + m] == in[b + m]) ++m;
     return m;
 }
 
-template <bool SWAP, bool SPEC, class Wr>
+template <bool SWAP, class Wr>
 __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length, Wr& w, uint32_t* __restrict__ table, uint32_t stamp) {
     for (int i = 0;; i++) {  // preamble (:84-92)
         const uint32_t b = (uint32_t)length >> (i * 7);
@@ -223,75 +240,33 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
         uint32_t nextWord = win.get(1);
         uint32_t nextHash = hash_of(nextWord, shift);
         for (;;) {  // outer: (:106)
-            // ---- probe run (:107-130), software-pipelined by one probe
             int32_t skip = 32;
             int32_t nextIndex = inIndex;
             int32_t candidate;
             uint32_t curWord;
-            if constexpr (!SPEC) {
-                // Java's order: each probe's swap waits for the previous compare, so no probe is
-                // made and undone (fewer memory requests; the kernel is request-rate bound)
-                uint32_t entry;
-                do {
-                    inIndex = nextIndex;
-                    const uint32_t hash = nextHash;
-                    curWord = nextWord;
-                    nextIndex = inIndex + (skip++ >> 5);
-                    if (nextIndex > length - 4) goto done;
-                    nextWord = win.get(nextIndex);
-                    nextHash = hash_of(nextWord, shift);
-                    entry = XCH(table + hash, MK(inIndex, curWord));
-                    candidate = TBL_DEC(entry);
-                } while (!(MAYBE(entry, curWord) && curWord == ld32(in + candidate)));
-            } else {
-            // first probe of the run
-            inIndex = nextIndex;
-            uint32_t hash = nextHash;
-            curWord = nextWord;
-            nextIndex = inIndex + (skip++ >> 5);
-            if (nextIndex > length - 4) goto done;
-            nextWord = win.get(nextIndex);
-            nextHash = hash_of(nextWord, shift);
-            uint32_t entry = XCH(table + hash, MK(inIndex, curWord));
-            candidate = TBL_DEC(entry);
-            bool maybe = MAYBE(entry, curWord);
-            for (;;) {
-                // speculative: the next probe's position, bytes and table entry
-                const int32_t pIndex = nextIndex;
-                const uint32_t pHash = nextHash;
-                const uint32_t pWord = nextWord;
-                const int32_t pNext = pIndex + (skip >> 5);
-                const bool pValid = pNext <= length - 4;
-                uint32_t pEntry = 0, pNextWord = 0;
-                if (pValid) {
-                    // the next probe's insert is made now; undone below if this probe matches
-                    pEntry = XCH(table + pHash, MK(pIndex, pWord));
-                    pNextWord = win.get(pNext);
-                }
-                if (maybe && curWord == ld32(in + candidate)) {  // match at inIndex
-                    if (pValid) TST(table + pHash, pEntry);   // Java never probes pIndex: restore
-                    break;
-                }
-                // advance to the next probe (:111-128)
-                skip++;
-                inIndex = pIndex;
-                hash = pHash;
-                curWord = pWord;
-                nextIndex = pNext;
-                if (!pValid) goto done;
-                nextWord = pNextWord;
-                nextHash = hash_of(pNextWord, shift);
-                candidate = TBL_DEC(pEntry);
-                maybe = MAYBE(pEntry, curWord);
-            }
-            }
+            uint64_t cand8;  // the 8 bytes at candidate (4 near the chunk end), read once per compare
+            // ---- probe run (:107-130), in Java's order: each probe's swap waits for the previous
+            // compare (a speculative next swap, undone on a match, cost 7 % more time in requests);
+            // only the next position's bytes and hash are computed ahead
+            uint32_t entry;
+            do {
+                inIndex = nextIndex;
+                const uint32_t hash = nextHash;
+                curWord = nextWord;
+                nextIndex = inIndex + (skip++ >> 5);
+                if (nextIndex > length - 4) goto done;
+                nextWord = win.get(nextIndex);
+                nextHash = hash_of(nextWord, shift);
+                entry = XCH(table + hash, MK(inIndex, curWord));
+                candidate = TBL_DEC(entry);
+            } while (!(MAYBE(entry, curWord) && curWord == (uint32_t)(cand8 = ld_cand(in, candidate, length))));
 
             enc_literal(in + nextEmit, w, inIndex - nextEmit);  // (:132)
 
             int32_t insertTail;
             for (;;) {  // (:135-154)
                 const int32_t base = inIndex;
-                const int32_t matched = 4 + match_len(in, win, candidate + 4, inIndex + 4, length);
+                const int32_t matched = 4 + match_len(in, win, candidate + 4, inIndex + 4, length, (uint32_t)(cand8 >> 32));
                 inIndex += matched;
                 enc_copy(w, base - candidate, matched);
                 insertTail = inIndex - 1;
@@ -304,7 +279,7 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
                 const uint32_t currentHash = hash_of(wCur, shift);
                 const uint32_t e = XCH(table + currentHash, MK(inIndex, wCur));
                 candidate = TBL_DEC(e);
-                if (!MAYBE(e, wCur) || wCur != ld32(in + candidate)) break;
+                if (!MAYBE(e, wCur) || wCur != (uint32_t)(cand8 = ld_cand(in, candidate, length))) break;
             }
             nextWord = win.get(insertTail + 2);
             nextHash = hash_of(nextWord, shift);  // (:156)
@@ -324,7 +299,7 @@ done:
     return w.pos();
 }
 
-template <bool SWAP, bool SPEC>
+template <bool SWAP>
 __global__ void __launch_bounds__(256, 8) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                        const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
@@ -348,10 +323,10 @@ __global__ void __launch_bounds__(256, 8) k_snappy_encode(const uint8_t* __restr
         const uint8_t* src = in + in_off[c];
         if ((((uintptr_t)o) & 3u) == 0) {
             Writer w{reinterpret_cast<uint32_t*>(o), 0, 0, 0};
-            olen = encode_chunk<SWAP, SPEC>(src, (int32_t)len, w, table, stamp);
+            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
         } else {
             ByteWriter w{o, 0};
-            olen = encode_chunk<SWAP, SPEC>(src, (int32_t)len, w, table, stamp);
+            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
         }
         out_len[c] = olen;
         status[c] = NX_OK;
@@ -409,10 +384,7 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
         }
         static const uint32_t alias = getenv("NX_ENC_ALIAS") ? (uint32_t)atoi(getenv("NX_ENC_ALIAS")) : 0u;
         static const bool swap = getenv("NX_ENC_SWAP") ? atoi(getenv("NX_ENC_SWAP")) != 0 : true;
-        static const bool spec = getenv("NX_ENC_SPEC") ? atoi(getenv("NX_ENC_SPEC")) != 0 : false;
-        auto kern = swap ? (spec ? nx::enc::k_snappy_encode<true, true> : nx::enc::k_snappy_encode<true, false>)
-                         : (spec ? nx::enc::k_snappy_encode<false, true> : nx::enc::k_snappy_encode<false, false>);
-        hipLaunchKernelGGL(kern, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
+        hipLaunchKernelGGL(swap ? nx::enc::k_snappy_encode<true> : nx::enc::k_snappy_encode<false>, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
                            in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp, alias);
         NX_HIP_CHECK(hipGetLastError());
         W.stamp += iters;
