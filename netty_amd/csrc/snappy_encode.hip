@@ -162,12 +162,23 @@ struct StreamWin {
         const uint32_t q = (uint32_t)p + pad;
         uint32_t off = q - wb;
         if (off > 27u) {
-            wb = q & ~15u;
-            const uint4 x = *reinterpret_cast<const uint4*>(origin + wb);
-            w0 = x.x; w1 = x.y; w2 = x.z; w3 = x.w;
-            if (wb + 16u < end) {
-                const uint4 y = *reinterpret_cast<const uint4*>(origin + wb + 16u);
-                w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
+            if (off < 44u) {
+                // forward by less than 16 bytes past the window: slide it one block, keeping the
+                // upper block, so each input block is loaded once on a forward scan
+                wb += 16u;
+                w0 = w4; w1 = w5; w2 = w6; w3 = w7;
+                if (wb + 16u < end) {
+                    const uint4 y = *reinterpret_cast<const uint4*>(origin + wb + 16u);
+                    w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
+                }
+            } else {
+                wb = q & ~15u;
+                const uint4 x = *reinterpret_cast<const uint4*>(origin + wb);
+                w0 = x.x; w1 = x.y; w2 = x.z; w3 = x.w;
+                if (wb + 16u < end) {
+                    const uint4 y = *reinterpret_cast<const uint4*>(origin + wb + 16u);
+                    w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
+                }
             }
             off = q - wb;
         }
