@@ -50,11 +50,13 @@ def _corpus(oracle, kat):
     return chunks
 
 
-def test_snappy_encode_parity(dev, B, oracle, kat):
+@pytest.mark.parametrize("in_align,out_align", [(16, 16), (16, 4), (1, 1)])
+def test_snappy_encode_parity(dev, B, oracle, kat, in_align, out_align):
+    """Output slots 16-aligned (16-byte staged stores), 4-aligned (dword stores) and unaligned (bytes)."""
     chunks = _corpus(oracle, kat)
-    inp, off, ln = B.pack(chunks, dev)
-    cap = [B.snappy_max_compressed_length(len(c)) for c in chunks]
-    out, ooff = B.out_slots(cap, dev)
+    inp, off, ln = B.pack(chunks, dev, align=in_align)
+    cap = [B.snappy_max_compressed_length(len(c)) + (3 if out_align == 1 else 0) for c in chunks]
+    out, ooff = B.out_slots(cap, dev, align=out_align)
     olen, st = B.snappy_encode(inp, off, ln, out, ooff)
     torch.cuda.synchronize()
     olen, st, ooff_h, outh = olen.cpu().tolist(), st.cpu().tolist(), ooff.cpu().tolist(), out.cpu().numpy().tobytes()
