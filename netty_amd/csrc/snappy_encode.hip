@@ -40,16 +40,29 @@ __device__ __forceinline__ uint32_t hash_of(uint32_t le, int shift) {
     return (__builtin_bswap32(le) * 0x1e35a7bdu) >> shift;  // hash (:177-179) on the BIG-endian getInt
 }
 
-// Output writer: bytes are packed into `acc` and leave as aligned dword stores.
-struct Writer {
+// Output writer: bytes are packed into `acc` and leave as aligned dword stores; with PAIR (8-byte
+// aligned destination) two dwords leave as one 8-byte store.
+template <bool PAIR>
+struct WriterT {
     uint32_t* w;   // next aligned dword to store
     uint32_t acc;  // pending bytes (little-endian order)
     uint32_t na;   // number of pending bytes (0..3)
     uint32_t nw;   // dwords stored
+    uint32_t s0;   // PAIR: the staged even dword
+    __device__ __forceinline__ void emit(uint32_t v) {
+        if (!PAIR) {
+            w[nw] = v;
+        } else if (nw & 1u) {
+            *reinterpret_cast<uint2*>(w + nw - 1u) = make_uint2(s0, v);
+        } else {
+            s0 = v;
+        }
+        ++nw;
+    }
     __device__ __forceinline__ void put(uint32_t b) {
         acc |= b << (8 * na);
         if (++na == 4) {
-            w[nw++] = acc;
+            emit(acc);
             acc = 0;
             na = 0;
         }
@@ -59,9 +72,9 @@ struct Writer {
         while (n >= 4) {
             const uint32_t v = ld32(p);
             if (na == 0) {
-                w[nw++] = v;
+                emit(v);
             } else {
-                w[nw++] = acc | (v << (8 * na));
+                emit(acc | (v << (8 * na)));
                 acc = v >> (32 - 8 * na);
             }
             p += 4;
@@ -71,6 +84,7 @@ struct Writer {
     }
     __device__ __forceinline__ uint32_t pos() const { return nw * 4 + na; }
     __device__ __forceinline__ void finish() {
+        if (PAIR && (nw & 1u)) w[nw - 1u] = s0;
         uint8_t* t = reinterpret_cast<uint8_t*>(w + nw);
         for (uint32_t i = 0; i < na; ++i) t[i] = (uint8_t)(acc >> (8 * i));
     }
@@ -311,7 +325,13 @@ done:
 }
 
 template <bool SWAP>
-__global__ void __launch_bounds__(256, 8) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+#ifndef NX_ENC_PAIR
+#define NX_ENC_PAIR 1
+#endif
+#ifndef NX_ENC_MINBLK
+#define NX_ENC_MINBLK 6
+#endif
+__global__ void __launch_bounds__(256, NX_ENC_MINBLK) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                        const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
                                                        int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
@@ -332,8 +352,11 @@ __global__ void __launch_bounds__(256, 8) k_snappy_encode(const uint8_t* __restr
         uint8_t* o = out + out_off[c];
         uint32_t olen;
         const uint8_t* src = in + in_off[c];
-        if ((((uintptr_t)o) & 3u) == 0) {
-            Writer w{reinterpret_cast<uint32_t*>(o), 0, 0, 0};
+        if ((((uintptr_t)o) & 7u) == 0 && NX_ENC_PAIR) {
+            WriterT<true> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
+            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
+        } else if ((((uintptr_t)o) & 3u) == 0) {
+            WriterT<false> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
             olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
         } else {
             ByteWriter w{o, 0};
