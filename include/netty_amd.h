@@ -149,6 +149,13 @@ int32_t nx_lzf_decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
                             uint8_t* out, const uint64_t* out_off, const uint32_t* out_len,
                             int32_t* status, uint32_t n, void* stream);
 
+/* Replaces LZ4FastDecompressor.decompress as Lz4FrameDecoder.decode calls it for one
+ * BLOCK_TYPE_COMPRESSED block (Lz4FrameDecoder.java:199-208; lz4-java 1.8.0, third-party, parity
+ * unpinned): block i = in[in_off[i] .. +in_len[i]) must decode to exactly out_len[i] bytes at
+ * out + out_off[i].  status NX_OK / NX_ERR_LZ4_MALFORMED.  Same parse/expand kernels as Snappy. */
+int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                            const uint64_t* out_off, const uint32_t* out_len, int32_t* status, uint32_t n, void* stream);
+
 /* Bench/test data: the text-like generator of include/netty_amd_textgen.h on the device.
  * Chunk k (global index first_chunk + k) is written to out + k*chunk_len. */
 int32_t nx_textgen_device(uint8_t* out, uint64_t first_chunk, uint32_t n_chunks, uint32_t chunk_len,

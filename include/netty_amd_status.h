@@ -47,6 +47,12 @@
  * LzfDecoder.java:120-122,134-137).  The handle's err_msg carries the reference message. */
 #define NX_ERR_FRAME_CORRUPT              (-40)
 
+/* Lz4FrameDecoder.java:203-217: the LZ4 decompressor's LZ4Exception ("Malformed input at %d",
+ * lz4-java 1.8.0, third-party) → DecompressionException.  Raised for a block that reads past its
+ * input, copies from before the output start (offset 0 or > bytes produced), or does not produce
+ * exactly the frame's decompressedLength. */
+#define NX_ERR_LZ4_MALFORMED              (-50)
+
 /* Device frame scan (nx_snappy_frame_scan_batch), one code per SnappyFrameDecoder throw site: */
 /* :116-118  "Unexpected length of stream identifier: %d" */
 #define NX_ERR_SNAPPY_STREAM_ID_LENGTH        (-41)

@@ -44,6 +44,7 @@ _SIGS = {
     "nx_adler32_batch": (i32, [vp, vp, vp, vp, u32, vp]),
     "nx_lzf_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_lzf_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
+    "nx_lz4_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_textgen_device": (i32, [vp, u64, u32, u32, vp]),
     "nx_pack_batch": (i32, [vp, vp, vp, vp, vp, u32, vp]),
     "nx_device_alloc": (vp, [sz]),

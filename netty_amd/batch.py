@@ -148,6 +148,15 @@ def lzf_decode(inp, in_off, in_len, out, out_off, out_len):
     return status
 
 
+def lz4_decode(inp, in_off, in_len, out, out_off, out_len):
+    """LZ4 block decode per chunk to exactly out_len[i] bytes (nx_lz4_decode_batch).  Returns status."""
+    n = in_len.numel()
+    status = torch.empty(n, dtype=torch.int32, device=inp.device)
+    _chk(_lib.load().nx_lz4_decode_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_len),
+                                         _ptr(status), n, _stream()), "nx_lz4_decode_batch")
+    return status
+
+
 def textgen(out, first_chunk: int, n_chunks: int, chunk_len: int):
     """Fill out[k*chunk_len:(k+1)*chunk_len] with text-like chunk first_chunk+k."""
     _chk(_lib.load().nx_textgen_device(_ptr(out), first_chunk, n_chunks, chunk_len, _stream()), "nx_textgen_device")

@@ -29,6 +29,7 @@ extern "C" const char* nx_status_string(int32_t s) {
         case NX_ERR_SNAPPY_DECOMPRESSED_TOO_LARGE: return "Received COMPRESSED_DATA that contains uncompressed data that exceeds 65536 bytes";
         case NX_ERR_SNAPPY_CHUNK_TOO_SHORT: return "Received a data chunk shorter than its checksum";
         case NX_ERR_SNAPPY_UNSKIPPABLE: return "Found reserved unskippable chunk type";
+        case NX_ERR_LZ4_MALFORMED: return "Malformed LZ4 input";
         case NX_SCAN_LIST_FULL: return "chunk list full (call again from consumed)";
         case NX_ERR_INVALID_ARG: return "invalid argument";
         case NX_ERR_HIP: return "HIP runtime error";

@@ -896,6 +896,189 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
     }
 }
 
+// =====================================================================================
+// LZ4 blocks through the same record expander
+// =====================================================================================
+// The LZ4 block format (lz4-java 1.8.0 as Lz4FrameDecoder.java:203-208 drives it: the decompressor
+// must produce exactly decompressedLength bytes): sequences of token | literal-length extension |
+// literals | 2-byte LE offset | match-length extension (+4); the last sequence is literals only.
+// k_parse_lz4 walks a block per lane and emits the same 32-bit records as k_parse (literal runs and
+// matches split at 64 bytes: a match's bytes repeat at its distance, so the split is exact); k_expand
+// produces the bytes.  Checks (each NX_ERR_LZ4_MALFORMED, oracle/netty_oracle.c orc_lz4_decompress):
+// reading past the block, an offset of 0 or beyond the bytes produced, output past want, and a block
+// that ends with the output short of want.
+__device__ __forceinline__ uint32_t win_byte(BurstWin& win, uint32_t p) {
+    if (!win.has(p)) win.load(p);
+    return (uint32_t)win.get8(p) & 0xFFu;
+}
+
+__global__ void __launch_bounds__(kParseBlock) k_parse_lz4(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                           const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ want_a,
+                                                           uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
+                                                           uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t n) {
+    __shared__ uint32_t wins[kParseBlock * kWinDw + 4];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint32_t in_len = in_len_a[c];
+    const uint32_t want = want_a[c];
+    if (in_len >= (1u << 25) || want >= (1u << 25)) {  // literal positions need 25 bits
+        status[c] = kNeedFused;
+        return;
+    }
+    BurstWin win;
+    win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
+    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), 0, 0, 0, 0, 0};
+    uint32_t ip = 0, op = 0;
+    int32_t st = NX_OK;
+    bool fit = true;
+    for (;;) {
+        if (ip >= in_len) {  // a block ends after a literal run, never before a token
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        const uint32_t token = win_byte(win, ip++);
+        uint32_t lit = token >> 4;
+        if (lit == 15u) {
+            uint32_t b = 255u;
+            while (b == 255u && ip < in_len) {
+                b = win_byte(win, ip++);
+                lit += b;  // < 15 + 255 * 2^25: no wrap
+            }
+            if (b == 255u) {
+                st = NX_ERR_LZ4_MALFORMED;
+                break;
+            }
+        }
+        if (lit > in_len - ip || lit > want - op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        for (uint32_t k = 0; k < lit && fit; k += 64u) {
+            const uint32_t m = lit - k < 64u ? lit - k : 64u;
+            fit = rw.put(((m - 1u) << 25) | (ip + k));
+        }
+        if (!fit) break;
+        ip += lit;
+        op += lit;
+        if (ip == in_len) break;  // the last sequence
+        if (in_len - ip < 2u) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        const uint32_t off = win_byte(win, ip) | (win_byte(win, ip + 1u) << 8);
+        ip += 2u;
+        if (off == 0u || off > op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        uint32_t ml = token & 15u;
+        if (ml == 15u) {
+            uint32_t b = 255u;
+            while (b == 255u && ip < in_len) {
+                b = win_byte(win, ip++);
+                ml += b;
+            }
+            if (b == 255u) {
+                st = NX_ERR_LZ4_MALFORMED;
+                break;
+            }
+        }
+        ml += 4u;
+        if (ml > want - op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        for (uint32_t k = 0; k < ml && fit; k += 64u) {
+            const uint32_t m = ml - k < 64u ? ml - k : 64u;
+            fit = rw.put(0x80000000u | ((m - 1u) << 25) | off);
+        }
+        if (!fit) break;
+        op += ml;
+    }
+    if (!fit) {
+        status[c] = kNeedFused;
+        return;
+    }
+    if (st == NX_OK && op != want) st = NX_ERR_LZ4_MALFORMED;
+    rw.finish();
+    nrec[c] = rw.n;
+    out_len[c] = op;
+    status[c] = st;
+}
+
+// Blocks k_parse_lz4 could not slot (more than kRecCap records, or >= 32 MiB): one lane decodes the
+// block byte by byte, same checks.
+__global__ void __launch_bounds__(256) k_lz4_serial(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                    const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ want_a,
+                                                    uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                                    int32_t* __restrict__ status, uint32_t n) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n || status[c] != kNeedFused) return;
+    const uint8_t* s = in + in_off[c];
+    uint8_t* d = out + out_off[c];
+    const uint64_t in_len = in_len_a[c], want = want_a[c];
+    uint64_t ip = 0, op = 0;
+    int32_t st = NX_OK;
+    for (;;) {
+        if (ip >= in_len) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        const uint32_t token = s[ip++];
+        uint64_t lit = token >> 4;
+        if (lit == 15u) {
+            uint32_t b = 255u;
+            while (b == 255u && ip < in_len) {
+                b = s[ip++];
+                lit += b;
+            }
+            if (b == 255u) {
+                st = NX_ERR_LZ4_MALFORMED;
+                break;
+            }
+        }
+        if (lit > in_len - ip || lit > want - op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        for (uint64_t k = 0; k < lit; ++k) d[op + k] = s[ip + k];
+        ip += lit;
+        op += lit;
+        if (ip == in_len) break;
+        if (in_len - ip < 2u) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        const uint64_t off = (uint64_t)s[ip] | ((uint64_t)s[ip + 1] << 8);
+        ip += 2;
+        if (off == 0u || off > op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        uint64_t ml = token & 15u;
+        if (ml == 15u) {
+            uint32_t b = 255u;
+            while (b == 255u && ip < in_len) {
+                b = s[ip++];
+                ml += b;
+            }
+            if (b == 255u) {
+                st = NX_ERR_LZ4_MALFORMED;
+                break;
+            }
+        }
+        ml += 4u;
+        if (ml > want - op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        for (uint64_t k = 0; k < ml; ++k) d[op + k] = d[op + k - off];
+        op += ml;
+    }
+    if (st == NX_OK && op != want) st = NX_ERR_LZ4_MALFORMED;
+    status[c] = st;
+}
+
 }  // namespace dec
 }  // namespace nx
 
@@ -905,11 +1088,48 @@ namespace {
 struct DecWorkspace {
     uint32_t* rec = nullptr;
     uint32_t* nrec = nullptr;
+    uint32_t* olen = nullptr;  // LZ4: bytes produced per block (the caller's lengths are inputs)
     size_t frames = 0;
 };
 std::mutex g_dws_mu;
 std::map<std::pair<int, hipStream_t>, DecWorkspace> g_dws;
 }  // namespace
+
+// Dynamic-LDS limit of the wave kernels, set once per process.
+static hipError_t wave_kernel_attrs(size_t lds) {
+    static std::once_flag once;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [&] {
+        for (const void* k : {(const void*)nx::dec::k_decode_fused, (const void*)nx::dec::k_expand})
+            if (attr_err == hipSuccess) attr_err = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    });
+    return attr_err;
+}
+
+// The (device, stream) record workspace with room for `sb` frames; caller holds g_dws_mu.
+static hipError_t dec_workspace(int dev, hipStream_t st, uint32_t sb, DecWorkspace** out) {
+    DecWorkspace& W = g_dws[{dev, st}];
+#define NX_HIP_CHECK_E(x)                \
+    do {                                 \
+        hipError_t e_ = (x);             \
+        if (e_ != hipSuccess) return e_; \
+    } while (0)
+    if (W.rec == nullptr || W.frames < sb) {
+        if (W.rec) NX_HIP_CHECK_E(hipFree(W.rec));  // hipFree synchronises with pending work
+        if (W.nrec) NX_HIP_CHECK_E(hipFree(W.nrec));
+        if (W.olen) NX_HIP_CHECK_E(hipFree(W.olen));
+        W.rec = nullptr;
+        W.nrec = nullptr;
+        W.olen = nullptr;
+        NX_HIP_CHECK_E(hipMalloc(&W.rec, (size_t)sb * nx::dec::kRecCap * sizeof(uint32_t)));
+        NX_HIP_CHECK_E(hipMalloc(&W.nrec, (size_t)sb * sizeof(uint32_t)));
+        NX_HIP_CHECK_E(hipMalloc(&W.olen, (size_t)sb * sizeof(uint32_t)));
+        W.frames = sb;
+    }
+#undef NX_HIP_CHECK_E
+    *out = &W;
+    return hipSuccess;
+}
 
 static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
                             const uint32_t* out_cap, uint32_t* out_len, uint32_t* consumed, int32_t* status,
@@ -922,13 +1142,7 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const size_t lds = kTabBytes + kWaves * sizeof(WaveLds);
-    static std::once_flag once;
-    static hipError_t attr_err = hipSuccess;
-    std::call_once(once, [&] {
-        for (const void* k : {(const void*)k_decode_fused, (const void*)k_expand})
-            if (attr_err == hipSuccess) attr_err = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    });
-    NX_HIP_CHECK(attr_err);
+    NX_HIP_CHECK(wave_kernel_attrs(lds));
     unsigned blocks_per_cu = (unsigned)(160 * 1024 / lds);
     if (blocks_per_cu < 1) blocks_per_cu = 1;
     const hipStream_t st = (hipStream_t)stream;
@@ -945,16 +1159,9 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
     }
     const uint32_t sb = n < kSubBatch ? n : kSubBatch;
     std::lock_guard<std::mutex> lk(g_dws_mu);
-    DecWorkspace& W = g_dws[{dev, st}];
-    if (W.rec == nullptr || W.frames < sb) {
-        if (W.rec) NX_HIP_CHECK(hipFree(W.rec));  // hipFree synchronises with pending work
-        if (W.nrec) NX_HIP_CHECK(hipFree(W.nrec));
-        W.rec = nullptr;
-        W.nrec = nullptr;
-        NX_HIP_CHECK(hipMalloc(&W.rec, (size_t)sb * kRecCap * sizeof(uint32_t)));
-        NX_HIP_CHECK(hipMalloc(&W.nrec, (size_t)sb * sizeof(uint32_t)));
-        W.frames = sb;
-    }
+    DecWorkspace* Wp = nullptr;
+    NX_HIP_CHECK(dec_workspace(dev, st, sb, &Wp));
+    DecWorkspace& W = *Wp;
     for (uint32_t base = 0; base < n; base += sb) {
         const uint32_t m = n - base < sb ? n - base : sb;
         hipLaunchKernelGGL(k_parse, dim3((m + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, st, in, in_off + base, in_len + base,
@@ -990,4 +1197,44 @@ extern "C" int32_t nx_snappy_decode_batch_fused(const uint8_t* in, const uint64_
                                                 uint32_t* crc_out, uint32_t n, void* stream) {
     return decode_batch(in, in_off, in_len, out, out_off, out_cap, out_len, consumed, status, expected_masked_crc, crc_out, n, stream,
                         true);
+}
+
+// Replaces LZ4FastDecompressor.decompress as Lz4FrameDecoder.decode calls it for one
+// BLOCK_TYPE_COMPRESSED block (Lz4FrameDecoder.java:199-208): block i = in[in_off[i] .. +in_len[i])
+// must decode to exactly out_len[i] bytes at out + out_off[i].
+extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                       const uint64_t* out_off, const uint32_t* out_len, int32_t* status, uint32_t n,
+                                       void* stream) {
+    using namespace nx::dec;
+    if (n == 0) return NX_OK;
+    if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
+    if (nx::crc_tables_init() != NX_OK) return NX_ERR_HIP;
+    int dev = 0, cus = 256;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const size_t lds = kTabBytes + kWaves * sizeof(WaveLds);
+    NX_HIP_CHECK(wave_kernel_attrs(lds));
+    unsigned blocks_per_cu = (unsigned)(160 * 1024 / lds);
+    if (blocks_per_cu < 1) blocks_per_cu = 1;
+    const hipStream_t st = (hipStream_t)stream;
+    const uint64_t want = (uint64_t)cus * blocks_per_cu;
+    const uint32_t sb = n < kSubBatch ? n : kSubBatch;
+    std::lock_guard<std::mutex> lk(g_dws_mu);
+    DecWorkspace* W = nullptr;
+    NX_HIP_CHECK(dec_workspace(dev, st, sb, &W));
+    for (uint32_t base = 0; base < n; base += sb) {
+        const uint32_t m = n - base < sb ? n - base : sb;
+        const uint64_t need = (m + kWaves - 1) / kWaves;
+        hipLaunchKernelGGL(k_parse_lz4, dim3((m + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, st, in, in_off + base,
+                           in_len + base, out_len + base, W->rec, W->nrec, W->olen, status + base, m);
+        NX_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_expand, dim3((unsigned)(need < want ? need : want)), dim3(kWaves * 64), lds, st, in, in_off + base,
+                           in_len + base, out, out_off + base, W->rec, W->nrec, W->olen, status + base, nullptr, nullptr, m,
+                           nx::crc_tables_dev());
+        NX_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_lz4_serial, dim3((m + 255) / 256), dim3(256), 0, st, in, in_off + base, in_len + base, out_len + base,
+                           out, out_off + base, status + base, m);
+        NX_HIP_CHECK(hipGetLastError());
+    }
+    return NX_OK;
 }

@@ -861,6 +861,101 @@ size_t orc_lzf_frame_encode(const uint8_t* in, size_t n, int32_t compress_thresh
 #define JR_MULT 0x5DEECE66DLL
 #define JR_MASK ((1LL << 48) - 1)
 
+
+/* ================================================================== LZ4 block (parity unpinned) */
+int32_t orc_lz4_decompress(const uint8_t* in, int32_t in_len, uint8_t* out, int32_t out_len) {
+    int64_t ip = 0, op = 0;
+    for (;;) {
+        if (ip >= in_len) return NX_ERR_LZ4_MALFORMED; /* a block ends after literals, never before a token */
+        const uint32_t token = in[ip++];
+        int64_t lit = token >> 4;
+        if (lit == 15) {
+            uint32_t b;
+            do {
+                if (ip >= in_len) return NX_ERR_LZ4_MALFORMED;
+                b = in[ip++];
+                lit += b;
+            } while (b == 255);
+        }
+        if (lit > in_len - ip || lit > out_len - op) return NX_ERR_LZ4_MALFORMED;
+        memcpy(out + op, in + ip, (size_t)lit);
+        ip += lit;
+        op += lit;
+        if (ip == in_len) break; /* the last sequence */
+        if (in_len - ip < 2) return NX_ERR_LZ4_MALFORMED;
+        const int64_t off = in[ip] | (in[ip + 1] << 8);
+        ip += 2;
+        if (off == 0 || off > op) return NX_ERR_LZ4_MALFORMED;
+        int64_t ml = token & 15;
+        if (ml == 15) {
+            uint32_t b;
+            do {
+                if (ip >= in_len) return NX_ERR_LZ4_MALFORMED;
+                b = in[ip++];
+                ml += b;
+            } while (b == 255);
+        }
+        ml += 4;
+        if (ml > out_len - op) return NX_ERR_LZ4_MALFORMED;
+        for (int64_t k = 0; k < ml; ++k) out[op + k] = out[op + k - off];
+        op += ml;
+    }
+    return op == out_len ? NX_OK : NX_ERR_LZ4_MALFORMED;
+}
+
+size_t orc_lz4_max_compressed(size_t n) { return n + n / 255 + 16; }
+
+static size_t lz4_put_len(uint8_t* out, size_t op, int64_t v) { /* extension bytes of a length >= 15 */
+    v -= 15;
+    while (v >= 255) {
+        out[op++] = 255;
+        v -= 255;
+    }
+    out[op++] = (uint8_t)v;
+    return op;
+}
+
+int32_t orc_lz4_compress(const uint8_t* in, int32_t n, uint8_t* out) {
+    enum { HBITS = 12, MINMATCH = 4, LASTLITERALS = 5, MFLIMIT = 12 };
+    int32_t table[1 << HBITS];
+    for (int i = 0; i < (1 << HBITS); ++i) table[i] = -1;
+    size_t op = 0;
+    int32_t anchor = 0, ip = 0;
+    const int32_t mlimit = n - MFLIMIT;
+    while (n >= MFLIMIT + 1 && ip <= mlimit) {
+        uint32_t w;
+        memcpy(&w, in + ip, 4);
+        const uint32_t h = (w * 2654435761u) >> (32 - HBITS);
+        const int32_t ref = table[h];
+        table[h] = ip;
+        uint32_t rw = 0;
+        if (ref >= 0) memcpy(&rw, in + ref, 4);
+        if (ref < 0 || ip - ref > 65535 || rw != w) {
+            ++ip;
+            continue;
+        }
+        int32_t ml = MINMATCH;
+        while (ip + ml < n - LASTLITERALS && in[ref + ml] == in[ip + ml]) ++ml;
+        const int64_t lit = ip - anchor;
+        const size_t tok = op++;
+        out[tok] = (uint8_t)(((lit >= 15 ? 15 : lit) << 4) | ((ml - MINMATCH) >= 15 ? 15 : (ml - MINMATCH)));
+        if (lit >= 15) op = lz4_put_len(out, op, lit);
+        memcpy(out + op, in + anchor, (size_t)lit);
+        op += (size_t)lit;
+        out[op++] = (uint8_t)((ip - ref) & 255);
+        out[op++] = (uint8_t)((ip - ref) >> 8);
+        if (ml - MINMATCH >= 15) op = lz4_put_len(out, op, ml - MINMATCH);
+        ip += ml;
+        anchor = ip;
+    }
+    const int64_t lit = n - anchor; /* last literals */
+    out[op++] = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
+    if (lit >= 15) op = lz4_put_len(out, op, lit);
+    memcpy(out + op, in + anchor, (size_t)lit);
+    op += (size_t)lit;
+    return (int32_t)op;
+}
+
 int64_t orc_java_random_scramble(int64_t seed) { return (seed ^ JR_MULT) & JR_MASK; }
 
 static int32_t jr_next(int64_t* s, int bits) {

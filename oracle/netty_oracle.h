@@ -73,6 +73,18 @@ int32_t orc_lzf_compress_body(const uint8_t* in, int32_t in_len, uint8_t* out);
 size_t orc_lzf_frame_encode(const uint8_t* in, size_t n, int32_t compress_threshold, uint8_t* out);
 size_t orc_lzf_frame_max_encoded(size_t n);
 
+/* LZ4 block format (lz4-java 1.8.0, a third-party dependency absent from the reference: pom.xml
+ * 946-950; Lz4FrameDecoder.java:203-208 calls its decompressor with the exact decompressed length).
+ * Restated from the published block format: sequences of token | literal-length extension |
+ * literals | 2-byte LE offset | match-length extension (+4), the last sequence literals only.
+ * PARITY UNPINNED against lz4-java: no fixtures for it exist in the reference.
+ * orc_lz4_decompress returns NX_OK when exactly out_len bytes are produced from all in_len bytes,
+ * else NX_ERR_LZ4_MALFORMED.  orc_lz4_compress is a greedy single-probe compressor producing valid
+ * blocks for tests (last 5 bytes literals, no match starting in the last 12). */
+int32_t orc_lz4_decompress(const uint8_t* in, int32_t in_len, uint8_t* out, int32_t out_len);
+int32_t orc_lz4_compress(const uint8_t* in, int32_t n, uint8_t* out);
+size_t orc_lz4_max_compressed(size_t n);
+
 /* ---- Test data: java.util.Random restatement and the text-like generator ---- */
 void orc_java_random_bytes(int64_t seed, uint8_t* out, size_t n);
 int64_t orc_java_random_next_long(int64_t* state_seed); /* state already scrambled */

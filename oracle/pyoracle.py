@@ -28,6 +28,10 @@ def lib():
         build()
         L = C.CDLL(_LIB_PATH)
         L.orc_crc32c.restype = C.c_uint32
+        L.orc_lz4_max_compressed.restype = C.c_size_t
+        L.orc_lz4_max_compressed.argtypes = [C.c_size_t]
+        L.orc_lz4_compress.argtypes = [C.c_char_p, C.c_int32, C.c_void_p]
+        L.orc_lz4_decompress.argtypes = [C.c_char_p, C.c_int32, C.c_void_p, C.c_int32]
         L.orc_crc32c.argtypes = [C.c_char_p, C.c_size_t]
         L.orc_mask_checksum.restype = C.c_uint32
         L.orc_mask_checksum.argtypes = [C.c_uint32]
@@ -181,6 +185,21 @@ def lzf_compress_body(data: bytes) -> bytes:
 def lzf_decode_chunk(body: bytes, out_len: int):
     out = _buf(out_len)
     st = lib().orc_lzf_decode_chunk(bytes(body), len(body), out, out_len)
+    return st, bytes(out[:out_len]) if st == 0 else b""
+
+
+def lz4_compress(data: bytes) -> bytes:
+    """A valid LZ4 block for `data` (greedy test compressor; lz4-java's exact output is unpinned)."""
+    L = lib()
+    out = _buf(L.orc_lz4_max_compressed(len(data)))
+    n = L.orc_lz4_compress(bytes(data), len(data), out)
+    return bytes(out[:n])
+
+
+def lz4_decompress(block: bytes, out_len: int):
+    """(status, bytes): NX_OK and out_len bytes, or NX_ERR_LZ4_MALFORMED (-50) and b''."""
+    out = _buf(max(out_len, 1))
+    st = lib().orc_lz4_decompress(bytes(block), len(block), out, out_len)
     return st, bytes(out[:out_len]) if st == 0 else b""
 
 

@@ -1,0 +1,83 @@
+"""GPU parity: LZ4 block decode (nx_lz4_decode_batch, §8f row 4) against the oracle's restatement of
+the LZ4 block format (oracle/netty_oracle.c orc_lz4_decompress; parity against lz4-java itself is
+unpinned): bytes and status, through the same parse/expand kernels as Snappy."""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def B():
+    from netty_amd import batch
+    return batch
+
+
+def _run(B, dev, blocks, wants, align=16):
+    inp, off, ln = B.pack(blocks, dev, align=align)
+    out, ooff = B.out_slots([max(w, 1) for w in wants], dev, align=align)
+    want = torch.tensor(wants, dtype=torch.int32, device=dev)
+    st = B.lz4_decode(inp, off, ln, out, ooff, want)
+    torch.cuda.synchronize()
+    outh, oo = out.cpu().numpy().tobytes(), ooff.cpu().tolist()
+    return st.cpu().tolist(), [outh[o:o + w] for o, w in zip(oo, wants)]
+
+
+def _corpus(oracle):
+    rng = random.Random(11)
+    data = [b"a", b"hello", bytes(100), bytes(range(256)) * 3]
+    for n in (15, 16, 17, 63, 64, 65, 1000, 4096, 40000, 65536):
+        data.append(oracle.textgen_chunk(n, n))
+        data.append(bytes(rng.getrandbits(8) for _ in range(min(n, 3000))))
+    for per in (1, 2, 3, 7, 64, 65, 300):
+        data.append(bytes((i % per) * 31 & 0xFF for i in range(20000)))
+    data += [oracle.textgen_chunk(500 + i, 65536) for i in range(32)]
+    return data
+
+
+@pytest.mark.parametrize("align", [16, 1])
+def test_lz4_decode_parity(dev, B, oracle, align):
+    data = _corpus(oracle)
+    blocks = [oracle.lz4_compress(d) for d in data]
+    st, outs = _run(B, dev, blocks, [len(d) for d in data], align)
+    assert st == [0] * len(data)
+    for i, d in enumerate(data):
+        assert outs[i] == d, i
+
+
+def test_lz4_decode_malformed(dev, B, oracle):
+    cases = [(b"", 0), (b"\x50hell", 5), (b"\x50hello", 4), (b"\x50hello", 6), (b"\x10a\x00\x00\x50bcdef", 10),
+             (b"\x10a\x02\x00\x50bcdef", 10), (b"\x10a\x01", 10), (b"\xf0", 20), (b"\xf0\xff", 300),
+             (b"\x10a\x01\x00\x50bcdef", 10), (b"\x50hello", 5), (b"\x1fa\x01\x00\xff\x05\x50bcdef", 300),
+             (b"\x1fa\x01\x00\xff\x05\x50bcdef", 285)]
+    good = oracle.lz4_compress(oracle.textgen_chunk(3, 30000))
+    for cut in (1, 2, 100, len(good) // 2, len(good) - 1):
+        cases.append((good[:cut], 30000))
+    cases.append((good, 29999))
+    cases.append((good, 30001))
+    st, outs = _run(B, dev, [c for c, _ in cases], [w for _, w in cases])
+    for i, (blk, w) in enumerate(cases):
+        ost, obytes = oracle.lz4_decompress(blk, w)
+        assert st[i] == ost, (i, blk[:16], w)
+        if ost == 0:
+            assert outs[i] == obytes
+
+
+def test_lz4_record_overflow_falls_back(dev, B, oracle):
+    """A block of 20 000 one-literal + 4-byte-match sequences needs 40 000 records (> 16 384 per slot):
+    it is decoded by the lane-serial kernel, with the same result."""
+    blk = b"".join(bytes([0x10, 65 + (i % 26), 0x01, 0x00]) for i in range(20000)) + b"\x10z"
+    want = 20000 * 5 + 1
+    ost, obytes = oracle.lz4_decompress(blk, want)
+    assert ost == 0
+    st, outs = _run(B, dev, [blk, oracle.lz4_compress(b"xyz" * 1000)], [want, 3000])
+    assert st == [0, 0] and outs[0] == obytes and outs[1] == b"xyz" * 1000

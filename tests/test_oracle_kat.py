@@ -230,3 +230,21 @@ def test_snappy_frame_scan_partial_and_skip(oracle):
         assert [(t, o + c1, n, c) for t, o, n, c in e2] == [(t, o, n, c) for t, o, n, c in full[0][len(e1):]]
     e, c, s, r = oracle.snappy_frame_scan(buf, cap=1)
     assert r == oracle.SCAN_LIST_FULL and len(e) == 1 and not s & 2
+
+
+def test_lz4_block_roundtrip_and_errors(oracle):
+    """LZ4 block restatement (parity unpinned against lz4-java, see oracle/netty_oracle.h): round trips
+    and the malformed-input cases the GPU decoder must agree on."""
+    import random
+    rng = random.Random(4)
+    for data in [b"", b"a", b"hello", bytes(100), oracle.textgen_chunk(1, 65536), oracle.java_random_bytes(2, 5000),
+                 bytes((i % 7) for i in range(70000)), bytes(rng.getrandbits(8) for _ in range(300))]:
+        blk = oracle.lz4_compress(data)
+        assert oracle.lz4_decompress(blk, len(data)) == (0, data)
+    assert oracle.lz4_decompress(b"\x50hello", 5) == (0, b"hello")
+    # sequences: literal 'a' then a 4-byte match at offset 1, then the literal tail "bcdef"
+    assert oracle.lz4_decompress(b"\x10a\x01\x00\x50bcdef", 10) == (0, b"aaaaabcdef")
+    bad = [(b"", 0), (b"\x50hell", 5), (b"\x50hello", 4), (b"\x50hello", 6), (b"\x10a\x00\x00\x50bcdef", 10),
+           (b"\x10a\x02\x00\x50bcdef", 10), (b"\x10a\x01", 10), (b"\xf0", 20), (b"\xf0\xff", 300)]
+    for blk, n in bad:
+        assert oracle.lz4_decompress(blk, n)[0] == -50, (blk, n)
