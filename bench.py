@@ -245,6 +245,26 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2):
     res["lzf"] = {"encode_gib_s": round(U / te * 1e3 / 2**30, 3),
                   "decode_gib_s": round(Ud / td * 1e3 / 2**30, 3) if idx.numel() else None,
                   "decoded_chunks": int(idx.numel()), "ratio": round(int(llen.to(torch.int64).sum()) / U, 4), "verified": ok}
+    del lout
+    # LZ4 blocks (§8f row 4): GPU greedy block encoder, then decode through the parse/expand kernels
+    zcap = (B.lz4_max_compressed_length(CH) + 15) // 16 * 16
+    zout = torch.empty(n * zcap, dtype=torch.uint8, device=dev)
+    zoff = torch.arange(n, dtype=torch.int64, device=dev) * zcap
+
+    def zenc():
+        box["z"] = B.lz4_encode(src, off, ln, zout, zoff)
+
+    te = timed(zenc)
+    zlen, zst = box["z"]
+
+    def zdec():
+        box["zd"] = B.lz4_decode(zout, zoff, zlen, dec, off, ln)
+
+    td = timed(zdec)
+    ok = (int((zst != 0).sum()) == 0 and int((box["zd"] != 0).sum()) == 0
+          and all(bool(torch.equal(dec[i * CH:i * CH + int(ln[i])], src[i * CH:i * CH + int(ln[i])])) for i in (0, 1, n - 1)))
+    res["lz4"] = {"encode_gib_s": round(U / te * 1e3 / 2**30, 3), "decode_gib_s": round(U / td * 1e3 / 2**30, 3),
+                  "ratio": round(int(zlen.to(torch.int64).sum()) / U, 4), "verified": ok}
     return res
 
 

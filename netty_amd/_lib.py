@@ -45,6 +45,8 @@ _SIGS = {
     "nx_lzf_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_lzf_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_lz4_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
+    "nx_lz4_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
+    "nx_lz4_max_compressed_length": (sz, [sz]),
     "nx_textgen_device": (i32, [vp, u64, u32, u32, vp]),
     "nx_pack_batch": (i32, [vp, vp, vp, vp, vp, u32, vp]),
     "nx_device_alloc": (vp, [sz]),

@@ -148,6 +148,21 @@ def lzf_decode(inp, in_off, in_len, out, out_off, out_len):
     return status
 
 
+def lz4_max_compressed_length(n: int) -> int:
+    return _lib.load().nx_lz4_max_compressed_length(n)
+
+
+def lz4_encode(inp, in_off, in_len, out, out_off):
+    """LZ4 block encode per chunk (nx_lz4_encode_batch).  Returns (out_len, status)."""
+    n = in_len.numel()
+    dev = inp.device
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    _chk(_lib.load().nx_lz4_encode_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_len),
+                                         _ptr(status), n, _stream()), "nx_lz4_encode_batch")
+    return out_len, status
+
+
 def lz4_decode(inp, in_off, in_len, out, out_off, out_len):
     """LZ4 block decode per chunk to exactly out_len[i] bytes (nx_lz4_decode_batch).  Returns status."""
     n = in_len.numel()

@@ -81,3 +81,21 @@ def test_lz4_record_overflow_falls_back(dev, B, oracle):
     assert ost == 0
     st, outs = _run(B, dev, [blk, oracle.lz4_compress(b"xyz" * 1000)], [want, 3000])
     assert st == [0, 0] and outs[0] == obytes and outs[1] == b"xyz" * 1000
+
+
+@pytest.mark.parametrize("align", [16, 1])
+def test_lz4_encode_parity_and_roundtrip(dev, B, oracle, align):
+    """GPU encoder bytes == the oracle's greedy compressor, and GPU decode restores the input."""
+    data = _corpus(oracle) + [b"", b"abc", oracle.java_random_bytes(5, 65536)]
+    inp, off, ln = B.pack(data, dev, align=align)
+    cap = [B.lz4_max_compressed_length(len(d)) for d in data]
+    out, ooff = B.out_slots(cap, dev, align=align)
+    olen, st = B.lz4_encode(inp, off, ln, out, ooff)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [0] * len(data)
+    outh, oo, ol = out.cpu().numpy().tobytes(), ooff.cpu().tolist(), olen.cpu().tolist()
+    blocks = [outh[o:o + n] for o, n in zip(oo, ol)]
+    for i, d in enumerate(data):
+        assert blocks[i] == oracle.lz4_compress(d), i
+    st2, outs = _run(B, dev, blocks, [len(d) for d in data], align)
+    assert st2 == [0] * len(data) and outs == list(data)
