@@ -956,6 +956,52 @@ int32_t orc_lz4_compress(const uint8_t* in, int32_t n, uint8_t* out) {
     return (int32_t)op;
 }
 
+/* ---- XXHash32 (published XXH32; lz4-java XXHash32 as Lz4XXHash32.java:37-88 calls it) ---- */
+static uint32_t xxh_rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+static uint32_t xxh_le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+enum { XP1 = 0x9E3779B1u, XP2 = 0x85EBCA77u, XP3 = 0xC2B2AE3Du, XP4 = 0x27D4EB2Fu, XP5 = 0x165667B1u };
+
+uint32_t orc_xxhash32(const uint8_t* p, size_t n, uint32_t seed) {
+    size_t i = 0;
+    uint32_t h;
+    if (n >= 16) {
+        uint32_t v[4] = {seed + XP1 + XP2, seed + XP2, seed, seed - XP1};
+        for (; i + 16 <= n; i += 16)
+            for (int k = 0; k < 4; ++k) v[k] = xxh_rotl(v[k] + xxh_le32(p + i + 4 * k) * XP2, 13) * XP1;
+        h = xxh_rotl(v[0], 1) + xxh_rotl(v[1], 7) + xxh_rotl(v[2], 12) + xxh_rotl(v[3], 18);
+    } else {
+        h = seed + XP5;
+    }
+    h += (uint32_t)n;
+    for (; i + 4 <= n; i += 4) h = xxh_rotl(h + xxh_le32(p + i) * XP3, 17) * XP4;
+    for (; i < n; ++i) h = xxh_rotl(h + p[i] * XP5, 11) * XP1;
+    h ^= h >> 15;
+    h *= XP2;
+    h ^= h >> 13;
+    h *= XP3;
+    h ^= h >> 16;
+    return h;
+}
+
+size_t orc_lz4_frame_block(const uint8_t* in, int32_t n, int32_t compression_level, uint8_t* out) {
+    const uint32_t check = orc_xxhash32(in, (size_t)n, 0x9747b28cu) & 0x0FFFFFFFu; /* :250-252 */
+    int32_t clen = orc_lz4_compress(in, n, out + 21);                               /* :259-269 */
+    int32_t type = 0x20;
+    if (clen >= n) { /* :270-273 */
+        type = 0x10;
+        clen = n;
+        memcpy(out + 21, in, (size_t)n);
+    }
+    memcpy(out, "LZ4Block", 8); /* :278-282 */
+    out[8] = (uint8_t)(type | compression_level);
+    const uint32_t f[3] = {(uint32_t)clen, (uint32_t)n, check};
+    for (int k = 0; k < 3; ++k)
+        for (int b = 0; b < 4; ++b) out[9 + 4 * k + b] = (uint8_t)(f[k] >> (8 * b));
+    return 21 + (size_t)clen;
+}
+
 int64_t orc_java_random_scramble(int64_t seed) { return (seed ^ JR_MULT) & JR_MASK; }
 
 static int32_t jr_next(int64_t* s, int bits) {

@@ -85,6 +85,17 @@ int32_t orc_lz4_decompress(const uint8_t* in, int32_t in_len, uint8_t* out, int3
 int32_t orc_lz4_compress(const uint8_t* in, int32_t n, uint8_t* out);
 size_t orc_lz4_max_compressed(size_t n);
 
+/* XXHash32 (lz4-java 1.8.0 XXHash32.hash, third-party; restated from the published XXH32
+ * algorithm: four lane accumulators over 16-byte stripes, then 4-byte and 1-byte tails and the
+ * avalanche).  Pinned by Lz4FrameDecoderTest.java:33-41 ("Netty" -> 0x0F79E486 after the
+ * Lz4XXHash32.java:101 mask) and by the independent python-xxhash package in tests. */
+uint32_t orc_xxhash32(const uint8_t* p, size_t n, uint32_t seed);
+/* One Lz4FrameEncoder.flushBufferedData block (Lz4FrameEncoder.java:248-284): 21-byte header
+ * (magic "LZ4Block", token = blockType | compressionLevel, LE compressedLength, LE decompressedLength,
+ * LE checksum = XXH32(seed 0x9747b28c) & 0x0FFFFFFF) then the compressed block, or the raw bytes
+ * when compression does not shrink them.  n >= 1.  Returns bytes written (<= 21 + max_compressed). */
+size_t orc_lz4_frame_block(const uint8_t* in, int32_t n, int32_t compression_level, uint8_t* out);
+
 /* ---- Test data: java.util.Random restatement and the text-like generator ---- */
 void orc_java_random_bytes(int64_t seed, uint8_t* out, size_t n);
 int64_t orc_java_random_next_long(int64_t* state_seed); /* state already scrambled */

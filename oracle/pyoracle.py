@@ -28,6 +28,10 @@ def lib():
         build()
         L = C.CDLL(_LIB_PATH)
         L.orc_crc32c.restype = C.c_uint32
+        L.orc_xxhash32.restype = C.c_uint32
+        L.orc_xxhash32.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
+        L.orc_lz4_frame_block.restype = C.c_size_t
+        L.orc_lz4_frame_block.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_void_p]
         L.orc_lz4_max_compressed.restype = C.c_size_t
         L.orc_lz4_max_compressed.argtypes = [C.c_size_t]
         L.orc_lz4_compress.argtypes = [C.c_char_p, C.c_int32, C.c_void_p]
@@ -201,6 +205,103 @@ def lz4_decompress(block: bytes, out_len: int):
     out = _buf(max(out_len, 1))
     st = lib().orc_lz4_decompress(bytes(block), len(block), out, out_len)
     return st, bytes(out[:out_len]) if st == 0 else b""
+
+
+LZ4_MAGIC = b"LZ4Block"  # Lz4Constants.java:22-30
+LZ4_DEFAULT_SEED = 0x9747B28C  # Lz4Constants.java:70
+LZ4_ERR = {"bad_magic": -51, "compressed_length": -52, "decompressed_length": -53, "length_mismatch": -54,
+           "block_type": -55, "checksum": -56, "end_checksum": -57}
+
+
+def xxhash32(data: bytes, seed: int = LZ4_DEFAULT_SEED) -> int:
+    return lib().orc_xxhash32(bytes(data), len(data), seed & 0xFFFFFFFF)
+
+
+def lz4_checksum(data: bytes) -> int:
+    """Lz4XXHash32(DEFAULT_SEED).getValue() as the frame stores it (Lz4XXHash32.java:94-102: top nibble dropped)."""
+    return xxhash32(data) & 0x0FFFFFFF
+
+
+def lz4_compression_level(block_size: int) -> int:
+    """Lz4FrameEncoder.compressionLevel (Lz4FrameEncoder.java:158-166)."""
+    if not 64 <= block_size <= 1 << 25:
+        raise ValueError("blockSize")
+    return max(0, (block_size - 1).bit_length() - 10)
+
+
+def lz4_frame_block(data: bytes, level: int = 6) -> bytes:
+    """One Lz4FrameEncoder.flushBufferedData block (header + compressed-or-raw payload)."""
+    out = _buf(21 + lib().orc_lz4_max_compressed(len(data)))
+    n = lib().orc_lz4_frame_block(bytes(data), len(data), level, out)
+    return bytes(out[:n])
+
+
+def lz4_frame_end(level: int = 6) -> bytes:
+    """finishEncode's last empty block (Lz4FrameEncoder.java:326-335)."""
+    return LZ4_MAGIC + bytes([0x10 | level]) + bytes(12)
+
+
+def lz4_frame_encode(data: bytes, block_size: int = 1 << 16, close: bool = True) -> bytes:
+    """Lz4FrameEncoder.encode (:231-244: fill the block buffer, flush each full one) then close()
+    (:317-336: flush the rest, append the end block)."""
+    level = lz4_compression_level(block_size)
+    out = [lz4_frame_block(data[i:i + block_size], level) for i in range(0, len(data), block_size)]
+    return b"".join(out) + (lz4_frame_end(level) if close else b"")
+
+
+def lz4_frame_scan(buf: bytes, state: int = 0, cap: int | None = None):
+    """Pure-Python restatement of Lz4FrameDecoder.decode's block walk (Lz4FrameDecoder.java:121-261)
+    under ByteToMessageDecoder.callDecode.  state = finished | corrupted << 1.  Returns
+    (entries, consumed, state, status); entries = [(block_type, payload_off, compressed_len,
+    decompressed_len, stored_checksum)] in stream order.  A block whose payload is not all readable
+    yet stops the walk at its header (Java has consumed the header and waits in DECOMPRESS_DATA; the
+    header is re-read on the next call, with the same outcome)."""
+    n = len(buf)
+    finished, corrupted = bool(state & 1), bool(state & 2)
+    p, res, ents = 0, SCAN_OK, []
+    if finished or corrupted:  # :251-254
+        p = n
+    while p < n and not (finished or corrupted):
+        if n - p < 21:  # :124-126
+            break
+        h = buf[p:p + 21]
+        if h[:8] != LZ4_MAGIC:  # :127-130
+            res = LZ4_ERR["bad_magic"]
+            break
+        token = h[8]
+        level, btype = (token & 0x0F) + 10, token & 0xF0
+        clen = int.from_bytes(h[9:13], "little", signed=True)
+        if clen < 0 or clen > 1 << 25:  # :136-141
+            res = LZ4_ERR["compressed_length"]
+            break
+        dlen = int.from_bytes(h[13:17], "little", signed=True)
+        if dlen < 0 or dlen > 1 << level:  # :143-149
+            res = LZ4_ERR["decompressed_length"]
+            break
+        if (dlen == 0) != (clen == 0) or (btype == 0x10 and dlen != clen):  # :150-156
+            res = LZ4_ERR["length_mismatch"]
+            break
+        chk = int.from_bytes(h[17:21], "little")
+        if dlen == 0:  # :158-166
+            if chk != 0:
+                res = LZ4_ERR["end_checksum"]
+                break
+            p += 21
+            finished = True
+            continue
+        if n - p - 21 < clen:  # :180-182
+            break
+        if btype not in (0x10, 0x20):  # :209-213
+            res = LZ4_ERR["block_type"]
+            break
+        if cap is not None and len(ents) >= cap:
+            res = SCAN_LIST_FULL
+            break
+        ents.append((btype, p + 21, clen, dlen, chk))
+        p += 21 + clen
+    if res < 0:
+        corrupted = True  # :257-259
+    return ents, p, int(finished) | (int(corrupted) << 1), res
 
 
 def lzf_frame_encode(data: bytes, compress_threshold: int = 16) -> bytes:

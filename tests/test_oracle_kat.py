@@ -248,3 +248,71 @@ def test_lz4_block_roundtrip_and_errors(oracle):
            (b"\x10a\x02\x00\x50bcdef", 10), (b"\x10a\x01", 10), (b"\xf0", 20), (b"\xf0\xff", 300)]
     for blk, n in bad:
         assert oracle.lz4_decompress(blk, n)[0] == -50, (blk, n)
+
+
+# ---- LZ4 frame (§8f row 4): Lz4FrameEncoder / Lz4FrameDecoder / Lz4XXHash32 ----
+# Lz4FrameDecoderTest.java:33-41: "Netty" as one non-compressed block, then the end block.
+LZ4_DECODER_TEST_DATA = bytes([0x4C, 0x5A, 0x34, 0x42, 0x6C, 0x6F, 0x63, 0x6B, 0x16,
+                               0x05, 0, 0, 0, 0x05, 0, 0, 0, 0x86, 0xE4, 0x79, 0x0F,
+                               0x4E, 0x65, 0x74, 0x74, 0x79,
+                               0x4C, 0x5A, 0x34, 0x42, 0x6C, 0x6F, 0x63, 0x6B, 0x16] + [0] * 12)
+
+
+def test_xxhash32_against_independent_implementation(oracle):
+    """The XXH32 restatement equals python-xxhash (an independent implementation of the published
+    algorithm lz4-java 1.8.0 implements) on every tail length and several seeds."""
+    xxhash = pytest.importorskip("xxhash")
+    import random
+    rng = random.Random(3)
+    for n in list(range(0, 70)) + [255, 256, 1000, 4097, 65536]:
+        d = bytes(rng.getrandbits(8) for _ in range(n))
+        for seed in (0, 0x9747B28C, 0xFFFFFFFF, 1):
+            assert oracle.xxhash32(d, seed) == xxhash.xxh32_intdigest(d, seed), (n, seed)
+    assert oracle.xxhash32(b"", 0) == 0x02CC5D05
+
+
+def test_lz4_frame_encoder_matches_decoder_test_vector(oracle):
+    assert oracle.lz4_checksum(b"Netty") == 0x0F79E486
+    assert oracle.lz4_compression_level(1 << 16) == 6  # token 0x16 = NON_COMPRESSED | 6
+    assert oracle.lz4_frame_encode(b"Netty") == LZ4_DECODER_TEST_DATA
+
+
+def test_lz4_frame_scan_decoder_test_cases(oracle):
+    """Lz4FrameDecoderTest.java:50-147: each corrupted byte maps to its exception."""
+    ents, p, st, res = oracle.lz4_frame_scan(LZ4_DECODER_TEST_DATA)
+    assert (ents, p, st, res) == ([(0x10, 21, 5, 5, 0x0F79E486)], len(LZ4_DECODER_TEST_DATA), 1, 0)
+    E = oracle.LZ4_ERR
+    for idx, val, err in [(1, 0x00, "bad_magic"), (12, 0xFF, "compressed_length"), (16, 0xFF, "decompressed_length"),
+                          (13, 0x01, "length_mismatch"), (8, 0x36, "block_type"), (44, 0x01, "end_checksum")]:
+        d = bytearray(LZ4_DECODER_TEST_DATA)
+        d[idx] = val
+        ents, p, st, res = oracle.lz4_frame_scan(bytes(d))
+        assert res == E[err] and st & 2, (idx, err, res)
+    # data[17] = 0x01: "mismatching checksum" is raised by the checksum check on the decoded block
+    d = bytearray(LZ4_DECODER_TEST_DATA)
+    d[17] = 0x01
+    ents, _, _, res = oracle.lz4_frame_scan(bytes(d))
+    assert res == 0 and ents[0][4] != oracle.lz4_checksum(b"Netty")
+
+
+def test_lz4_frame_roundtrip_and_partial(oracle):
+    data = oracle.textgen_chunk(9, 200000) + oracle.java_random_bytes(2, 70000)
+    f = oracle.lz4_frame_encode(data)
+    ents, p, st, res = oracle.lz4_frame_scan(f)
+    assert res == 0 and st == 1 and p == len(f)
+    out = b""
+    for bt, off, cl, dl, chk in ents:
+        blk = f[off:off + cl]
+        dec = blk if bt == 0x10 else oracle.lz4_decompress(blk, dl)[1]
+        assert oracle.lz4_checksum(dec) == chk
+        out += dec
+    assert out == data
+    assert {e[0] for e in ents} == {0x10, 0x20}
+    # a cut inside a payload stops at that block's header; resuming from there finishes the walk
+    cut = ents[2][1] + 100
+    e1, p1, st1, r1 = oracle.lz4_frame_scan(f[:cut])
+    assert (len(e1), p1, st1, r1) == (2, ents[2][1] - 21, 0, 0)
+    e2, p2, st2, r2 = oracle.lz4_frame_scan(f[p1:], st1, cap=1)
+    assert r2 == oracle.SCAN_LIST_FULL and len(e2) == 1
+    # after the end block everything readable is discarded (FINISHED)
+    assert oracle.lz4_frame_scan(b"junk", 1) == ([], 4, 1, 0)
