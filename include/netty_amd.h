@@ -164,6 +164,44 @@ int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off, const uin
 int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                             const uint64_t* out_off, const uint32_t* out_len, int32_t* status, uint32_t n, void* stream);
 
+/* Replaces Lz4XXHash32.update + getValue (Lz4XXHash32.java:37-102; XXH32 of lz4-java 1.8.0,
+ * third-party, restated from the published algorithm): out[i] = XXH32(block i, seed), unmasked
+ * (the frame stores out[i] & 0x0FFFFFFF, :101).  Lz4FrameDecoder with validateChecksums compares it
+ * with the header's checksum (Lz4FrameDecoder.java:226-228). */
+int32_t nx_xxhash32_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t seed,
+                          uint32_t* out, uint32_t n, void* stream);
+
+/* Replaces Lz4FrameEncoder.flushBufferedData (Lz4FrameEncoder.java:248-284) for n buffered blocks:
+ * slot i = out[out_off[i] .. + 21 + nx_lz4_max_compressed_length(in_len[i])) receives the 21-byte
+ * header (magic, token = blockType | compression_level, LE compressedLength, LE decompressedLength,
+ * LE XXH32 & 0x0FFFFFFF) and the block (compressed, or raw when not smaller, :270-273).
+ * out_len[i] = bytes written (0 for an empty block, as :249).  compression_level as
+ * Lz4FrameEncoder.compressionLevel(blockSize) (:158-166): 6 for the default 64 KiB; in_len[i] <= 65536.
+ * The end block of close() (:326-335) is 21 host-written bytes. */
+int32_t nx_lz4_frame_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                  uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
+                                  int32_t compression_level, int32_t* status, uint32_t n, void* stream);
+
+/* Replaces the block walk of Lz4FrameDecoder.decode (Lz4FrameDecoder.java:121-261) under
+ * ByteToMessageDecoder.callDecode, for n device-resident cumulations (one per stream).
+ *   state[s] (in/out) — finished (bit 0) | corrupted (bit 1); 0 for a new decoder.
+ *   consumed[s] — bytes read.  A block whose payload is not all readable stops the walk at its
+ *                 header (Java has read the header and waits in DECOMPRESS_DATA; re-reading it next
+ *                 call gives the same result).  On an error: the start of the failing block.  After
+ *                 the end block: all of in_len (FINISHED discards the rest, :251-254).
+ *   status[s]   — NX_OK; NX_SCAN_LIST_FULL (call again from consumed[s]); < 0 = NX_ERR_LZ4_* header
+ *                 error (the decoder is now corrupted, :257-259).
+ * Blocks are listed as the Snappy scan lists chunks: BLOCK_TYPE_COMPRESSED at [0, counts[0]),
+ * BLOCK_TYPE_NON_COMPRESSED at [cap - counts[1], cap).  Entry k: data_off[k] = absolute payload
+ * position in `in`, comp_len / decomp_len / checksum = the header's fields, block_stream[k] = s,
+ * block_seq[k] = the block's index within stream s.  The first counts[0] entries of data_off /
+ * comp_len / decomp_len are nx_lz4_decode_batch's in_off / in_len / out_len as they stand. */
+int32_t nx_lz4_frame_scan_batch(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                                uint32_t* state, uint64_t* consumed, int32_t* status, uint64_t* data_off,
+                                uint32_t* comp_len, uint32_t* decomp_len, uint32_t* checksum,
+                                uint32_t* block_stream, uint32_t* block_seq, uint32_t* counts, uint32_t cap,
+                                uint32_t n, void* stream);
+
 /* Bench/test data: the text-like generator of include/netty_amd_textgen.h on the device.
  * Chunk k (global index first_chunk + k) is written to out + k*chunk_len. */
 int32_t nx_textgen_device(uint8_t* out, uint64_t first_chunk, uint32_t n_chunks, uint32_t chunk_len,

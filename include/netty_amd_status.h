@@ -53,6 +53,22 @@
  * exactly the frame's decompressedLength. */
 #define NX_ERR_LZ4_MALFORMED              (-50)
 
+/* Device LZ4 frame scan (nx_lz4_frame_scan_batch), one code per Lz4FrameDecoder throw site: */
+/* :127-130  "unexpected block identifier" */
+#define NX_ERR_LZ4_BAD_MAGIC              (-51)
+/* :136-141  "invalid compressedLength: %d (expected: 0-%d)" */
+#define NX_ERR_LZ4_COMPRESSED_LENGTH      (-52)
+/* :143-149  "invalid decompressedLength: %d (expected: 0-%d)" */
+#define NX_ERR_LZ4_DECOMPRESSED_LENGTH    (-53)
+/* :150-156  "stream corrupted: compressedLength(%d) and decompressedLength(%d) mismatch" */
+#define NX_ERR_LZ4_LENGTH_MISMATCH        (-54)
+/* :209-213  "unexpected blockType: %d (expected: %d or %d)" */
+#define NX_ERR_LZ4_BLOCK_TYPE             (-55)
+/* :226-228 → CompressionUtil.checkChecksum  "stream corrupted: mismatching checksum: %d (expected: %d)" */
+#define NX_ERR_LZ4_CHECKSUM_MISMATCH      (-56)
+/* :160-162  "stream corrupted: checksum error" (end block with a non-zero checksum) */
+#define NX_ERR_LZ4_END_CHECKSUM           (-57)
+
 /* Device frame scan (nx_snappy_frame_scan_batch), one code per SnappyFrameDecoder throw site: */
 /* :116-118  "Unexpected length of stream identifier: %d" */
 #define NX_ERR_SNAPPY_STREAM_ID_LENGTH        (-41)

@@ -47,6 +47,9 @@ _SIGS = {
     "nx_lz4_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_lz4_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_lz4_max_compressed_length": (sz, [sz]),
+    "nx_xxhash32_batch": (i32, [vp, vp, vp, u32, vp, u32, vp]),
+    "nx_lz4_frame_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, u32, vp]),
+    "nx_lz4_frame_scan_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, vp]),
     "nx_textgen_device": (i32, [vp, u64, u32, u32, vp]),
     "nx_pack_batch": (i32, [vp, vp, vp, vp, vp, u32, vp]),
     "nx_device_alloc": (vp, [sz]),

@@ -172,6 +172,83 @@ def lz4_decode(inp, in_off, in_len, out, out_off, out_len):
     return status
 
 
+LZ4_DEFAULT_SEED = 0x9747B28C  # Lz4Constants.java:70
+
+
+def xxhash32(inp, off, length, seed: int = LZ4_DEFAULT_SEED, out=None):
+    """XXH32 per block (nx_xxhash32_batch), unmasked; Lz4XXHash32.getValue() is this & 0x0FFFFFFF."""
+    n = length.numel()
+    out = torch.empty(n, dtype=torch.int32, device=inp.device) if out is None else out
+    _chk(_lib.load().nx_xxhash32_batch(_ptr(inp), _ptr(off), _ptr(length), seed & 0xFFFFFFFF, _ptr(out), n, _stream()),
+         "nx_xxhash32_batch")
+    return out
+
+
+def lz4_frame_encode(inp, in_off, in_len, out, out_off, compression_level: int = 6):
+    """Lz4FrameEncoder.flushBufferedData per block (nx_lz4_frame_encode_batch): header + block in each
+    out slot (capacity 21 + lz4_max_compressed_length).  Returns (out_len, status)."""
+    n = in_len.numel()
+    dev = inp.device
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    _chk(_lib.load().nx_lz4_frame_encode_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
+                                               _ptr(out_len), int(compression_level), _ptr(status), n, _stream()),
+         "nx_lz4_frame_encode_batch")
+    return out_len, status
+
+
+def lz4_frame_scan(inp, in_off, in_len, state, cap: int):
+    """Lz4FrameDecoder's block walk over device cumulations (nx_lz4_frame_scan_batch).  state: int32
+    tensor (finished | corrupted << 1), updated in place.  Returns a dict of tensors: consumed, status,
+    counts [compressed, non-compressed, claims] and the list arrays data_off, comp_len, decomp_len,
+    checksum, stream, seq (compressed at [0, counts[0]), non-compressed at [cap - counts[1], cap))."""
+    n = in_len.numel()
+    dev = inp.device
+    c = max(int(cap), 1)
+    r = {"consumed": torch.empty(n, dtype=torch.int64, device=dev),
+         "status": torch.empty(n, dtype=torch.int32, device=dev),
+         "data_off": torch.empty(c, dtype=torch.int64, device=dev),
+         "comp_len": torch.empty(c, dtype=torch.int32, device=dev),
+         "decomp_len": torch.empty(c, dtype=torch.int32, device=dev),
+         "checksum": torch.empty(c, dtype=torch.int32, device=dev),
+         "stream": torch.empty(c, dtype=torch.int32, device=dev),
+         "seq": torch.empty(c, dtype=torch.int32, device=dev),
+         "counts": torch.empty(3, dtype=torch.int32, device=dev)}
+    _chk(_lib.load().nx_lz4_frame_scan_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(state), _ptr(r["consumed"]),
+                                             _ptr(r["status"]), _ptr(r["data_off"]), _ptr(r["comp_len"]),
+                                             _ptr(r["decomp_len"]), _ptr(r["checksum"]), _ptr(r["stream"]), _ptr(r["seq"]),
+                                             _ptr(r["counts"]), int(cap), n, _stream()), "nx_lz4_frame_scan_batch")
+    return r
+
+
+def lz4_frame_decode(inp, scan: dict, cap: int, validate_checksums: bool = True):
+    """The data half of Lz4FrameDecoder.decode (Lz4FrameDecoder.java:184-229) for the blocks a scan listed:
+    compressed blocks are decoded into one output buffer (slots packed by decomp_len), non-compressed
+    blocks stay where they are in `inp` (Java's retainedSlice, :197-199).  With validate_checksums the
+    masked XXH32 of every block's bytes is compared with its header (:226-228).
+    Returns {"compressed": (out, out_off, status), "raw": (data_off, len, status)} over the two list ranges."""
+    nc, nu = (int(v) for v in scan["counts"][:2].tolist())
+    dev = inp.device
+    dl = scan["decomp_len"][:nc].to(torch.int64)
+    out_off = torch.cumsum(dl, 0) - dl
+    total = int(dl.sum().item()) if nc else 0
+    out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    st_c = lz4_decode(inp, scan["data_off"][:nc], scan["comp_len"][:nc], out, out_off, scan["decomp_len"][:nc]) if nc \
+        else torch.empty(0, dtype=torch.int32, device=dev)
+    lo = cap - nu
+    r_off, r_len = scan["data_off"][lo:cap], scan["decomp_len"][lo:cap]
+    st_u = torch.zeros(nu, dtype=torch.int32, device=dev)
+    if validate_checksums:
+        bad = torch.tensor(-56, dtype=torch.int32, device=dev)  # NX_ERR_LZ4_CHECKSUM_MISMATCH
+        if nc:
+            hc = xxhash32(out, out_off, scan["decomp_len"][:nc]) & 0x0FFFFFFF
+            st_c = torch.where((st_c == 0) & (hc != scan["checksum"][:nc]), bad, st_c)
+        if nu:
+            hu = xxhash32(inp, r_off, r_len) & 0x0FFFFFFF
+            st_u = torch.where(hu != scan["checksum"][lo:cap], bad, st_u)
+    return {"compressed": (out, out_off, st_c), "raw": (r_off, r_len, st_u)}
+
+
 def textgen(out, first_chunk: int, n_chunks: int, chunk_len: int):
     """Fill out[k*chunk_len:(k+1)*chunk_len] with text-like chunk first_chunk+k."""
     _chk(_lib.load().nx_textgen_device(_ptr(out), first_chunk, n_chunks, chunk_len, _stream()), "nx_textgen_device")

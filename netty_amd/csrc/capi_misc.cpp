@@ -7,6 +7,13 @@ extern "C" const char* nx_version(void) { return "netty_amd 0.1.0 (gfx950)"; }
 extern "C" const char* nx_status_string(int32_t s) {
     switch (s) {
         case NX_OK: return "ok";
+        case NX_ERR_LZ4_BAD_MAGIC: return "unexpected block identifier";
+        case NX_ERR_LZ4_COMPRESSED_LENGTH: return "invalid compressedLength";
+        case NX_ERR_LZ4_DECOMPRESSED_LENGTH: return "invalid decompressedLength";
+        case NX_ERR_LZ4_LENGTH_MISMATCH: return "stream corrupted: compressedLength and decompressedLength mismatch";
+        case NX_ERR_LZ4_BLOCK_TYPE: return "unexpected blockType";
+        case NX_ERR_LZ4_CHECKSUM_MISMATCH: return "stream corrupted: mismatching checksum";
+        case NX_ERR_LZ4_END_CHECKSUM: return "stream corrupted: checksum error";
         case NX_ERR_SNAPPY_PREAMBLE_TOO_LONG: return "Preamble is greater than 4 bytes";
         case NX_ERR_SNAPPY_OFFSET_ZERO: return "Offset is less than minimum permissible value";
         case NX_ERR_SNAPPY_OFFSET_NEGATIVE: return "Offset is greater than maximum value supported by this implementation";

@@ -286,8 +286,7 @@ def lz4_frame_scan(buf: bytes, state: int = 0, cap: int | None = None):
             if chk != 0:
                 res = LZ4_ERR["end_checksum"]
                 break
-            p += 21
-            finished = True
+            p, finished = n, True  # callDecode runs decode() again and FINISHED skips the rest (:251-254)
             continue
         if n - p - 21 < clen:  # :180-182
             break

@@ -1,0 +1,149 @@
+"""GPU parity for the LZ4 frame codec (§8f row 4): nx_xxhash32_batch against the oracle's XXH32
+(itself pinned by Lz4FrameDecoderTest.java:33-41 and python-xxhash), nx_lz4_frame_encode_batch
+byte-for-byte against the oracle's Lz4FrameEncoder.flushBufferedData restatement, and
+nx_lz4_frame_scan_batch + decode + checksum against the oracle's Lz4FrameDecoder walk, including the
+reference's own corrupted-stream cases (Lz4FrameDecoderTest.java:50-147)."""
+import random
+
+import pytest
+
+from tests.test_oracle_kat import LZ4_DECODER_TEST_DATA
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def B():
+    from netty_amd import batch
+    return batch
+
+
+def _blocks(oracle):
+    rng = random.Random(5)
+    data = [b"", b"a", b"Netty", bytes(15), bytes(16), bytes(range(17)), bytes(range(63)), bytes(range(64)) * 2]
+    for n in (65, 100, 1000, 4095, 40000, 65536):
+        data.append(oracle.textgen_chunk(n, n))
+        data.append(bytes(rng.getrandbits(8) for _ in range(min(n, 5000))))
+    data.append(oracle.java_random_bytes(7, 65536))
+    data += [oracle.textgen_chunk(900 + i, 65536) for i in range(16)]
+    return data
+
+
+@pytest.mark.parametrize("align", [16, 1])
+def test_xxhash32_parity(dev, B, oracle, align):
+    data = _blocks(oracle)
+    inp, off, ln = B.pack(data, dev, align=align)
+    for seed in (0, B.LZ4_DEFAULT_SEED):
+        h = B.xxhash32(inp, off, ln, seed)
+        torch.cuda.synchronize()
+        got = [v & 0xFFFFFFFF for v in h.cpu().tolist()]
+        assert got == [oracle.xxhash32(d, seed) for d in data]
+
+
+@pytest.mark.parametrize("align", [16, 1])
+def test_lz4_frame_encode_parity(dev, B, oracle, align):
+    data = _blocks(oracle)
+    inp, off, ln = B.pack(data, dev, align=align)
+    out, ooff = B.out_slots([21 + B.lz4_max_compressed_length(len(d)) for d in data], dev, align=align)
+    olen, st = B.lz4_frame_encode(inp, off, ln, out, ooff, 6)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [0] * len(data)
+    outh, oo, ol = out.cpu().numpy().tobytes(), ooff.cpu().tolist(), olen.cpu().tolist()
+    for i, d in enumerate(data):
+        want = oracle.lz4_frame_block(d, 6) if d else b""
+        assert outh[oo[i]:oo[i] + ol[i]] == want, i
+    # "Netty" alone is Lz4FrameDecoderTest's first block
+    k = data.index(b"Netty")
+    assert outh[oo[k]:oo[k] + ol[k]] + oracle.lz4_frame_end(6) == LZ4_DECODER_TEST_DATA
+
+
+def _streams(oracle):
+    s = [LZ4_DECODER_TEST_DATA]
+    for idx, val in [(1, 0x00), (12, 0xFF), (16, 0xFF), (13, 0x01), (8, 0x36), (17, 0x01), (44, 0x01)]:
+        d = bytearray(LZ4_DECODER_TEST_DATA)
+        d[idx] = val
+        s.append(bytes(d))
+    big = oracle.lz4_frame_encode(oracle.textgen_chunk(77, 300000) + oracle.java_random_bytes(3, 100000))
+    s += [big, big[:-21], big[:1000], big[:21], big[:20], b"", big + b"trailing junk", b"LZ4Block\x26" + bytes(12)]
+    s += [oracle.lz4_frame_encode(oracle.textgen_chunk(i, 10000 + 997 * i), close=bool(i & 1)) for i in range(40)]
+    return s
+
+
+def _scan_cmp(B, oracle, dev, streams, states, cap):
+    inp, off, ln = B.pack(streams, dev, align=16)
+    off64, ln64 = off.to(torch.int64), ln.to(torch.int64)
+    st = torch.tensor(states, dtype=torch.int32, device=dev)
+    r = B.lz4_frame_scan(inp, off64, ln64, st, cap)
+    torch.cuda.synchronize()
+    base = off.cpu().tolist()
+    nc, nu, _ = r["counts"].cpu().tolist()
+    lists = {k: r[k].cpu().tolist() for k in ("data_off", "comp_len", "decomp_len", "checksum", "stream", "seq")}
+    got = {}
+    for k in list(range(nc)) + list(range(cap - nu, cap)):
+        s = lists["stream"][k]
+        got.setdefault(s, []).append((lists["seq"][k], 0x20 if k < nc else 0x10, lists["data_off"][k] - base[s],
+                                      lists["comp_len"][k], lists["decomp_len"][k], lists["checksum"][k] & 0xFFFFFFFF))
+    cons, stat, stt = r["consumed"].cpu().tolist(), r["status"].cpu().tolist(), st.cpu().tolist()
+    for s, buf in enumerate(streams):
+        ents, p, ost, res = oracle.lz4_frame_scan(buf, states[s])
+        mine = [e[1:] for e in sorted(got.get(s, []))]
+        assert [e[0] for e in sorted(got.get(s, []))] == list(range(len(mine)))
+        assert (mine, cons[s], stt[s], stat[s]) == (ents, p, ost, res), s
+    return inp, r, nc, nu
+
+
+def test_lz4_frame_scan_parity(dev, B, oracle):
+    streams = _streams(oracle)
+    states = [0] * len(streams)
+    states[1] = 1  # finished decoder: everything is skipped
+    states[2] = 2  # corrupted decoder
+    _scan_cmp(B, oracle, dev, streams, states, cap=4096)
+
+
+def test_lz4_frame_scan_list_full(dev, B, oracle):
+    f = oracle.lz4_frame_encode(oracle.textgen_chunk(5, 65536 * 5))
+    inp, off, ln = B.pack([f], dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    r = B.lz4_frame_scan(inp, off.to(torch.int64), ln.to(torch.int64), st, 3)
+    torch.cuda.synchronize()
+    assert r["status"].item() == 1 and r["counts"][:2].sum().item() == 3
+    ents, p, _, _ = oracle.lz4_frame_scan(f)
+    assert r["consumed"].item() == ents[3][1] - 21
+
+
+def test_lz4_frame_scan_decode_roundtrip(dev, B, oracle):
+    """Device scan → nx_lz4_decode_batch → XXH32 verify restores every stream's bytes; a flipped stored
+    checksum (Lz4FrameDecoderTest data[17]) is reported as NX_ERR_LZ4_CHECKSUM_MISMATCH."""
+    payloads = [oracle.textgen_chunk(40 + i, 20000 + 4099 * i) + oracle.java_random_bytes(i, 3000 * (i % 3))
+                for i in range(24)]
+    streams = [oracle.lz4_frame_encode(p) for p in payloads]
+    bad = bytearray(LZ4_DECODER_TEST_DATA)
+    bad[17] = 0x01
+    streams.append(bytes(bad))
+    cap = 1024
+    inp, r, nc, nu = _scan_cmp(B, oracle, dev, streams, [0] * len(streams), cap)
+    d = B.lz4_frame_decode(inp, r, cap)
+    torch.cuda.synchronize()
+    out, oo, stc = (t.cpu() for t in d["compressed"])
+    roff, rlen, stu = (t.cpu().tolist() for t in d["raw"])
+    outh, inh = out.numpy().tobytes(), inp.cpu().numpy().tobytes()
+    pieces = {}
+    lists = {k: r[k].cpu().tolist() for k in ("stream", "seq", "decomp_len")}
+    stc, oo = stc.tolist(), oo.tolist()
+    for k in range(nc):
+        pieces[(lists["stream"][k], lists["seq"][k])] = (stc[k], outh[oo[k]:oo[k] + lists["decomp_len"][k]])
+    for j, k in enumerate(range(cap - nu, cap)):
+        pieces[(lists["stream"][k], lists["seq"][k])] = (stu[j], inh[roff[j]:roff[j] + rlen[j]])
+    for s, p in enumerate(payloads):
+        seqs = sorted(q for (t, q) in pieces if t == s)
+        assert all(pieces[(s, q)][0] == 0 for q in seqs), s
+        assert b"".join(pieces[(s, q)][1] for q in seqs) == p, s
+    assert pieces[(len(payloads), 0)][0] == -56
