@@ -267,7 +267,7 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2):
                   "ratio": round(int(zlen.to(torch.int64).sum()) / U, 4), "verified": ok}
     del zout
     # LZ4 frame (Lz4FrameEncoder / Lz4FrameDecoder with validateChecksums): XXH32, frame blocks into
-    # slots, gathered into 256 contiguous streams, then device scan -> block decode -> XXH32 verify.
+    # slots, gathered into 4096 contiguous streams (64 blocks each), then device scan -> block decode -> XXH32 verify.
     def xh():
         box["h"] = B.xxhash32(src, off, ln)
 
@@ -281,7 +281,7 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2):
 
     tfe = timed(fenc)
     fzlen, fzst = box["f"]
-    streams = 256
+    streams = max(1, min(4096, n // 64))
     packed, poff = B.gather(fz, fzoff, fzlen)
     del fz
     per = n // streams
