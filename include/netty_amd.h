@@ -281,6 +281,28 @@ void nx_lzf_decoder_free(nx_lzf_decoder* d);
 int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
                               const nx_msg** msgs, size_t* n_msgs, const char** err_msg);
 
+/* Lz4FrameEncoder(LZ4Factory.fastestInstance(), false, blockSize, new Lz4XXHash32(DEFAULT_SEED))
+ * Lz4FrameEncoder.java:140-166; blockSize in [64, 65536] (the device block encoder's limit).
+ * encode buffers a partial block (:231-248) and returns the bytes of every full block it flushed;
+ * flush() writes the partial block (:291-300); close() flushes and appends the end block (:317-336),
+ * after which encode passes bytes through (:233-239). */
+typedef struct nx_lz4_frame_encoder nx_lz4_frame_encoder;
+nx_lz4_frame_encoder* nx_lz4_frame_encoder_new(int32_t block_size);
+void nx_lz4_frame_encoder_free(nx_lz4_frame_encoder* e);
+size_t nx_lz4_frame_max_encoded_length(size_t n, int32_t block_size);
+int64_t nx_lz4_frame_encoder_encode(nx_lz4_frame_encoder* e, const uint8_t* in, size_t n, uint8_t* out, size_t out_cap);
+int64_t nx_lz4_frame_encoder_flush(nx_lz4_frame_encoder* e, uint8_t* out, size_t out_cap);
+int64_t nx_lz4_frame_encoder_close(nx_lz4_frame_encoder* e, uint8_t* out, size_t out_cap);
+
+/* Lz4FrameDecoder(validateChecksums)  Lz4FrameDecoder.java:95-261.  Returns NX_OK or the
+ * NX_ERR_LZ4_* code of the first failure (err_msg = the reference's message; the decoder is then
+ * corrupted and discards what follows, :251-259). */
+typedef struct nx_lz4_frame_decoder nx_lz4_frame_decoder;
+nx_lz4_frame_decoder* nx_lz4_frame_decoder_new(int32_t validate_checksums);
+void nx_lz4_frame_decoder_free(nx_lz4_frame_decoder* d);
+int32_t nx_lz4_frame_decoder_decode(nx_lz4_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
+                                    const nx_msg** msgs, size_t* n_msgs, const char** err_msg);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,7 +1,7 @@
 """netty_amd — MI355X-native (gfx950 HIP) implementation of Netty's codec-compression hot path.
 
-Snappy (block + framing, masked CRC32C), FastLZ (level 1/2 + framing, Adler32) and LZF
-codecs, with the per-chunk arithmetic in hand-written HIP kernels (libnetty_amd.so) behind
+Snappy (block + framing, masked CRC32C), FastLZ (level 1/2 + framing, Adler32), LZF and LZ4
+(block + framing, XXHash32) codecs, with the per-chunk arithmetic in hand-written HIP kernels (libnetty_amd.so) behind
 the reference's handler API (see ``netty_amd.handlers``) and a device-resident batch API
 (``netty_amd.batch``).  The C-ABI is declared in ``include/netty_amd.h``.
 """
@@ -14,6 +14,8 @@ from .handlers import (  # noqa: F401
     EncoderException,
     FastLzFrameDecoder,
     FastLzFrameEncoder,
+    Lz4FrameDecoder,
+    Lz4FrameEncoder,
     LzfDecoder,
     LzfEncoder,
     SnappyFrameDecoder,

@@ -78,6 +78,16 @@ _SIGS = {
     "nx_lzf_encoder_free": (None, [vp]),
     "nx_lzf_frame_max_encoded_length": (sz, [sz]),
     "nx_lzf_encoder_encode": (i64, [vp, C.c_char_p, sz, vp, sz]),
+    "nx_lz4_frame_encoder_new": (vp, [i32]),
+    "nx_lz4_frame_encoder_free": (None, [vp]),
+    "nx_lz4_frame_max_encoded_length": (sz, [sz, i32]),
+    "nx_lz4_frame_encoder_encode": (i64, [vp, C.c_char_p, sz, vp, sz]),
+    "nx_lz4_frame_encoder_flush": (i64, [vp, vp, sz]),
+    "nx_lz4_frame_encoder_close": (i64, [vp, vp, sz]),
+    "nx_lz4_frame_decoder_new": (vp, [i32]),
+    "nx_lz4_frame_decoder_free": (None, [vp]),
+    "nx_lz4_frame_decoder_decode": (i32, [vp, C.c_char_p, sz, C.POINTER(sz), C.POINTER(C.POINTER(NxMsg)),
+                                         C.POINTER(sz), C.POINTER(C.c_char_p)]),
     "nx_lzf_decoder_new": (vp, []),
     "nx_lzf_decoder_free": (None, [vp]),
     "nx_lzf_decoder_decode": (i32, [vp, C.c_char_p, sz, C.POINTER(sz), C.POINTER(C.POINTER(NxMsg)),

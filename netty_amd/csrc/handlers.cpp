@@ -1014,3 +1014,354 @@ extern "C" int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, s
     d->isCompressed = isCompressed;
     return finish(NX_OK);
 }
+
+// ======================================================================= LZ4 frame encoder / decoder
+//   Lz4FrameEncoder   Lz4FrameEncoder.java:231-336 (encode, flushBufferedData, finishEncode)
+//   Lz4FrameDecoder   Lz4FrameDecoder.java:121-261
+// Every full block of one encode() call (and every block of one decode() call) goes to the GPU in
+// one batch: nx_lz4_frame_encode_batch / nx_lz4_decode_batch + nx_xxhash32_batch.
+namespace {
+const uint8_t kLz4Magic[8] = {'L', 'Z', '4', 'B', 'l', 'o', 'c', 'k'};
+constexpr uint32_t kLz4Header = 21;
+constexpr uint32_t kLz4Seed = 0x9747b28cu;  // Lz4Constants.java:70
+}  // namespace
+
+struct nx_lz4_frame_encoder {
+    Gpu g;
+    uint32_t block_size = 65536;
+    int32_t level = 6;
+    bool finished = false;
+    std::vector<uint8_t> buf;  // the block buffer (Lz4FrameEncoder.java:221-226)
+};
+
+extern "C" nx_lz4_frame_encoder* nx_lz4_frame_encoder_new(int32_t block_size) {
+    // compressionLevel(blockSize) :158-166; the device block encoder takes blocks of <= 64 KiB
+    if (block_size < 64 || block_size > 65536) return nullptr;
+    auto* e = new nx_lz4_frame_encoder();
+    if (!e->g.ok) {
+        delete e;
+        return nullptr;
+    }
+    e->block_size = (uint32_t)block_size;
+    const int32_t ceil_log2 = 32 - __builtin_clz((uint32_t)block_size - 1u);
+    e->level = ceil_log2 - 10 > 0 ? ceil_log2 - 10 : 0;
+    e->buf.reserve(block_size);
+    return e;
+}
+extern "C" void nx_lz4_frame_encoder_free(nx_lz4_frame_encoder* e) { delete e; }
+extern "C" size_t nx_lz4_frame_max_encoded_length(size_t n, int32_t block_size) {
+    const size_t bs = block_size > 0 ? (size_t)block_size : 65536;
+    return (n / bs + 2) * (kLz4Header + 16 + bs / 255) + n + kLz4Header;
+}
+
+namespace {
+// flushBufferedData (:248-284) for nb consecutive blocks of `src` (the last may be short).
+int64_t lz4_flush_blocks(nx_lz4_frame_encoder* e, const uint8_t* src, size_t n, uint8_t* out, size_t out_cap) {
+    if (n == 0) return 0;
+    const uint32_t bs = e->block_size;
+    const uint32_t nb = (uint32_t)((n + bs - 1) / bs);
+    std::vector<uint64_t> ioff(nb), ooff(nb);
+    std::vector<uint32_t> ilen(nb);
+    uint64_t oc = 0;
+    for (uint32_t i = 0; i < nb; ++i) {
+        ioff[i] = (uint64_t)i * bs;
+        ilen[i] = (uint32_t)((n - ioff[i]) < bs ? (n - ioff[i]) : bs);
+        ooff[i] = oc;
+        oc += kLz4Header + nx_lz4_max_compressed_length(ilen[i]);
+    }
+    Gpu& g = e->g;
+    if (!g.din.ensure(n) || !g.dout.ensure(oc) || !g.a0.ensure(8ull * nb) || !g.a1.ensure(8ull * nb) || !g.a2.ensure(4ull * nb) ||
+        !g.a3.ensure(4ull * nb) || !g.a4.ensure(4ull * nb))
+        return NX_ERR_HIP;
+    bool ok = g.h2d(g.din.p, src, n) && g.h2d(g.a0.p, ioff.data(), 8ull * nb) && g.h2d(g.a1.p, ooff.data(), 8ull * nb) &&
+              g.h2d(g.a2.p, ilen.data(), 4ull * nb);
+    if (!ok) return NX_ERR_HIP;
+    int32_t r = nx_lz4_frame_encode_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.dout.as<uint8_t>(),
+                                          g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), e->level, g.a4.as<int32_t>(), nb, g.s);
+    if (r != NX_OK) return r;
+    std::vector<uint32_t> olen(nb);
+    std::vector<int32_t> st(nb);
+    std::vector<uint8_t> hout(oc);
+    ok = g.d2h(olen.data(), g.a3.p, 4ull * nb) && g.d2h(st.data(), g.a4.p, 4ull * nb) && g.d2h(hout.data(), g.dout.p, oc) &&
+         g.sync();
+    if (!ok) return NX_ERR_HIP;
+    size_t op = 0;
+    for (uint32_t i = 0; i < nb; ++i) {
+        if (st[i] != NX_OK) return st[i];
+        if (op + olen[i] > out_cap) return NX_ERR_INVALID_ARG;
+        memcpy(out + op, hout.data() + ooff[i], olen[i]);
+        op += olen[i];
+    }
+    return (int64_t)op;
+}
+}  // namespace
+
+extern "C" int64_t nx_lz4_frame_encoder_encode(nx_lz4_frame_encoder* e, const uint8_t* in, size_t n, uint8_t* out,
+                                               size_t out_cap) {
+    if (!e || (!in && n)) return NX_ERR_INVALID_ARG;
+    if (e->finished) {  // :233-239 — after close() the bytes pass through
+        if (out_cap < n) return NX_ERR_INVALID_ARG;
+        if (n) memcpy(out, in, n);
+        return (int64_t)n;
+    }
+    // :241-248 — fill the block buffer; every full buffer is flushed
+    const size_t have = e->buf.size();
+    const size_t total = have + n;
+    const size_t full = total / e->block_size * e->block_size;
+    if (full == 0) {
+        e->buf.insert(e->buf.end(), in, in + n);
+        return 0;
+    }
+    std::vector<uint8_t> joined;
+    const uint8_t* src = in;
+    if (have) {
+        joined.reserve(full);
+        joined.insert(joined.end(), e->buf.begin(), e->buf.end());
+        joined.insert(joined.end(), in, in + (full - have));
+        src = joined.data();
+    }
+    const int64_t w = lz4_flush_blocks(e, src, full, out, out_cap);
+    if (w < 0) return w;
+    e->buf.assign(in + (full - have), in + n);
+    return w;
+}
+
+extern "C" int64_t nx_lz4_frame_encoder_flush(nx_lz4_frame_encoder* e, uint8_t* out, size_t out_cap) {
+    if (!e) return NX_ERR_INVALID_ARG;  // flush() :291-300
+    const int64_t w = lz4_flush_blocks(e, e->buf.data(), e->buf.size(), out, out_cap);
+    if (w >= 0) e->buf.clear();
+    return w;
+}
+
+extern "C" int64_t nx_lz4_frame_encoder_close(nx_lz4_frame_encoder* e, uint8_t* out, size_t out_cap) {
+    if (!e) return NX_ERR_INVALID_ARG;
+    if (e->finished) return 0;  // finishEncode :318-321
+    const int64_t w = nx_lz4_frame_encoder_flush(e, out, out_cap);
+    if (w < 0) return w;
+    if ((size_t)w + kLz4Header > out_cap) return NX_ERR_INVALID_ARG;
+    uint8_t* f = out + w;  // the end block :326-335
+    memcpy(f, kLz4Magic, 8);
+    f[8] = (uint8_t)(0x10 | e->level);
+    memset(f + 9, 0, 12);
+    e->finished = true;
+    return w + kLz4Header;
+}
+
+struct nx_lz4_frame_decoder {
+    Gpu g;
+    bool validate = false;
+    int state = 0;  // 0 INIT_BLOCK, 1 DECOMPRESS_DATA, 2 FINISHED, 3 CORRUPTED
+    uint32_t blockType = 0, compressedLength = 0, decompressedLength = 0, currentChecksum = 0;
+    MsgList ml;
+};
+
+extern "C" nx_lz4_frame_decoder* nx_lz4_frame_decoder_new(int32_t validate_checksums) {
+    auto* d = new nx_lz4_frame_decoder();
+    if (!d->g.ok) {
+        delete d;
+        return nullptr;
+    }
+    d->validate = validate_checksums != 0;
+    return d;
+}
+extern "C" void nx_lz4_frame_decoder_free(nx_lz4_frame_decoder* d) { delete d; }
+
+extern "C" int32_t nx_lz4_frame_decoder_decode(nx_lz4_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
+                                               const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {
+    if (!d || (!in && n) || !consumed || !msgs || !n_msgs) return NX_ERR_INVALID_ARG;
+    MsgList& ml = d->ml;
+    ml.clear();
+    size_t rd = 0;
+    auto finish = [&](int32_t r) {
+        *consumed = rd;
+        *msgs = ml.msgs.data();
+        *n_msgs = ml.msgs.size();
+        if (err_msg) *err_msg = ml.err.empty() ? nullptr : ml.err.c_str();
+        return r;
+    };
+    if (d->state >= 2) {  // FINISHED / CORRUPTED :251-254
+        rd = n;
+        return finish(NX_OK);
+    }
+    struct Blk {
+        size_t data, end;
+        uint32_t type, clen, dlen, chk;
+        int job;
+    };
+    std::vector<Blk> blks;
+    int state = d->state;
+    uint32_t blockType = d->blockType, clen = d->compressedLength, dlen = d->decompressedLength, chk = d->currentChecksum;
+    size_t p = 0;
+    std::string perr;
+    int32_t perr_code = NX_OK;
+    size_t perr_at = 0;
+    char mbuf[160];
+    auto fail = [&](int32_t code, const char* msg, size_t at) {
+        perr = msg;
+        perr_code = code;
+        perr_at = at;
+    };
+    while (perr_code == NX_OK && state < 2) {
+        if (state == 0) {
+            if (n - p < kLz4Header) break;  // :124-126
+            const uint8_t* h = in + p;
+            if (memcmp(h, kLz4Magic, 8) != 0) {  // :127-130
+                fail(NX_ERR_LZ4_BAD_MAGIC, "unexpected block identifier", p + 8);
+                break;
+            }
+            const uint32_t token = h[8];
+            const uint32_t level = (token & 0x0Fu) + 10u;
+            blockType = token & 0xF0u;
+            const int32_t c = (int32_t)le32(h + 9), u = (int32_t)le32(h + 13);
+            if (c < 0 || c > (1 << 25)) {  // :136-141
+                snprintf(mbuf, sizeof mbuf, "invalid compressedLength: %d (expected: 0-%d)", c, 1 << 25);
+                fail(NX_ERR_LZ4_COMPRESSED_LENGTH, mbuf, p + 13);
+                break;
+            }
+            const int64_t maxd = (int64_t)1 << level;
+            if (u < 0 || u > maxd) {  // :143-149
+                snprintf(mbuf, sizeof mbuf, "invalid decompressedLength: %d (expected: 0-%lld)", u, (long long)maxd);
+                fail(NX_ERR_LZ4_DECOMPRESSED_LENGTH, mbuf, p + 17);
+                break;
+            }
+            if ((u == 0) != (c == 0) || (blockType == 0x10u && u != c)) {  // :150-156
+                snprintf(mbuf, sizeof mbuf, "stream corrupted: compressedLength(%d) and decompressedLength(%d) mismatch", c, u);
+                fail(NX_ERR_LZ4_LENGTH_MISMATCH, mbuf, p + 17);
+                break;
+            }
+            chk = le32(h + 17);
+            p += kLz4Header;
+            clen = (uint32_t)c;
+            dlen = (uint32_t)u;
+            if (u == 0) {  // :158-166
+                if (chk != 0u) {
+                    fail(NX_ERR_LZ4_END_CHECKSUM, "stream corrupted: checksum error", p);
+                    break;
+                }
+                state = 2;
+                p = n;  // callDecode runs decode() again; FINISHED skips the rest
+                break;
+            }
+            state = 1;
+        }
+        if (state == 1) {
+            if (n - p < clen) break;  // :180-182
+            if (blockType != 0x10u && blockType != 0x20u) {  // :209-213
+                snprintf(mbuf, sizeof mbuf, "unexpected blockType: %u (expected: %d or %d)", blockType, 0x10, 0x20);
+                fail(NX_ERR_LZ4_BLOCK_TYPE, mbuf, p);
+                break;
+            }
+            blks.push_back({p, p + clen, blockType, clen, dlen, chk, -1});
+            p += clen;
+            state = 0;
+        }
+    }
+    // GPU: decode the compressed blocks; hash every block's bytes when validating
+    uint32_t nz = 0;
+    uint64_t ocap = 0;
+    std::vector<uint64_t> ooff;
+    for (auto& b : blks)
+        if (b.type == 0x20u) {
+            b.job = (int)nz++;
+            ooff.push_back(ocap);
+            ocap += ((uint64_t)b.dlen + 15) & ~15ull;
+        }
+    const uint32_t nb = (uint32_t)blks.size();
+    std::vector<int32_t> st(nz);
+    std::vector<uint32_t> hz(nz), hr(nb);
+    std::vector<uint8_t> hout(ocap);
+    Gpu& g = d->g;
+    if (nb) {
+        const size_t lo = blks.front().data, span = blks.back().end - lo;
+        std::vector<uint64_t> ioff(nz), roff(nb);
+        std::vector<uint32_t> ilen(nz), olen(nz), rlen(nb);
+        for (uint32_t k = 0; k < nb; ++k) {
+            const Blk& b = blks[k];
+            roff[k] = b.data - lo;
+            rlen[k] = b.type == 0x10u ? b.clen : 0u;
+            if (b.job >= 0) {
+                ioff[b.job] = b.data - lo;
+                ilen[b.job] = b.clen;
+                olen[b.job] = b.dlen;
+            }
+        }
+        if (!g.din.ensure(span + 1) || !g.dout.ensure(ocap + 16) || !g.a0.ensure(8ull * nb) || !g.a1.ensure(8ull * nb) ||
+            !g.a2.ensure(4ull * nb) || !g.a3.ensure(4ull * nb) || !g.a4.ensure(4ull * nb) || !g.a5.ensure(4ull * nb) ||
+            !g.a6.ensure(4ull * nb))
+            return finish(NX_ERR_HIP);
+        bool ok = g.h2d(g.din.p, in + lo, span);
+        if (nz)
+            ok = ok && g.h2d(g.a0.p, ioff.data(), 8ull * nz) && g.h2d(g.a1.p, ooff.data(), 8ull * nz) &&
+                 g.h2d(g.a2.p, ilen.data(), 4ull * nz) && g.h2d(g.a3.p, olen.data(), 4ull * nz);
+        if (!ok) return finish(NX_ERR_HIP);
+        if (nz) {
+            int32_t r = nx_lz4_decode_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.dout.as<uint8_t>(),
+                                            g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), g.a4.as<int32_t>(), nz, g.s);
+            if (r != NX_OK) return finish(r);
+            if (d->validate) {
+                r = nx_xxhash32_batch(g.dout.as<uint8_t>(), g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), kLz4Seed, g.a5.as<uint32_t>(),
+                                      nz, g.s);
+                if (r != NX_OK) return finish(r);
+                ok = g.d2h(hz.data(), g.a5.p, 4ull * nz);
+            }
+            ok = ok && g.d2h(st.data(), g.a4.p, 4ull * nz) && g.d2h(hout.data(), g.dout.p, ocap);
+        }
+        if (ok && d->validate) {  // non-compressed blocks are hashed where they lie (retainedSlice :197-199)
+            ok = g.sync() && g.h2d(g.a0.p, roff.data(), 8ull * nb) && g.h2d(g.a2.p, rlen.data(), 4ull * nb);
+            if (ok) {
+                int32_t r = nx_xxhash32_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), kLz4Seed,
+                                              g.a6.as<uint32_t>(), nb, g.s);
+                if (r != NX_OK) return finish(r);
+                ok = g.d2h(hr.data(), g.a6.p, 4ull * nb);
+            }
+        }
+        ok = ok && g.sync();
+        if (!ok) return finish(NX_ERR_HIP);
+    }
+    for (uint32_t k = 0; k < nb; ++k) {
+        const Blk& b = blks[k];
+        const uint8_t* data;
+        if (b.job >= 0) {
+            if (st[b.job] != NX_OK) {  // LZ4Exception → DecompressionException (:218-219)
+                ml.err = "LZ4 block decompression failed: malformed input";
+                d->state = 3;
+                rd = b.data;
+                return finish(st[b.job]);
+            }
+            data = hout.data() + ooff[b.job];
+        } else {
+            data = in + b.data;
+        }
+        if (d->validate) {  // CompressionUtil.checkChecksum (:226-228; Lz4XXHash32.getValue masks, :101)
+            const uint32_t got = (b.job >= 0 ? hz[b.job] : hr[k]) & 0x0FFFFFFFu;
+            if (got != b.chk) {
+                snprintf(mbuf, sizeof mbuf, "stream corrupted: mismatching checksum: %d (expected: %d)", (int32_t)got,
+                         (int32_t)b.chk);
+                ml.err = mbuf;
+                d->state = 3;
+                rd = b.end;
+                return finish(NX_ERR_LZ4_CHECKSUM_MISMATCH);
+            }
+        }
+        if (b.job >= 0) {
+            ml.owned.emplace_back(data, data + b.dlen);
+            ml.msgs.push_back({ml.owned.back().data(), b.dlen});
+        } else {
+            ml.msgs.push_back({in + b.data, b.dlen});
+        }
+        rd = b.end;
+    }
+    if (perr_code != NX_OK) {
+        ml.err = perr;
+        d->state = 3;
+        rd = perr_at;
+        return finish(perr_code);
+    }
+    rd = p;
+    d->state = state;
+    d->blockType = blockType;
+    d->compressedLength = clen;
+    d->decompressedLength = dlen;
+    d->currentChecksum = chk;
+    return finish(NX_OK);
+}

@@ -227,6 +227,52 @@ class LzfDecoder(_Decoder):
         self._h = _new(_lib.load().nx_lzf_decoder_new(), "LzfDecoder")
 
 
+class Lz4FrameEncoder(_Encoder):
+    """Lz4FrameEncoder.java:61-403 (fast compressor, XXHash32 seed 0x9747b28c).  encode() returns the
+    full blocks it flushed (a partial block stays buffered, :231-248); flush() writes the partial
+    block (:291-300); finish_encode() = close(): flush + end block (:317-336)."""
+
+    _free = "nx_lz4_frame_encoder_free"
+
+    def __init__(self, block_size: int = 1 << 16):
+        if not 64 <= block_size <= 1 << 25:
+            raise ValueError(f"blockSize: {block_size} (expected: 64-{1 << 25})")
+        self.block_size = block_size
+        self._h = _new(_lib.load().nx_lz4_frame_encoder_new(block_size), "Lz4FrameEncoder")
+
+    def _out(self, n: int):
+        cap = _lib.load().nx_lz4_frame_max_encoded_length(n, self.block_size)
+        return (C.c_uint8 * cap)(), cap
+
+    def _ret(self, r, out) -> bytes:
+        if r < 0:
+            raise CompressionException(_lib.status_string(r))
+        return bytes(out[:r])
+
+    def encode(self, data: bytes) -> bytes:
+        out, cap = self._out(len(data) + self.block_size)
+        return self._ret(_lib.load().nx_lz4_frame_encoder_encode(self._h, data, len(data), out, cap), out)
+
+    def flush(self) -> bytes:
+        out, cap = self._out(self.block_size)
+        return self._ret(_lib.load().nx_lz4_frame_encoder_flush(self._h, out, cap), out)
+
+    def finish_encode(self) -> bytes:
+        out, cap = self._out(self.block_size)
+        return self._ret(_lib.load().nx_lz4_frame_encoder_close(self._h, out, cap), out)
+
+
+class Lz4FrameDecoder(_Decoder):
+    """Lz4FrameDecoder.java:36-277 (validateChecksums default false, :100-102)."""
+
+    _free = "nx_lz4_frame_decoder_free"
+    _decode_fn = "nx_lz4_frame_decoder_decode"
+
+    def __init__(self, validate_checksums: bool = False):
+        super().__init__()
+        self._h = _new(_lib.load().nx_lz4_frame_decoder_new(int(validate_checksums)), "Lz4FrameDecoder")
+
+
 # ------------------------------------------------------------------------------------- harness
 class EmbeddedChannel:
     """The subset of io.netty.channel.embedded.EmbeddedChannel the codec tests use

@@ -226,3 +226,78 @@ def test_lzf_decoder_errors(nx):
         nx.LzfDecoder().channel_read(b"ZV\x07\x00\x01x")
     with pytest.raises(nx.DecompressionException):
         nx.LzfDecoder().channel_read(b"ZV\x01\x00\x02\x00\x05" + bytes([0x20, 0x05]))
+
+
+# ---- LZ4 frame handlers (Lz4FrameEncoder / Lz4FrameDecoder over the GPU block + XXH32 kernels) ----
+def _lz4_encode_all(enc, data, step=None):
+    out = b""
+    step = step or max(len(data), 1)
+    for i in range(0, len(data), step):
+        out += enc.encode(data[i:i + step])
+    return out + enc.finish_encode()
+
+
+@pytest.mark.parametrize("validate", [False, True])
+def test_lz4_identity_and_parity(nx, oracle, kat, validate):
+    """Lz4FrameIntegrationTest (AbstractIntegrationTest.testIdentity) over the shared corpus; the
+    stream equals the oracle's Lz4FrameEncoder restatement byte for byte."""
+    for name, data in _corpus(oracle, kat).items():
+        enc, dec = nx.Lz4FrameEncoder(), nx.Lz4FrameDecoder(validate)
+        comp = _lz4_encode_all(enc, data)
+        assert comp == oracle.lz4_frame_encode(data), name
+        dch = nx.EmbeddedChannel(dec)
+        dch.write_inbound(comp)
+        assert dec.readable_bytes() == 0
+        out = b""
+        while (m := dch.read_inbound()) is not None:
+            out += m
+        assert out == data, name
+
+
+def test_lz4_decoder_test_vector_and_errors(nx):
+    """Lz4FrameDecoderTest.java:33-147 with the reference's own stream and corrupted bytes."""
+    from tests.test_oracle_kat import LZ4_DECODER_TEST_DATA as D
+    assert nx.Lz4FrameDecoder(True).channel_read(D) == [b"Netty"]
+    assert nx.Lz4FrameEncoder().encode(b"Netty") == b""  # buffered until flush / close
+    e = nx.Lz4FrameEncoder()
+    e.encode(b"Netty")
+    assert e.finish_encode() == D
+    for idx, val, msg in [(1, 0x00, "unexpected block identifier"), (12, 0xFF, "invalid compressedLength"),
+                          (16, 0xFF, "invalid decompressedLength"), (13, 0x01, "mismatch"),
+                          (8, 0x36, "unexpected blockType"), (17, 0x01, "mismatching checksum"),
+                          (44, 0x01, "checksum error")]:
+        d = bytearray(D)
+        d[idx] = val
+        with pytest.raises(nx.DecompressionException, match=msg):
+            nx.Lz4FrameDecoder(True).channel_read(bytes(d))
+    # without validateChecksums the flipped checksum is not noticed (Lz4FrameDecoder() default)
+    d = bytearray(D)
+    d[17] = 0x01
+    assert nx.Lz4FrameDecoder().channel_read(bytes(d)) == [b"Netty"]
+
+
+def test_lz4_streaming_partial_writes(nx, oracle):
+    """Small writes into the encoder's block buffer and byte-dribbled reads give the same stream and data."""
+    data = oracle.textgen_chunk(8, 200000) + oracle.java_random_bytes(4, 30000)
+    comp = _lz4_encode_all(nx.Lz4FrameEncoder(), data, step=7777)
+    assert comp == oracle.lz4_frame_encode(data)
+    dec = nx.Lz4FrameDecoder(True)
+    out = b""
+    for i in range(0, len(comp), 5003):
+        out += b"".join(dec.channel_read(comp[i:i + 5003]))
+    assert out == data and dec.readable_bytes() == 0
+    # after the end block the decoder is FINISHED and discards what follows
+    assert dec.channel_read(b"garbage") == [] and dec.readable_bytes() == 0
+
+
+def test_lz4_block_size_and_flush(nx, oracle):
+    data = oracle.textgen_chunk(12, 10000)
+    enc = nx.Lz4FrameEncoder(4096)
+    comp = enc.encode(data[:5000]) + enc.flush() + enc.encode(data[5000:]) + enc.finish_encode()
+    level = oracle.lz4_compression_level(4096)
+    want = (oracle.lz4_frame_block(data[:4096], level) + oracle.lz4_frame_block(data[4096:5000], level)
+            + oracle.lz4_frame_block(data[5000:9096], level) + oracle.lz4_frame_block(data[9096:], level)
+            + oracle.lz4_frame_end(level))
+    assert comp == want
+    assert b"".join(nx.Lz4FrameDecoder(True).channel_read(comp)) == data
+    assert enc.encode(b"raw after close") == b"raw after close"
