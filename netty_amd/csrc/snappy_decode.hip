@@ -921,7 +921,9 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lz4(const uint8_t* __rest
     if (c >= n) return;
     const uint32_t in_len = in_len_a[c];
     const uint32_t want = want_a[c];
-    if (in_len >= (1u << 25) || want >= (1u << 25)) {  // literal positions need 25 bits
+    // literal positions need 25 bits; blocks of more than 64 KiB output (Lz4FrameEncoder block sizes
+    // above the default, :158-166) go to the lane-serial kernel, which has no window limit
+    if (in_len >= (1u << 25) || want > 65536u) {
         status[c] = kNeedFused;
         return;
     }

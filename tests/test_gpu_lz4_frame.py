@@ -147,3 +147,30 @@ def test_lz4_frame_scan_decode_roundtrip(dev, B, oracle):
         assert all(pieces[(s, q)][0] == 0 for q in seqs), s
         assert b"".join(pieces[(s, q)][1] for q in seqs) == p, s
     assert pieces[(len(payloads), 0)][0] == -56
+
+
+@pytest.mark.parametrize("block_size", [1 << 18, 1 << 20])
+def test_lz4_frame_large_blocks(dev, B, oracle, block_size):
+    """Streams from an Lz4FrameEncoder with a block size above 64 KiB (compressionLevel 8 / 10):
+    blocks of more than 64 KiB output decode through the lane-serial kernel, by the scan path and by
+    the Lz4FrameDecoder handler, with checksums validated."""
+    import netty_amd as nx
+    data = oracle.textgen_chunk(61, 3 * block_size // 2) + bytes(block_size // 3) + oracle.java_random_bytes(8, 5000)
+    f = oracle.lz4_frame_encode(data, block_size=block_size)
+    assert f[8] & 0x0F == oracle.lz4_compression_level(block_size)
+    assert b"".join(nx.Lz4FrameDecoder(True).channel_read(f)) == data
+    cap = 64
+    inp, r, nc, nu = _scan_cmp(B, oracle, dev, [f], [0], cap)
+    d = B.lz4_frame_decode(inp, r, cap)
+    torch.cuda.synchronize()
+    out, oo, stc = (t.cpu() for t in d["compressed"])
+    assert stc.tolist() == [0] * nc and d["raw"][2].cpu().tolist() == [0] * nu
+    seq = r["seq"][:nc].cpu().tolist()
+    dl = r["decomp_len"][:nc].cpu().tolist()
+    outh, oo = out.numpy().tobytes(), oo.tolist()
+    got = {seq[k]: outh[oo[k]:oo[k] + dl[k]] for k in range(nc)}
+    inh = inp.cpu().numpy().tobytes()
+    for k in range(cap - nu, cap):
+        o, n = int(r["data_off"][k]), int(r["decomp_len"][k])
+        got[int(r["seq"][k])] = inh[o:o + n]
+    assert b"".join(got[i] for i in range(len(got))) == data
