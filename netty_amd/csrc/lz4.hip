@@ -3,8 +3,9 @@
 // Lz4FrameEncoder compresses each block with lz4-java 1.8.0's LZ4Compressor
 // (Lz4FrameEncoder.java:259-275), a third-party dependency absent from the reference, so its exact
 // output cannot be pinned here.  This kernel is bit-exact with the oracle's greedy block compressor
-// (oracle/netty_oracle.c orc_lz4_compress): a 4096-entry hash of the 4 bytes at each position, one
-// probe per position, matches of >= 4 bytes extended to at most 5 bytes before the end, the last
+// (oracle/netty_oracle.c orc_lz4_compress): a 4096-entry hash of the 4 bytes at each probed position
+// (the step over misses grows by one every 64 misses, LZ4's skip acceleration), matches of >= 4
+// bytes extended to at most 5 bytes before the end, the last
 // 5 bytes always literal and no match starting in the last 12 (the block-format end rules every
 // LZ4 decoder relies on).  Its blocks decode with nx_lz4_decode_batch and any LZ4 block decoder.
 //
@@ -38,7 +39,7 @@ __device__ __forceinline__ uint32_t put_len(uint8_t* out, uint32_t op, uint32_t 
 __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint8_t* __restrict__ out,
                                  uint32_t* __restrict__ table, uint32_t stamp) {
     uint32_t op = 0;
-    int32_t anchor = 0, ip = 0;
+    int32_t anchor = 0, ip = 0, search = 64;
     const int32_t mlimit = n - kMfLimit;
     const uint32_t stag = stamp << 16;
     while (n >= kMfLimit + 1 && ip <= mlimit) {
@@ -47,9 +48,10 @@ __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint
         const uint32_t e = __hip_atomic_exchange(table + h, stag | (uint32_t)ip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int32_t ref = (e & 0xFFFF0000u) == stag ? (int32_t)(e & 0xFFFFu) : -1;
         if (ref < 0 || ip - ref > 65535 || ld32(in + ref) != w) {
-            ++ip;
+            ip += search++ >> 6;  // LZ4's skip acceleration (skipTrigger 6), as the oracle
             continue;
         }
+        search = 64;
         int32_t ml = kMinMatch;
         while (ip + ml < n - kLastLiterals && in[ref + ml] == in[ip + ml]) ++ml;
         const uint32_t lit = (uint32_t)(ip - anchor);

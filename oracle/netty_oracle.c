@@ -920,7 +920,7 @@ int32_t orc_lz4_compress(const uint8_t* in, int32_t n, uint8_t* out) {
     int32_t table[1 << HBITS];
     for (int i = 0; i < (1 << HBITS); ++i) table[i] = -1;
     size_t op = 0;
-    int32_t anchor = 0, ip = 0;
+    int32_t anchor = 0, ip = 0, search = 64;
     const int32_t mlimit = n - MFLIMIT;
     while (n >= MFLIMIT + 1 && ip <= mlimit) {
         uint32_t w;
@@ -931,9 +931,10 @@ int32_t orc_lz4_compress(const uint8_t* in, int32_t n, uint8_t* out) {
         uint32_t rw = 0;
         if (ref >= 0) memcpy(&rw, in + ref, 4);
         if (ref < 0 || ip - ref > 65535 || rw != w) {
-            ++ip;
+            ip += search++ >> 6; /* LZ4's skip acceleration (skipTrigger 6): longer steps over misses */
             continue;
         }
+        search = 64;
         int32_t ml = MINMATCH;
         while (ip + ml < n - LASTLITERALS && in[ref + ml] == in[ip + ml]) ++ml;
         const int64_t lit = ip - anchor;

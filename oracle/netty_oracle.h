@@ -79,7 +79,8 @@ size_t orc_lzf_frame_max_encoded(size_t n);
  * literals | 2-byte LE offset | match-length extension (+4), the last sequence literals only.
  * PARITY UNPINNED against lz4-java: no fixtures for it exist in the reference.
  * orc_lz4_decompress returns NX_OK when exactly out_len bytes are produced from all in_len bytes,
- * else NX_ERR_LZ4_MALFORMED.  orc_lz4_compress is a greedy single-probe compressor producing valid
+ * else NX_ERR_LZ4_MALFORMED.  orc_lz4_compress is a greedy single-probe compressor (LZ4's skip acceleration: the step over
+ * misses grows by one every 64 misses) producing valid
  * blocks for tests (last 5 bytes literals, no match starting in the last 12). */
 int32_t orc_lz4_decompress(const uint8_t* in, int32_t in_len, uint8_t* out, int32_t out_len);
 int32_t orc_lz4_compress(const uint8_t* in, int32_t n, uint8_t* out);
