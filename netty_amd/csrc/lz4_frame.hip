@@ -28,6 +28,20 @@ __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return __builtin_rotateleft32(x, r); }
 __device__ __forceinline__ uint32_t round1(uint32_t v, uint32_t w) { return rotl(v + w * P2, 13) * P1; }
 
+__device__ __forceinline__ uint32_t sel4(uint32_t j, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    const uint32_t lo = (j & 1u) ? b : a, hi = (j & 1u) ? d : c;
+    return (j & 2u) ? hi : lo;
+}
+// The four little-endian words at byte offset 4*j + sb of the 32-byte window lo:hi.
+__device__ __forceinline__ void window_words(const uint4& lo, const uint4& hi, uint32_t j, uint32_t sb, uint32_t w[4]) {
+    const uint32_t D[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    uint32_t S[5];
+#pragma unroll
+    for (int m = 0; m < 5; ++m) S[m] = sel4(j, D[m], D[m + 1], D[m + 2], D[m + 3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = __builtin_amdgcn_alignbyte(S[k + 1], S[k], sb);
+}
+
 __device__ uint32_t xxh32(const uint8_t* __restrict__ p, uint32_t n, uint32_t seed) {
     uint32_t i = 0, h;
     if (n >= 16u) {
@@ -45,6 +59,29 @@ __device__ uint32_t xxh32(const uint8_t* __restrict__ p, uint32_t n, uint32_t se
                     v1 = round1(v1, q[k].y);
                     v2 = round1(v2, q[k].z);
                     v3 = round1(v3, q[k].w);
+                }
+            }
+        }
+        else {
+            // Misaligned block (raw frame blocks sit at header + 21): aligned 16-byte loads, each
+            // stripe's four words cut out of a 32-byte window with alignbyte (branch-free for any
+            // offset).  Every granule read holds a byte of the block, so none crosses its page.
+            const uint32_t r = (uint32_t)((uintptr_t)p & 15u), j = r >> 2, sb = r & 3u;
+            const uint4* a = reinterpret_cast<const uint4*>(p - r);
+            uint4 prev = a[0];
+            for (; i + 64u <= n; i += 64u) {
+                uint4 q[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) q[k] = a[(i >> 4) + 1u + k];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    uint32_t w[4];
+                    window_words(prev, q[k], j, sb, w);
+                    v0 = round1(v0, w[0]);
+                    v1 = round1(v1, w[1]);
+                    v2 = round1(v2, w[2]);
+                    v3 = round1(v3, w[3]);
+                    prev = q[k];
                 }
             }
         }
