@@ -124,10 +124,15 @@ __device__ uint32_t wave_crc_update(const uint32_t* __restrict__ T, const uint32
             const uint32_t* q4 = (const uint32_t*)q;
             w0 = q4[0]; w1 = q4[1]; w2 = q4[2]; w3 = q4[3];
         } else {
-            w0 = q[0] | (q[1] << 8) | (q[2] << 16) | ((uint32_t)q[3] << 24);
-            w1 = q[4] | (q[5] << 8) | (q[6] << 16) | ((uint32_t)q[7] << 24);
-            w2 = q[8] | (q[9] << 8) | (q[10] << 16) | ((uint32_t)q[11] << 24);
-            w3 = q[12] | (q[13] << 8) | (q[14] << 16) | ((uint32_t)q[15] << 24);
+            // aligned dword loads, words cut out with alignbyte: the fifth dword holds byte q[15]
+            // (sb >= 1), so no load leaves the chunk's last dword
+            const uint32_t sb = (uint32_t)((uintptr_t)q & 3u);
+            const uint32_t* q4 = (const uint32_t*)(q - sb);
+            const uint32_t d0 = q4[0], d1 = q4[1], d2 = q4[2], d3 = q4[3], d4 = q4[4];
+            w0 = __builtin_amdgcn_alignbyte(d1, d0, sb);
+            w1 = __builtin_amdgcn_alignbyte(d2, d1, sb);
+            w2 = __builtin_amdgcn_alignbyte(d3, d2, sb);
+            w3 = __builtin_amdgcn_alignbyte(d4, d3, sb);
         }
         uint32_t c = raw16(T, w0, w1, w2, w3);
         c = fold_block(SH, c, lane);
