@@ -345,8 +345,35 @@ __global__ void __launch_bounds__(256) k_adler32(const uint8_t* __restrict__ in,
         const uint8_t* p = in + off[c];
         const uint32_t L = len[c];
         uint64_t sa = 0, sb = 0;  // Σ b_i, Σ (L - i) b_i
+        const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+        const uint32_t* p4 = reinterpret_cast<const uint32_t*>(p - sh);
         for (uint32_t base = 0; base < L; base += 1024) {
             const uint32_t i0 = base + 16u * lane;
+            if (i0 + 16u <= L) {
+                // a full slot: aligned dword loads (alignbyte for a misaligned chunk), byte sums
+                // with dot4: S = Σ b_k, T = Σ k b_k, so Σ (L - i0 - k) b_k = (L - i0) S - T
+                const uint32_t* q = p4 + (i0 >> 2);
+                uint32_t w[4];
+                if (sh == 0u) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) w[k] = q[k];
+                } else {
+                    uint32_t d[5];
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) d[k] = q[k];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+                }
+                uint32_t S = 0, T = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    S = __builtin_amdgcn_udot4(w[k], 0x01010101u, S, false);
+                    T = __builtin_amdgcn_udot4(w[k], 0x03020100u + 0x04040404u * (uint32_t)k, T, false);
+                }
+                sa += S;
+                sb += (uint64_t)(L - i0) * S - T;
+                continue;
+            }
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const uint32_t i = i0 + k;

@@ -1,4 +1,4 @@
-"""XXH32 and masked-CRC32C batch rates on 16-aligned vs misaligned blocks (the frame decoders checksum
+"""XXH32, masked-CRC32C and Adler32 batch rates on 16-aligned vs misaligned blocks (the frame decoders checksum
 raw blocks in place, after their headers).  262 144 blocks of 32 KiB."""
 import os
 import sys
@@ -12,7 +12,7 @@ dev = torch.device("cuda:0")
 n, L = 262144, 32768
 src = torch.randint(0, 256, (n * L + 64,), dtype=torch.uint8, device=dev)
 ln = torch.full((n,), L - 32, dtype=torch.int32, device=dev)
-for name, fn in (("xxh32", B.xxhash32), ("crc32c", B.crc32c_masked)):
+for name, fn in (("xxh32", B.xxhash32), ("crc32c", B.crc32c_masked), ("adler32", B.adler32)):
   for shift in (0, 1, 5, 21):
     off = torch.arange(n, dtype=torch.int64, device=dev) * L + shift
     fn(src, off, ln)
