@@ -150,7 +150,8 @@ int32_t nx_lzf_decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
                             int32_t* status, uint32_t n, void* stream);
 
 /* Replaces LZ4Compressor.compress as Lz4FrameEncoder.flushBufferedData calls it for one block
- * (Lz4FrameEncoder.java:259-275).  in_len[i] <= 65536; out capacity >= nx_lz4_max_compressed_length.
+ * (Lz4FrameEncoder.java:259-275).  in_len[i] < 2^25 (blocks over 64 KiB use 32-bit table entries in a
+ * table cleared per block); out capacity >= nx_lz4_max_compressed_length.
  * Bit-exact with the oracle's greedy block compressor; lz4-java's own output is unpinned (absent
  * third-party code), every block is valid LZ4. */
 size_t nx_lz4_max_compressed_length(size_t n);
@@ -176,7 +177,7 @@ int32_t nx_xxhash32_batch(const uint8_t* in, const uint64_t* off, const uint32_t
  * header (magic, token = blockType | compression_level, LE compressedLength, LE decompressedLength,
  * LE XXH32 & 0x0FFFFFFF) and the block (compressed, or raw when not smaller, :270-273).
  * out_len[i] = bytes written (0 for an empty block, as :249).  compression_level as
- * Lz4FrameEncoder.compressionLevel(blockSize) (:158-166): 6 for the default 64 KiB; in_len[i] <= 65536.
+ * Lz4FrameEncoder.compressionLevel(blockSize) (:158-166): 6 for the default 64 KiB; in_len[i] < 2^25.
  * The end block of close() (:326-335) is 21 host-written bytes. */
 int32_t nx_lz4_frame_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                   uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
@@ -282,7 +283,7 @@ int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, size_t n, si
                               const nx_msg** msgs, size_t* n_msgs, const char** err_msg);
 
 /* Lz4FrameEncoder(LZ4Factory.fastestInstance(), false, blockSize, new Lz4XXHash32(DEFAULT_SEED))
- * Lz4FrameEncoder.java:140-166; blockSize in [64, 65536] (the device block encoder's limit).
+ * Lz4FrameEncoder.java:140-166; blockSize in [64, 2^25) (MAX_BLOCK_SIZE 2^25 itself is refused).
  * encode buffers a partial block (:231-248) and returns the bytes of every full block it flushed;
  * flush() writes the partial block (:291-300); close() flushes and appends the end block (:317-336),
  * after which encode passes bytes through (:233-239). */

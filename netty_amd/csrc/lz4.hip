@@ -36,17 +36,25 @@ __device__ __forceinline__ uint32_t put_len(uint8_t* out, uint32_t op, uint32_t 
     return op;
 }
 
+// Large == false: blocks of <= 64 KiB, entries = stamp << 16 | position (no clearing).
+// Large == true: blocks of up to 32 MiB (Lz4FrameEncoder block sizes above the default), entries =
+// position + 1 in a table the lane zeroes before the block and again after it, so no stale entry
+// can pass a later small block's stamp check (stamps start at 1).
+template <bool Large>
 __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint8_t* __restrict__ out,
                                  uint32_t* __restrict__ table, uint32_t stamp) {
     uint32_t op = 0;
     int32_t anchor = 0, ip = 0, search = 64;
     const int32_t mlimit = n - kMfLimit;
     const uint32_t stag = stamp << 16;
+    if (Large)
+        for (uint32_t k = 0; k < (1u << kHashLog); ++k) __hip_atomic_store(table + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while (n >= kMfLimit + 1 && ip <= mlimit) {
         const uint32_t w = ld32(in + ip);
         const uint32_t h = (w * 2654435761u) >> (32 - kHashLog);
-        const uint32_t e = __hip_atomic_exchange(table + h, stag | (uint32_t)ip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int32_t ref = (e & 0xFFFF0000u) == stag ? (int32_t)(e & 0xFFFFu) : -1;
+        const uint32_t e = __hip_atomic_exchange(table + h, Large ? (uint32_t)ip + 1u : (stag | (uint32_t)ip), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+        const int32_t ref = Large ? (int32_t)e - 1 : ((e & 0xFFFF0000u) == stag ? (int32_t)(e & 0xFFFFu) : -1);
         if (ref < 0 || ip - ref > 65535 || ld32(in + ref) != w) {
             ip += search++ >> 6;  // LZ4's skip acceleration (skipTrigger 6), as the oracle
             continue;
@@ -66,6 +74,8 @@ __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint
         ip += ml;
         anchor = ip;
     }
+    if (Large)
+        for (uint32_t k = 0; k < (1u << kHashLog); ++k) __hip_atomic_store(table + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t lit = (uint32_t)(n - anchor);  // last literals
     out[op++] = (uint8_t)((lit >= 15u ? 15u : lit) << 4);
     if (lit >= 15u) op = put_len(out, op, lit);
@@ -84,12 +94,13 @@ __global__ void __launch_bounds__(256) k_lz4_encode(const uint8_t* __restrict__ 
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
         const uint32_t len = in_len[c];
-        if (len > 65536u) {
+        if (len >= (1u << 25)) {
             out_len[c] = 0;
             status[c] = NX_ERR_INVALID_ARG;
             continue;
         }
-        out_len[c] = encode_block(in + in_off[c], (int32_t)len, out + out_off[c], table, stamp_base + iter + 1u);
+        out_len[c] = len > 65536u ? encode_block<true>(in + in_off[c], (int32_t)len, out + out_off[c], table, 0u)
+                                  : encode_block<false>(in + in_off[c], (int32_t)len, out + out_off[c], table, stamp_base + iter + 1u);
         status[c] = NX_OK;
     }
 }

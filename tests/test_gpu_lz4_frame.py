@@ -174,3 +174,31 @@ def test_lz4_frame_large_blocks(dev, B, oracle, block_size):
         o, n = int(r["data_off"][k]), int(r["decomp_len"][k])
         got[int(r["seq"][k])] = inh[o:o + n]
     assert b"".join(got[i] for i in range(len(got))) == data
+
+
+def test_lz4_encode_large_and_small_blocks_mixed(dev, B, oracle):
+    """Blocks over 64 KiB (32-bit table entries, table cleared per block) interleaved with small
+    stamped blocks in one launch: bytes equal the oracle's compressor for every block."""
+    data = []
+    for i in range(6):
+        data.append(oracle.textgen_chunk(300 + i, 200000 + 50000 * i))
+        data.append(oracle.textgen_chunk(400 + i, 30000))
+    data.append(oracle.java_random_bytes(9, 150000))
+    inp, off, ln = B.pack(data, dev, align=1)
+    out, ooff = B.out_slots([B.lz4_max_compressed_length(len(d)) for d in data], dev, align=1)
+    olen, st = B.lz4_encode(inp, off, ln, out, ooff)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [0] * len(data)
+    outh, oo, ol = out.cpu().numpy().tobytes(), ooff.cpu().tolist(), olen.cpu().tolist()
+    for i, d in enumerate(data):
+        assert outh[oo[i]:oo[i] + ol[i]] == oracle.lz4_compress(d), i
+
+
+@pytest.mark.parametrize("block_size", [1 << 17, 1 << 20])
+def test_lz4_frame_encoder_large_block_size(dev, oracle, block_size):
+    import netty_amd as nx
+    data = oracle.textgen_chunk(71, 2 * block_size + 12345) + oracle.java_random_bytes(1, 70000)
+    enc = nx.Lz4FrameEncoder(block_size)
+    comp = enc.encode(data) + enc.finish_encode()
+    assert comp == oracle.lz4_frame_encode(data, block_size=block_size)
+    assert b"".join(nx.Lz4FrameDecoder(True).channel_read(comp)) == data
