@@ -48,13 +48,14 @@ __device__ uint32_t xxh32(const uint8_t* __restrict__ p, uint32_t n, uint32_t se
         uint32_t v0 = seed + P1 + P2, v1 = seed + P2, v2 = seed, v3 = seed - P1;
         const bool al16 = ((uintptr_t)p & 15u) == 0;
         if (al16) {
-            // 64 bytes (four 16-byte loads in flight) per step, then single stripes
-            for (; i + 64u <= n; i += 64u) {
-                uint4 q[4];
+            // 128 bytes (eight 16-byte loads in flight: a whole line per lane, so no line is
+            // fetched twice) per step, then single stripes
+            for (; i + 128u <= n; i += 128u) {
+                uint4 q[8];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const uint4*>(p + i + 16u * k);
+                for (int k = 0; k < 8; ++k) q[k] = *reinterpret_cast<const uint4*>(p + i + 16u * k);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+                for (int k = 0; k < 8; ++k) {
                     v0 = round1(v0, q[k].x);
                     v1 = round1(v1, q[k].y);
                     v2 = round1(v2, q[k].z);
@@ -69,12 +70,12 @@ __device__ uint32_t xxh32(const uint8_t* __restrict__ p, uint32_t n, uint32_t se
             const uint32_t r = (uint32_t)((uintptr_t)p & 15u), j = r >> 2, sb = r & 3u;
             const uint4* a = reinterpret_cast<const uint4*>(p - r);
             uint4 prev = a[0];
-            for (; i + 64u <= n; i += 64u) {
-                uint4 q[4];
+            for (; i + 128u <= n; i += 128u) {
+                uint4 q[8];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) q[k] = a[(i >> 4) + 1u + k];
+                for (int k = 0; k < 8; ++k) q[k] = a[(i >> 4) + 1u + k];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+                for (int k = 0; k < 8; ++k) {
                     uint32_t w[4];
                     window_words(prev, q[k], j, sb, w);
                     v0 = round1(v0, w[0]);
