@@ -50,6 +50,13 @@ __device__ uint32_t xxh32(const uint8_t* __restrict__ p, uint32_t n, uint32_t se
         if (al16) {
             // 128 bytes (eight 16-byte loads in flight: a whole line per lane, so no line is
             // fetched twice) per step, then single stripes
+            for (; i + 16u <= n && (((uintptr_t)(p + i)) & 127u) != 0u; i += 16u) {  // up to a line start
+                const uint4 q = *reinterpret_cast<const uint4*>(p + i);
+                v0 = round1(v0, q.x);
+                v1 = round1(v1, q.y);
+                v2 = round1(v2, q.z);
+                v3 = round1(v3, q.w);
+            }
             for (; i + 128u <= n; i += 128u) {
                 uint4 q[8];
 #pragma unroll
@@ -70,6 +77,19 @@ __device__ uint32_t xxh32(const uint8_t* __restrict__ p, uint32_t n, uint32_t se
             const uint32_t r = (uint32_t)((uintptr_t)p & 15u), j = r >> 2, sb = r & 3u;
             const uint4* a = reinterpret_cast<const uint4*>(p - r);
             uint4 prev = a[0];
+            // single stripes until the next granule load starts a 128-byte line, so the 128-byte
+            // steps below read whole lines
+            while (i + 16u <= n && (((uintptr_t)(a + (i >> 4) + 1u)) & 127u) != 0u) {
+                const uint4 q = a[(i >> 4) + 1u];
+                uint32_t w[4];
+                window_words(prev, q, j, sb, w);
+                v0 = round1(v0, w[0]);
+                v1 = round1(v1, w[1]);
+                v2 = round1(v2, w[2]);
+                v3 = round1(v3, w[3]);
+                prev = q;
+                i += 16u;
+            }
             for (; i + 128u <= n; i += 128u) {
                 uint4 q[8];
 #pragma unroll

@@ -13,7 +13,7 @@ n, L = 262144, 32768
 src = torch.randint(0, 256, (n * L + 64,), dtype=torch.uint8, device=dev)
 ln = torch.full((n,), L - 32, dtype=torch.int32, device=dev)
 for name, fn in (("xxh32", B.xxhash32), ("crc32c", B.crc32c_masked), ("adler32", B.adler32)):
-  for shift in (0, 1, 5, 21):
+  for shift in (0, 1, 5, 21, 48):
     off = torch.arange(n, dtype=torch.int64, device=dev) * L + shift
     fn(src, off, ln)
     torch.cuda.synchronize()
