@@ -1,20 +1,28 @@
-"""bench.py — BASELINE.json metric: "GiB/s device-resident Snappy encode+decode, 64 KiB chunks".
+"""bench.py — BASELINE.json metric: "GiB/s device-resident Snappy encode+decode, 64 KiB chunks, 1/2/4/8 MI355X".
 
-One step = one pass of the hot path over one batch of device-resident chunks:
+One step = one pass of the hot path over every chunk of the job, device-resident:
     encode leg: masked CRC32C of every 64 KiB chunk (SnappyFrameEncoder.calculateAndWriteChecksum)
                 + Snappy.encode of every chunk            (configs[1])
     decode leg: Snappy.decode of every chunk + CRC32C verify against the stored checksum (configs[2])
 value = Σ uncompressed bytes of all ranks / (max over ranks of the timed wall time) / 2^30,
-i.e. the round-trip rate Σ U / (t_enc + t_dec) of SURVEY.md §8d, inputs already resident in HBM.
+i.e. the round-trip rate Σ U / (t_enc + t_dec) of SURVEY.md §8d.
 
-Multi-GPU (weak scaling): one process per GPU (torchrun), each rank owns a contiguous shard of
-chunk indices generated on its own device; no data-path collective.  RCCL is used for the timing
-barrier/max-reduction and for one all-gather of per-rank compressed byte totals (the offset
-exchange that lays the shards out as one stream), outside the timed region.
+Workload (`value`): configs[4] — 100 GiB = 1 638 400 text-like 64 KiB chunks split across the ranks
+(STRONG scaling: the job is the same 100 GiB at N = 1, 2, 4, 8).  Each rank generates its contiguous
+shard of chunk indices on its own device (no host transfer) and runs it in sub-batches that fit HBM;
+the inputs of the whole shard are resident before the timed region starts.  A second, separate leg
+(`weak_1m_per_gpu`) runs configs[1]+[2] as stated: 1 048 576 chunks per GPU.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--chunks C] [--no-cpu-baseline]
+Multi-GPU: `python bench.py --gpus N` with no WORLD_SIZE in the environment starts N worker
+processes itself (spawn, before any GPU call in the parent); under torchrun (WORLD_SIZE set) each
+process is one rank.  Ranks talk over RCCL (backend "nccl") only for the timing barrier, the
+max-over-ranks reduction and one all-gather of per-rank compressed byte totals (the offset exchange
+that lays the shards out as one stream, netty_amd/shard.py), all outside the data path.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--total-chunks C] [--no-cpu-baseline]
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -26,30 +34,55 @@ sys.path.insert(0, ROOT)
 METRIC = "GiB/s device-resident Snappy encode+decode, 64 KiB chunks, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 CHUNK = 65536
+CONFIG5_CHUNKS = 1638400  # 100 GiB of 64 KiB chunks
+# kernels whose PMC traffic backs roofline.traffic; the summary must have been taken on these sources
+PMC_SOURCES = ("netty_amd/csrc/snappy_encode.hip", "netty_amd/csrc/snappy_decode.hip", "netty_amd/csrc/crc32c.hip",
+               "netty_amd/csrc/nx_common.hpp")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--chunks", type=int, default=1 << 20, help="64 KiB chunks per GPU (configs[1]: 1M)")
+    ap.add_argument("--total-chunks", type=int, default=CONFIG5_CHUNKS,
+                    help="64 KiB chunks of the whole job, split across ranks (configs[4]: 1 638 400 = 100 GiB)")
+    ap.add_argument("--sub-chunks", type=int, default=262144, help="chunks per device-resident sub-batch")
+    ap.add_argument("--weak-chunks", type=int, default=1 << 20,
+                    help="chunks per GPU of the separate configs[1]+[2] leg (0 = skip)")
+    ap.add_argument("--weak-steps", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (H2D/D2H) end-to-end measurement")
     ap.add_argument("--e2e-chunks", type=int, default=131072, help="chunks through the host pipeline (8 GiB)")
     ap.add_argument("--e2e-sub", type=int, default=65536, help="chunks per pipelined sub-batch")
-    ap.add_argument("--no-alt", action="store_true", help="skip the FastLZ/LZF (configs[3]) measurement")
+    ap.add_argument("--no-alt", action="store_true", help="skip the FastLZ/LZF/LZ4 (configs[3]) measurement")
     ap.add_argument("--alt-chunks", type=int, default=262144)
     ap.add_argument("--no-frame-scan", action="store_true", help="skip the framed-stream (§8f row 1) measurement")
     ap.add_argument("--scan-chunks", type=int, default=131072, help="chunks laid out as framed streams")
     ap.add_argument("--scan-per-stream", type=int, default=64, help="chunks per stream (one cumulation each)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------------------- CPU baseline
+def host_cores() -> int:
+    """CPUs this process may actually use: the affinity mask, capped by a cgroup CPU quota (on the GPU
+    box the affinity mask shows the whole machine while the job's share is a quota)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
 
 
 def cpu_baseline(seconds: float):
     """The oracle (C restatement of Snappy.encode/decode + Crc32c, byte-at-a-time CRC like Crc32c.java)
-    timed on this host: encode+CRC then decode+CRC-verify of text-like 64 KiB chunks."""
+    timed on this host: encode+CRC then decode+CRC-verify of text-like 64 KiB chunks, one thread per
+    available core; plus configs[0] (1 MiB java.util.Random(42) frame round trip) and a per-codec
+    configs[3] sample, single-thread."""
     import ctypes as C
     from concurrent.futures import ThreadPoolExecutor
 
@@ -77,45 +110,379 @@ def cpu_baseline(seconds: float):
             i += 1
         return done
 
-    # single thread
     t0 = time.perf_counter()
-    d1 = work(t0 + seconds / 3)
+    d1 = work(t0 + seconds / 4)
     t1 = time.perf_counter()
     single = d1 * CHUNK / (t1 - t0) / 2**30
-    # all cores of this box's share (ctypes releases the GIL during the C calls)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = host_cores()
     t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        dl = t0 + seconds * 2 / 3
-        counts = list(ex.map(work, [dl] * threads))
+    with ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL during the C calls
+        counts = list(ex.map(work, [t0 + seconds / 2] * threads))
     t1 = time.perf_counter()
     multi = sum(counts) * CHUNK / (t1 - t0) / 2**30
     return {"value": round(multi, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"oracle/netty_oracle.c encode+CRC32C then decode+verify of text-like 64 KiB chunks, "
                       f"{sum(counts)} chunks on {threads} threads in {t1 - t0:.1f}s (+ {d1} chunks single-thread)",
-            "single_thread_value": round(single, 4)}
+            "single_thread_value": round(single, 4),
+            "config1_frame_round_trip": config1_cpu(O, seconds / 8),
+            "config4_per_codec": config4_cpu(O, seconds / 8)}
+
+
+def config1_cpu(O, seconds: float):
+    """configs[0]: SnappyFrameEncoder then SnappyFrameDecoder (validating) over the 1 MiB
+    java.util.Random(42) message of AbstractIntegrationTest.java:106-112, default (32767-byte slices)
+    and jumbo (65535) framing; identity checked; single thread; GiB/s of the 1 MiB message."""
+    data = O.java_random_bytes(42, 1 << 20)
+    res = {}
+    for name, jumbo in (("default", False), ("jumbo", True)):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            framed, _ = O.snappy_frame_encode(data, jumbo=jumbo)
+            out = bytearray()
+            p = 10  # stream identifier
+            while p < len(framed):
+                typ, ln = framed[p], int.from_bytes(framed[p + 1:p + 4], "little")
+                crc = int.from_bytes(framed[p + 4:p + 8], "little")
+                body = framed[p + 8:p + 4 + ln]
+                if typ == 0:
+                    st, dec, _ = O.snappy_decode(body, 65536)
+                    assert st == 0
+                else:
+                    dec = body
+                assert O.snappy_checksum(dec) == crc
+                out += dec
+                p += 4 + ln
+            assert bytes(out) == data
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds / 2:
+                break
+        res[name] = {"gib_s": round(reps * len(data) / dt / 2**30, 4), "round_trips": reps,
+                     "framed_bytes": len(framed)}
+    return res
+
+
+def config4_cpu(O, seconds: float):
+    """configs[3] CPU beside-rate per codec and direction: the oracle on a mixed sample (sizes uniform in
+    [4096, 65535], half text-like, half random), single thread, GiB/s of uncompressed bytes."""
+    import random
+    rnd = random.Random(1234)
+    sample = []
+    for i in range(16):
+        n = rnd.randrange(4096, 65536)
+        sample.append(O.textgen_chunk(i, n) if i % 2 == 0 else rnd.randbytes(n))
+    U = sum(len(s) for s in sample)
+    per = seconds / 8
+
+    def rate(fn, inputs):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            for x in inputs:
+                fn(x)
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= per:
+                return round(reps * U / dt / 2**30, 4)
+
+    res = {"sample": "16 chunks, sizes uniform [4096, 65535], half text-like, half random", "threads": 1}
+    for lv in (1, 2):
+        enc = [O.fastlz_compress(s, lv) for s in sample]
+        res[f"fastlz_l{lv}"] = {"encode_gib_s": rate(lambda s: O.fastlz_compress(s, lv), sample),
+                                "decode_gib_s": rate(lambda e: O.fastlz_decompress(e[0], e[1]),
+                                                     [(e, len(s)) for e, s in zip(enc, sample)])}
+    lz = [O.lzf_compress_body(s) for s in sample]
+    res["lzf"] = {"encode_gib_s": rate(O.lzf_compress_body, sample),
+                  "decode_gib_s": rate(lambda e: O.lzf_decode_chunk(e[0], e[1]), [(e, len(s)) for e, s in zip(lz, sample)])}
+    z4 = [O.lz4_compress(s) for s in sample]
+    res["lz4"] = {"encode_gib_s": rate(O.lz4_compress, sample),
+                  "decode_gib_s": rate(lambda e: O.lz4_decompress(e[0], e[1]), [(e, len(s)) for e, s in zip(z4, sample)])}
+    return res
+
+
+# ---------------------------------------------------------------------------------------- PMC traffic
+def source_digest() -> str:
+    h = hashlib.sha256()
+    for p in PMC_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def load_traffic():
     """Per-chunk HBM bytes per kernel from the newest committed PMC summary (scripts/pmc_traffic.sh:
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench's workload)."""
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench's workload).  The summary
+    records the digest of the kernel sources it was taken on; a summary of other sources is stale and
+    is not used (roofline.traffic is then null with the reason)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
-    if not files:
-        return None
-    try:
-        d = json.load(open(files[-1]))
-        return {k: v["hbm_bytes_per_chunk"] for k, v in d["kernels"].items()}
-    except (OSError, ValueError, KeyError):
-        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", "pmc_traffic.json"), recursive=True),
+                   key=os.path.getmtime)
+    want = source_digest()
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("source_digest") == want:
+            return {k: v["hbm_bytes_per_chunk"] for k, v in d["kernels"].items()}, os.path.relpath(f, ROOT)
+    return None, f"no PMC summary for kernel sources {want} (run scripts/pmc_traffic.sh)"
 
 
-def bench_frame_scan(torch, B, dev, src, enc, eoff, elen, crc, dec, m: int, per_stream: int, reps: int = 3):
-    """§8f row 1: the encoded chunks laid out as SnappyFrameEncoder streams in HBM (stream identifier,
-    then one COMPRESSED_DATA chunk per 64 KiB: type 0, 24-bit length, masked CRC, payload), one stream
-    per connection cumulation; nx_snappy_frame_scan_batch lists their chunks and nx_snappy_decode_batch
-    decodes straight from that list with CRC verification.  Timed with HIP events on torch's stream."""
-    m = min(m, elen.numel())
+# ---------------------------------------------------------------------------------------- the GPU leg
+class SnappyRoundTrip:
+    """One rank's shard [first, first + n) of text-like 64 KiB chunks: the whole shard's inputs are
+    generated on the device up front; a step runs CRC32C + encode + decode/verify over them in
+    sub-batches whose output buffers are reused (the compressed bytes of every chunk are kept only as
+    per-chunk lengths, the decoded bytes are checked against the inputs after the timed region)."""
+
+    def __init__(self, torch, dev, first: int, n: int, sub: int):
+        from netty_amd import batch as B
+        self.torch, self.B, self.dev = torch, B, dev
+        self.first, self.n, self.sub = first, n, max(1, min(sub, n))
+        self.cap = (B.snappy_max_compressed_length(CHUNK) + 15) // 16 * 16
+        s = self.sub
+        self.src = torch.empty(n * CHUNK, dtype=torch.uint8, device=dev)
+        for lo in range(0, n, s):  # textgen in pieces keeps its temporaries small
+            B.textgen(self.src[lo * CHUNK:], first + lo, min(s, n - lo), CHUNK)
+        self.off = torch.arange(s, dtype=torch.int64, device=dev) * CHUNK
+        self.ln = torch.full((s,), CHUNK, dtype=torch.int32, device=dev)
+        self.enc = torch.empty(s * self.cap, dtype=torch.uint8, device=dev)
+        self.eoff = torch.arange(s, dtype=torch.int64, device=dev) * self.cap
+        self.dec = torch.empty(s * CHUNK, dtype=torch.uint8, device=dev)
+        self.elen = torch.empty(n, dtype=torch.int32, device=dev)
+        self.est = torch.empty(n, dtype=torch.int32, device=dev)
+        self.crc = torch.empty(n, dtype=torch.int32, device=dev)
+        self.dlen = torch.empty(n, dtype=torch.int32, device=dev)
+        self.dst = torch.empty(n, dtype=torch.int32, device=dev)
+        self.ev = {k: [] for k in ("crc", "enc", "dec")}
+        torch.cuda.synchronize(dev)
+
+    def batches(self):
+        for lo in range(0, self.n, self.sub):
+            yield lo, min(self.sub, self.n - lo)
+
+    def run_sub(self, lo, m, record=False, expected=None):
+        torch, B = self.torch, self.B
+        src = self.src[lo * CHUNK:(lo + m) * CHUNK]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        if record:
+            e[0].record()
+        B.crc32c_masked(src, self.off[:m], self.ln[:m], out=self.crc[lo:lo + m])
+        if record:
+            e[1].record()
+        B.snappy_encode(src, self.off[:m], self.ln[:m], self.enc, self.eoff[:m], out_len=self.elen[lo:lo + m],
+                        status=self.est[lo:lo + m])
+        if record:
+            e[2].record()
+        B.snappy_decode(self.enc, self.eoff[:m], self.elen[lo:lo + m], self.dec, self.off[:m],
+                        expected_crc=self.crc[lo:lo + m] if expected is None else expected,
+                        out_len=self.dlen[lo:lo + m], status=self.dst[lo:lo + m])
+        if record:
+            e[3].record()
+            self.ev["crc"].append((e[0], e[1]))
+            self.ev["enc"].append((e[1], e[2]))
+            self.ev["dec"].append((e[2], e[3]))
+
+    def step(self, record=False):
+        for lo, m in self.batches():
+            self.run_sub(lo, m, record)
+
+    def kernel_ms_per_step(self, steps: int):
+        def tot(pairs):
+            return sum(a.elapsed_time(b) for a, b in pairs) / max(1, steps)
+        return tot(self.ev["crc"]), tot(self.ev["enc"]), tot(self.ev["dec"])
+
+    def verify(self, rank: int):
+        """Outside the timed region: every status 0 and length right, decode(encode(x)) == x for every
+        chunk, and a 2 % subset with corrupted expected CRCs flagged (and nothing else)."""
+        torch = self.torch
+        ok = True
+        for lo, m in self.batches():
+            self.run_sub(lo, m)
+            ok = ok and bool(torch.equal(self.dec[:m * CHUNK], self.src[lo * CHUNK:(lo + m) * CHUNK]))
+        ok = (ok and int((self.est != 0).sum()) == 0 and int((self.dst != 0).sum()) == 0
+              and bool(torch.equal(self.dlen, torch.full_like(self.dlen, CHUNK))))
+        lo, m = 0, min(self.sub, self.n)
+        g = torch.Generator(device=self.dev).manual_seed(77 + rank)
+        bad = torch.rand(m, device=self.dev, generator=g) < 0.02
+        crc = self.crc[:m].clone()
+        self.run_sub(lo, m, expected=torch.where(bad, crc ^ 1, crc))
+        d = self.dst[:m]
+        detect = bool(torch.equal(d != 0, bad)) and bool(torch.equal(d[bad], torch.full_like(d[bad], -7)))
+        self.run_sub(lo, m)  # leave the first sub-batch's buffers decoded with the right CRCs
+        return ok and detect, detect
+
+    def comp_bytes(self) -> int:
+        return int(self.elen.to(self.torch.int64).sum().item())
+
+
+def copy_rate_gbs(torch, a, b):
+    ts = []
+    for _ in range(3):
+        x, y = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        x.record()
+        b.copy_(a)
+        y.record()
+        torch.cuda.synchronize()
+        ts.append(x.elapsed_time(y))
+    return 2 * a.numel() / (min(ts) / 1e3) / 1e9
+
+
+def roofline(algo_bytes, ms, n_chunks, kernels, traffic, copy_gbs):
+    a = algo_bytes / (ms / 1e3) / 1e9
+    tr, src = traffic
+    per_chunk = (sum(v for k2, v in tr.items() if any(k2.split("<")[0] == k.split("<")[0] for k in kernels))
+                 if tr else None)
+    return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(a / HBM_PEAK_GBS, 4),
+            "traffic": round(per_chunk * n_chunks) if per_chunk else None,
+            "traffic_per_chunk": round(per_chunk) if per_chunk else None,
+            "traffic_source": src,
+            "algorithmic_per_chunk": round(algo_bytes / n_chunks),
+            "achievable_copy_gbs": round(copy_gbs, 1) if copy_gbs else None,
+            "frac_of_achievable": round(a / copy_gbs, 4) if copy_gbs else None,
+            "kernel": " + ".join(kernels)}
+
+
+ENC_KERNELS = ["nx::enc::k_snappy_encode"]
+DEC_KERNELS = ["nx::dec::k_parse", "nx::dec::k_expand"]
+
+
+def timed_legs(torch, leg, steps, warmup, sync, S, dev):
+    """W untimed steps, then exactly K steps bracketed by barrier + device synchronize on both sides;
+    the job's time is the max over ranks."""
+    dsync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    for _ in range(warmup):
+        leg.step(False)
+    dsync()
+    sync()
+    dsync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        leg.step(True)
+    dsync()
+    sync()
+    t1 = time.perf_counter()
+    return S.max_over_ranks(t1 - t0, device=dev)
+
+
+def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg_factory=None, emit=print):
+    """One rank of the job.  `leg_factory(first, n)` builds the rank's work (default: the GPU
+    SnappyRoundTrip); the CPU test of the N>1 path passes its own over gloo.  Returns the JSON line
+    (rank 0) or None."""
+    import torch
+    import torch.distributed as dist
+
+    from netty_amd import shard as S
+
+    gpu = leg_factory is None
+    if gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if gpu:
+            dist.init_process_group(backend, rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+        world = dist.get_world_size()  # the ranks the backend actually sees
+
+    def sync():
+        if world > 1:
+            dist.barrier()
+
+    lo, hi = S.shard_range(args.total_chunks, rank, world)
+    n = hi - lo
+    leg = SnappyRoundTrip(torch, dev, lo, n, args.sub_chunks) if gpu else leg_factory(lo, n)
+    elapsed = timed_legs(torch, leg, args.steps, args.warmup, sync, S, dev)
+    ok, crc_detect = leg.verify(rank)
+    comp_bytes = leg.comp_bytes()
+    my_off, total_comp, totals_all = S.exchange_offsets(comp_bytes, device=dev)
+    t_crc, t_enc, t_dec = leg.kernel_ms_per_step(args.steps)
+    U, C_ = n * CHUNK, comp_bytes
+    copy_gbs = copy_rate_gbs(torch, leg.src[:min(n, leg.sub) * CHUNK], leg.dec) if gpu else None
+    traffic = load_traffic() if gpu else (None, "cpu test leg")
+    r_dec = roofline(C_ + U, t_dec, n, DEC_KERNELS, traffic, copy_gbs)  # decode: C_in + U_out per chunk
+    r_enc = roofline(U + C_, t_enc, n, ENC_KERNELS, traffic, copy_gbs)  # encode: U_in + C_out per chunk
+    dominant = r_enc if t_enc >= t_dec else r_dec
+    value = args.total_chunks * CHUNK / elapsed * args.steps / 2**30
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic text-like 64 KiB chunks (include/netty_amd_textgen.h: 4096-word Zipf(1.1) vocabulary), "
+                "generated on device",
+        "config": {"workload": "configs[4]: Snappy encode (+frame CRC32C) then decode + CRC32C verify of "
+                               f"{args.total_chunks} text-like 64 KiB chunks ({args.total_chunks * CHUNK / 2**30:.0f} GiB) "
+                               f"split across {world} GPU(s), device-resident",
+                   "chunk_bytes": CHUNK, "global_chunks": args.total_chunks, "chunks_per_gpu": n,
+                   "sub_batch_chunks": leg.sub,
+                   "parallelism": f"dp{world} (independent chunk shards, no data-path collective)"},
+        "roofline": dominant,
+        "roofline_decode": r_dec, "roofline_encode": r_enc,
+        "encode_gib_s": round(U / ((t_crc + t_enc) / 1e3) / 2**30, 3) if t_enc else None,
+        "decode_gib_s": round(U / (t_dec / 1e3) / 2**30, 3) if t_dec else None,
+        "kernel_ms_per_step": {"crc32c": round(t_crc, 3), "encode": round(t_enc, 3), "decode_crc": round(t_dec, 3)},
+        "compression_ratio": round(C_ / U, 4) if U else None,
+        "shard": {"first_chunk": lo, "chunks": n, "stream_offset": my_off, "stream_bytes": total_comp},
+        "compressed_bytes_per_rank": totals_all,
+        "crc_corruption_subset_detected": crc_detect,
+    }
+    ok = S.all_true(ok, device=dev)
+    line["verified"] = ok
+    if gpu and args.weak_chunks > 0:
+        del leg
+        torch.cuda.empty_cache()
+        wk = SnappyRoundTrip(torch, dev, rank * args.weak_chunks, args.weak_chunks, args.sub_chunks)
+        wel = timed_legs(torch, wk, args.weak_steps, 1 if args.warmup else 0, sync, S, dev)
+        wok, _ = wk.verify(rank)
+        wok = S.all_true(wok, device=dev)
+        _, we, wd = wk.kernel_ms_per_step(args.weak_steps)
+        line["weak_1m_per_gpu"] = {
+            "workload": "configs[1]+configs[2]: the same step over chunks_per_gpu chunks on every GPU (weak scaling)",
+            "chunks_per_gpu": args.weak_chunks, "steps": args.weak_steps,
+            "value": round(world * args.weak_chunks * CHUNK / wel * args.weak_steps / 2**30, 3), "unit": "GiB/s",
+            "ms_per_step": round(wel / args.weak_steps * 1e3, 3), "encode_ms": round(we, 3), "decode_crc_ms": round(wd, 3),
+            "scaling": "weak", "verified": wok}
+        ok = ok and wok
+        line["verified"] = ok
+        leg = wk
+    if gpu and rank == 0 and world == 1:
+        from netty_amd import batch as B
+        if not args.no_frame_scan:
+            line["frame_scan"] = bench_frame_scan(torch, B, dev, leg, args.scan_chunks, args.scan_per_stream)
+            ok = ok and line["frame_scan"]["verified"]
+            torch.cuda.empty_cache()
+        del leg
+        torch.cuda.empty_cache()
+        if not args.no_alt:
+            line["alt_codecs"] = bench_alt_codecs(torch, B, dev, args.alt_chunks)
+            torch.cuda.empty_cache()
+        if not args.no_e2e:
+            # host-memory path (pinned ByteBuf-like buffers, H2D → kernels → D2H, two streams); never `value`
+            from netty_amd import pipeline as P
+            line["end_to_end"] = P.measure(dev, n=args.e2e_chunks, sub=args.e2e_sub)
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        line["verified"] = ok
+    if rank == 0:
+        emit(json.dumps(line))
+        sys.stdout.flush()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return line if rank == 0 else None, ok
+
+
+# ---------------------------------------------------------------------------------------- extra legs
+def bench_frame_scan(torch, B, dev, leg, m: int, per_stream: int, reps: int = 3):
+    """§8f row 1: the first sub-batch's encoded chunks laid out as SnappyFrameEncoder streams in HBM
+    (stream identifier, then one COMPRESSED_DATA chunk per 64 KiB: type 0, 24-bit length, masked CRC,
+    payload), one stream per connection cumulation; nx_snappy_frame_scan_batch lists their chunks and
+    nx_snappy_decode_batch decodes straight from that list with CRC verification."""
+    m = min(m, leg.sub, leg.n)
+    src, enc, eoff, elen, crc, dec = leg.src, leg.enc, leg.eoff, leg.elen, leg.crc, leg.dec
     ns = (m + per_stream - 1) // per_stream
     fs = elen[:m].to(torch.int64) + 8
     sid = torch.arange(m, dtype=torch.int64, device=dev) // per_stream
@@ -153,11 +520,11 @@ def bench_frame_scan(torch, B, dev, src, enc, eoff, elen, crc, dec, m: int, per_
           and int((d["status"] != 0).sum()) == 0 and bool(torch.equal(dec[:m * CHUNK], src[:m * CHUNK])))
     ts, ta = min(t_scan), min(t_all)
     return {"streams": ns, "chunks_per_stream": per_stream, "chunks": m, "framed_bytes": total,
-            "scan_ms": round(ts, 3), "scan_framed_gib_s": round(total / (ts / 1e3) / 2**30, 1),
+            "scan_ms": round(ts, 3), "scan_chunks_per_s": round(m / (ts / 1e3)),
             "scan_decode_ms": round(ta, 3), "framed_decode_gib_s": round(m * CHUNK / (ta / 1e3) / 2**30, 2),
-            "note": "scan = one lane per stream walking its chunk headers; the list it writes is the decode "
-                    "batch's in_off / in_len / expected CRC as is; the decode kernels run on 131072 frames here, "
-                    "below the 262144 that fill the parse/expand pair",
+            "note": "scan = one lane per stream walking its chunk headers (it reads the 8-byte headers only, "
+                    "so it is reported in chunks/s, not bytes); the list it writes is the decode batch's "
+                    "in_off / in_len / expected CRC as is",
             "verified": ok}
 
 
@@ -246,7 +613,7 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2):
                   "decode_gib_s": round(Ud / td * 1e3 / 2**30, 3) if idx.numel() else None,
                   "decoded_chunks": int(idx.numel()), "ratio": round(int(llen.to(torch.int64).sum()) / U, 4), "verified": ok}
     del lout
-    # LZ4 blocks (§8f row 4): GPU greedy block encoder, then decode through the parse/expand kernels
+    # LZ4 blocks (§8f row 4): GPU block encoder, then decode through the parse/expand kernels
     zcap = (B.lz4_max_compressed_length(CH) + 15) // 16 * 16
     zout = torch.empty(n * zcap, dtype=torch.uint8, device=dev)
     zoff = torch.arange(n, dtype=torch.int64, device=dev) * zcap
@@ -308,182 +675,38 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2):
     return res
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+# ---------------------------------------------------------------------------------------- launcher
+def _spawned_rank(local: int, argv, world: int, port: int):
+    os.environ.update({"RANK": str(local), "LOCAL_RANK": str(local), "WORLD_SIZE": str(world),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    args = parse(argv)
+    _, ok = run_rank(args, local, world, local)
+    if not ok:
+        sys.exit(3)
 
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # start one process per GPU ourselves; nothing in this parent has touched the GPU
+        import torch.multiprocessing as mp
+        mp.start_processes(_spawned_rank, args=(argv, args.gpus, free_port()), nprocs=args.gpus, join=True,
+                           start_method="spawn")
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
-
-    from netty_amd import batch as B
-    from netty_amd import shard as S
-
-    n = args.chunks
-    # HBM budget: src + dec (n*64 KiB each) + encoded slots (n*cap) + encoder workspace (~8.6 GB)
-    cap = (B.snappy_max_compressed_length(CHUNK) + 15) // 16 * 16
-    free, total = torch.cuda.mem_get_info(dev)
-    # + encoder hash tables (16 GiB) and decoder record slots (16 GiB) allocated by the C-ABI, + slack
-    reserve = 40 << 30
-    need = n * (2 * CHUNK + cap) + reserve
-    if need > free:
-        n = int((free - reserve) // (2 * CHUNK + cap))
-    first = rank * n  # contiguous shard of chunk indices per rank
-
-    src = torch.empty(n * CHUNK, dtype=torch.uint8, device=dev)
-    B.textgen(src, first, n, CHUNK)
-    off = torch.arange(n, dtype=torch.int64, device=dev) * CHUNK
-    ln = torch.full((n,), CHUNK, dtype=torch.int32, device=dev)
-    enc = torch.empty(n * cap, dtype=torch.uint8, device=dev)
-    eoff = torch.arange(n, dtype=torch.int64, device=dev) * cap
-    dec = torch.empty_like(src)
-    elen = torch.empty(n, dtype=torch.int32, device=dev)
-    est = torch.empty(n, dtype=torch.int32, device=dev)
-    crc = torch.empty(n, dtype=torch.int32, device=dev)
-    dlen = torch.empty(n, dtype=torch.int32, device=dev)
-    dst = torch.empty(n, dtype=torch.int32, device=dev)
-    torch.cuda.synchronize()
-
-    ev = {k: [] for k in ("crc", "enc", "dec")}
-
-    def step(record):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
-        if record:
-            e[0].record()
-        B.crc32c_masked(src, off, ln, out=crc)
-        if record:
-            e[1].record()
-        B.snappy_encode(src, off, ln, enc, eoff, out_len=elen, status=est)
-        if record:
-            e[2].record()
-        B.snappy_decode(enc, eoff, elen, dec, off, expected_crc=crc, out_len=dlen, status=dst)
-        if record:
-            e[3].record()
-            ev["crc"].append((e[0], e[1]))
-            ev["enc"].append((e[1], e[2]))
-            ev["dec"].append((e[2], e[3]))
-
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = S.max_over_ranks(t1 - t0, device=dev)
-
-    # verification (outside the timed region): statuses, lengths, identity
-    def same(a, b, step=1 << 32):  # torch.equal in slices (it materialises a mask of the whole tensor)
-        return all(bool(torch.equal(a[i:i + step], b[i:i + step])) for i in range(0, a.numel(), step))
-
-    ok = (int((est != 0).sum()) == 0 and int((dst != 0).sum()) == 0 and bool(torch.equal(dlen, ln))
-          and same(dec, src))
-    # configs[2]: a 2 % subset with corrupted expected CRCs must be flagged, and nothing else
-    g = torch.Generator(device=dev).manual_seed(77 + rank)
-    bad = torch.rand(n, device=dev, generator=g) < 0.02
-    crc_bad = torch.where(bad, crc ^ 1, crc)
-    B.snappy_decode(enc, eoff, elen, dec, off, expected_crc=crc_bad, out_len=dlen, status=dst)
-    crc_detect = bool(torch.equal(dst != 0, bad)) and bool(torch.equal(dst[bad], torch.full_like(dst[bad], -7)))
-    ok = ok and crc_detect
-    # achievable HBM bandwidth on this device: a plain device-to-device copy (read + write bytes)
-    cb = []
-    for _ in range(3):
-        a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a_.record()
-        dec.copy_(src)
-        b_.record()
-        torch.cuda.synchronize()
-        cb.append(a_.elapsed_time(b_))
-    copy_gbs = 2 * src.numel() / (min(cb) / 1e3) / 1e9
-    comp_bytes = int(elen.to(torch.int64).sum().item())
-    # offset exchange that lays the shards out as one stream (outside the timed region)
-    _, _, totals_all = S.exchange_offsets(comp_bytes, device=dev)
-    ok = S.all_true(ok, device=dev)
-
-    def avg_ms(pairs):
-        return sum(a.elapsed_time(b) for a, b in pairs) / max(1, len(pairs))
-
-    t_crc, t_enc, t_dec = avg_ms(ev["crc"]), avg_ms(ev["enc"]), avg_ms(ev["dec"])
-    U = n * CHUNK
-    C_ = comp_bytes
-
-    traffic = load_traffic()
-
-    def roof(algo_bytes, ms, kernels):
-        a = algo_bytes / (ms / 1e3) / 1e9
-        # PMC summaries name kernels with their template arguments; match on the name before them
-        per_chunk = (sum(v for k2, v in traffic.items() if any(k2.split("<")[0] == k.split("<")[0] for k in kernels))
-                     if traffic else None)
-        return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(a / HBM_PEAK_GBS, 4),
-                "traffic": round(per_chunk * n) if per_chunk else None,
-                "traffic_per_chunk": round(per_chunk) if per_chunk else None,
-                "algorithmic_per_chunk": round(algo_bytes / n),
-                "achievable_copy_gbs": round(copy_gbs, 1), "frac_of_achievable": round(a / copy_gbs, 4),
-                "kernel": " + ".join(kernels)}
-
-    r_dec = roof(C_ + U, t_dec, ["nx::dec::k_parse", "nx::dec::k_expand"])  # decode: C_in + U_out per chunk
-    r_enc = roof(U + C_, t_enc, ["nx::enc::k_snappy_encode<true>"])           # encode: U_in + C_out per chunk
-    dominant = r_enc if t_enc >= t_dec else r_dec
-
-    value = world * U / elapsed * args.steps / 2**30
-    line = {
-        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic text-like 64 KiB chunks (include/netty_amd_textgen.h: 4096-word Zipf(1.1) vocabulary), "
-                "generated on device",
-        "config": {"workload": "configs[1]+configs[2]: Snappy encode (+frame CRC32C) then decode + CRC32C verify of "
-                               "text-like 64 KiB chunks, device-resident",
-                   "chunk_bytes": CHUNK, "chunks_per_gpu": n, "global_chunks": n * world,
-                   "parallelism": f"dp{world} (independent chunk shards, no data-path collective)"},
-        "roofline": dominant,
-        "roofline_decode": r_dec, "roofline_encode": r_enc,
-        "encode_gib_s": round(U / ((t_crc + t_enc) / 1e3) / 2**30, 3),
-        "decode_gib_s": round(U / (t_dec / 1e3) / 2**30, 3),
-        "kernel_ms": {"crc32c": round(t_crc, 3), "encode": round(t_enc, 3), "decode_crc": round(t_dec, 3)},
-        "compression_ratio": round(C_ / U, 4), "compressed_bytes_per_rank": totals_all,
-        "crc_corruption_subset_detected": crc_detect,
-        "verified": ok,
-    }
-    if rank == 0 and world == 1 and not args.no_frame_scan:
-        line["frame_scan"] = bench_frame_scan(torch, B, dev, src, enc, eoff, elen, crc, dec, args.scan_chunks,
-                                              args.scan_per_stream)
-        ok = ok and line["frame_scan"]["verified"]
-        line["verified"] = ok
-        torch.cuda.empty_cache()
-    if rank == 0 and world == 1 and not args.no_alt:
-        del src, dec, enc
-        torch.cuda.empty_cache()
-        src = dec = enc = None
-        line["alt_codecs"] = bench_alt_codecs(torch, B, dev, args.alt_chunks)
-        torch.cuda.empty_cache()
-    if rank == 0 and world == 1 and not args.no_e2e:
-        # host-memory path (pinned ByteBuf-like buffers, H2D → kernels → D2H, two streams); never `value`
-        del src, dec, enc
-        torch.cuda.empty_cache()
-        from netty_amd import pipeline as P
-        line["end_to_end"] = P.measure(dev, n=args.e2e_chunks, sub=args.e2e_sub)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    _, ok = run_rank(args, rank, world, local)
     if not ok:
         sys.exit(3)
 

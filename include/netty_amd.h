@@ -150,17 +150,17 @@ int32_t nx_lzf_decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
                             int32_t* status, uint32_t n, void* stream);
 
 /* Replaces LZ4Compressor.compress as Lz4FrameEncoder.flushBufferedData calls it for one block
- * (Lz4FrameEncoder.java:259-275).  in_len[i] < 2^25 (blocks over 64 KiB use 32-bit table entries in a
- * table cleared per block); out capacity >= nx_lz4_max_compressed_length.
- * Bit-exact with the oracle's greedy block compressor; lz4-java's own output is unpinned (absent
- * third-party code), every block is valid LZ4. */
+ * (Lz4FrameEncoder.java:259-275; fastCompressor() = liblz4's LZ4_compress_default through
+ * lz4-java's JNI, :125,163,273).  in_len[i] <= 2^25 (MAX_BLOCK_SIZE); out capacity >=
+ * nx_lz4_max_compressed_length (= LZ4_compressBound).  Bit-exact with LZ4_compress_default: the
+ * oracle's restatement is pinned byte-for-byte against pyarrow's bundled liblz4. */
 size_t nx_lz4_max_compressed_length(size_t n);
 int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                             const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream);
 
 /* Replaces LZ4FastDecompressor.decompress as Lz4FrameDecoder.decode calls it for one
- * BLOCK_TYPE_COMPRESSED block (Lz4FrameDecoder.java:199-208; lz4-java 1.8.0, third-party, parity
- * unpinned): block i = in[in_off[i] .. +in_len[i]) must decode to exactly out_len[i] bytes at
+ * BLOCK_TYPE_COMPRESSED block (Lz4FrameDecoder.java:199-208; lz4-java 1.8.0 = liblz4's
+ * LZ4_decompress_fast, restated from the published block format): block i = in[in_off[i] .. +in_len[i]) must decode to exactly out_len[i] bytes at
  * out + out_off[i].  status NX_OK / NX_ERR_LZ4_MALFORMED.  Same parse/expand kernels as Snappy. */
 int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                             const uint64_t* out_off, const uint32_t* out_len, int32_t* status, uint32_t n, void* stream);

@@ -1036,7 +1036,7 @@ struct nx_lz4_frame_encoder {
 
 extern "C" nx_lz4_frame_encoder* nx_lz4_frame_encoder_new(int32_t block_size) {
     // compressionLevel(blockSize) :158-166; the device block encoder takes blocks below 32 MiB
-    if (block_size < 64 || block_size >= (1 << 25)) return nullptr;
+    if (block_size < 64 || block_size > (1 << 25)) return nullptr;
     auto* e = new nx_lz4_frame_encoder();
     if (!e->g.ok) {
         delete e;

@@ -1,17 +1,21 @@
 // lz4.hip — LZ4 block encoder, one lane per block.
 //
-// Lz4FrameEncoder compresses each block with lz4-java 1.8.0's LZ4Compressor
-// (Lz4FrameEncoder.java:259-275), a third-party dependency absent from the reference, so its exact
-// output cannot be pinned here.  This kernel is bit-exact with the oracle's greedy block compressor
-// (oracle/netty_oracle.c orc_lz4_compress): a 4096-entry hash of the 4 bytes at each probed position
-// (the step over misses grows by one every 64 misses, LZ4's skip acceleration), matches of >= 4
-// bytes extended to at most 5 bytes before the end, the last
-// 5 bytes always literal and no match starting in the last 12 (the block-format end rules every
-// LZ4 decoder relies on).  Its blocks decode with nx_lz4_decode_batch and any LZ4 block decoder.
+// Lz4FrameEncoder compresses each block with lz4-java 1.8.0's fastCompressor()
+// (Lz4FrameEncoder.java:125,163,273), i.e. liblz4's LZ4_compress_default.  This kernel is that
+// algorithm, bit-exact with the oracle's restatement (oracle/netty_oracle.c orc_lz4_compress),
+// which tests/test_oracle_kat.py pins byte-for-byte against pyarrow's bundled liblz4:
+//   * blocks < 65547 bytes (LZ4_64Klimit): the byU16 table, 8192 slots hashed from the 4 bytes at a
+//     position (LZ4_hash4), no distance check; longer blocks: the byU32 table, 4096 slots hashed
+//     from the low 5 of the 8 bytes at a position (LZ4_hash5), matches farther than 65535 skipped;
+//   * a fresh table reads as all zeros = position 0 (a real candidate, as in liblz4);
+//   * the search step grows by one every 64 misses (skipTrigger 6), found matches are extended
+//     backwards over equal bytes (catch up) and forwards up to 5 bytes before the end, and after a
+//     match position ip-2 is inserted and ip is tested at once (a zero-literal sequence).
 //
-// Like the Snappy encoder, each lane owns a hash table in an HBM workspace; entries carry a 16-bit
-// stamp (the lane's chunk counter) above the 16-bit position, so a table is never cleared between
-// chunks.
+// Each lane owns a 32 KiB table in an HBM workspace.  Small blocks store stamp << 16 | index
+// (a stamp mismatch reads as the zeroed table), so the table is never cleared between blocks;
+// a large block zeroes its 4096 slots before and after itself, so none of its raw indices can pass
+// a later small block's stamp check.
 #include <algorithm>
 #include <map>
 #include <mutex>
@@ -20,65 +24,130 @@
 namespace nx {
 namespace lz4 {
 
-constexpr int kHashLog = 12;
-constexpr int kMinMatch = 4, kLastLiterals = 5, kMfLimit = 12;
+constexpr int kMinMatch = 4, kLastLiterals = 5, kMfLimit = 12, kMinLength = 13;
+constexpr int32_t k64KLimit = 65536 + kMfLimit - 1;
+constexpr uint32_t kTableSlots = 8192;  // byU16 slots (the byU32 table uses the first 4096)
 
 typedef uint32_t __attribute__((aligned(1))) u32u;
+typedef uint64_t __attribute__((aligned(1))) u64u;
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const u32u*>(p); }
+__device__ __forceinline__ uint64_t ld64(const uint8_t* p) { return *reinterpret_cast<const u64u*>(p); }
 
-__device__ __forceinline__ uint32_t put_len(uint8_t* out, uint32_t op, uint32_t v) {  // extension of a length >= 15
-    v -= 15u;
-    while (v >= 255u) {
-        out[op++] = 255u;
-        v -= 255u;
-    }
+template <bool Large>
+__device__ __forceinline__ uint32_t hash_at(const uint8_t* p) {
+    if (!Large) return (ld32(p) * 2654435761u) >> (32 - 13);                       // LZ4_hash4, byU16
+    return (uint32_t)(((ld64(p) << 24) * 889523592379ull) >> (64 - 12));           // LZ4_hash5, byU32
+}
+
+__device__ __forceinline__ uint32_t put_len(uint8_t* out, uint32_t op, uint32_t v) {  // 255-run of a length >= 15
+    for (; v >= 255u; v -= 255u) out[op++] = 255u;
     out[op++] = (uint8_t)v;
     return op;
 }
 
-// Large == false: blocks of <= 64 KiB, entries = stamp << 16 | position (no clearing).
-// Large == true: blocks of up to 32 MiB (Lz4FrameEncoder block sizes above the default), entries =
-// position + 1 in a table the lane zeroes before the block and again after it, so no stale entry
-// can pass a later small block's stamp check (stamps start at 1).
+// Large == false: blocks < 65547 bytes, entries stamp << 16 | index.  Large == true: blocks of up
+// to 32 MiB, raw indices in a table the lane zeroes before and after the block.
 template <bool Large>
 __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint8_t* __restrict__ out,
                                  uint32_t* __restrict__ table, uint32_t stamp) {
-    uint32_t op = 0;
-    int32_t anchor = 0, ip = 0, search = 64;
-    const int32_t mlimit = n - kMfLimit;
     const uint32_t stag = stamp << 16;
+#define XCH(h, v) __hip_atomic_exchange(table + (h), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#define PUT(h, v) __hip_atomic_store(table + (h), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#define ENT(i) (Large ? (uint32_t)(i) : (stag | (uint32_t)(i)))
+#define IDX(e) (Large ? (int32_t)(e) : (((e) & 0xFFFF0000u) == stag ? (int32_t)((e) & 0xFFFFu) : 0))
     if (Large)
-        for (uint32_t k = 0; k < (1u << kHashLog); ++k) __hip_atomic_store(table + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (n >= kMfLimit + 1 && ip <= mlimit) {
-        const uint32_t w = ld32(in + ip);
-        const uint32_t h = (w * 2654435761u) >> (32 - kHashLog);
-        const uint32_t e = __hip_atomic_exchange(table + h, Large ? (uint32_t)ip + 1u : (stag | (uint32_t)ip), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-        const int32_t ref = Large ? (int32_t)e - 1 : ((e & 0xFFFF0000u) == stag ? (int32_t)(e & 0xFFFFu) : -1);
-        if (ref < 0 || ip - ref > 65535 || ld32(in + ref) != w) {
-            ip += search++ >> 6;  // LZ4's skip acceleration (skipTrigger 6), as the oracle
-            continue;
+        for (uint32_t k = 0; k < 4096u; ++k) PUT(k, 0u);
+    uint32_t op = 0;
+    int32_t ip = 0, anchor = 0;
+    const int32_t mflimit_plus_one = n - kMfLimit + 1, matchlimit = n - kLastLiterals;
+    if (n >= kMinLength) {
+        PUT(hash_at<Large>(in), ENT(0));  // first byte
+        ip = 1;
+        uint32_t forward_h = hash_at<Large>(in + 1);
+        for (;;) {
+            int32_t match;
+            {   // find a match
+                int32_t forward_ip = ip, step = 1, search_nb = 1 << 6;
+                for (;;) {
+                    const uint32_t h = forward_h;
+                    const int32_t current = forward_ip;
+                    ip = forward_ip;
+                    forward_ip += step;
+                    step = search_nb++ >> 6;
+                    if (forward_ip > mflimit_plus_one) goto last_literals;
+                    forward_h = hash_at<Large>(in + forward_ip);
+                    match = IDX(XCH(h, ENT(current)));
+                    if (Large && match + 65535 < current) continue;  // too far
+                    if (ld32(in + match) == ld32(in + ip)) break;
+                }
+            }
+            while (ip > anchor && match > 0 && in[ip - 1] == in[match - 1]) {  // catch up
+                --ip;
+                --match;
+            }
+            uint32_t token = op++;
+            {
+                const uint32_t lit = (uint32_t)(ip - anchor);
+                if (lit >= 15u) {
+                    out[token] = 15u << 4;
+                    op = put_len(out, op, lit - 15u);
+                } else {
+                    out[token] = (uint8_t)(lit << 4);
+                }
+                for (uint32_t k = 0; k < lit; ++k) out[op + k] = in[anchor + k];
+                op += lit;
+            }
+            for (;;) {  // _next_match
+                const uint32_t off = (uint32_t)(ip - match);
+                out[op++] = (uint8_t)off;
+                out[op++] = (uint8_t)(off >> 8);
+                int32_t mc = 0;
+                while (ip + kMinMatch + mc + 4 <= matchlimit) {
+                    const uint32_t x = ld32(in + ip + kMinMatch + mc) ^ ld32(in + match + kMinMatch + mc);
+                    if (x) {
+                        mc += __builtin_ctz(x) >> 3;
+                        goto counted;
+                    }
+                    mc += 4;
+                }
+                while (ip + kMinMatch + mc < matchlimit && in[ip + kMinMatch + mc] == in[match + kMinMatch + mc]) ++mc;
+            counted:
+                ip += mc + kMinMatch;
+                if (mc >= 15) {
+                    out[token] += 15u;
+                    op = put_len(out, op, (uint32_t)(mc - 15));
+                } else {
+                    out[token] += (uint8_t)mc;
+                }
+                anchor = ip;
+                if (ip >= mflimit_plus_one) goto last_literals;
+                PUT(hash_at<Large>(in + ip - 2), ENT(ip - 2));  // fill table
+                const int32_t mi = IDX(XCH(hash_at<Large>(in + ip), ENT(ip)));  // test next position
+                if ((!Large || mi + 65535 >= ip) && ld32(in + mi) == ld32(in + ip)) {
+                    match = mi;
+                    token = op++;
+                    out[token] = 0;
+                    continue;
+                }
+                break;
+            }
+            forward_h = hash_at<Large>(in + ++ip);  // prepare next loop
         }
-        search = 64;
-        int32_t ml = kMinMatch;
-        while (ip + ml < n - kLastLiterals && in[ref + ml] == in[ip + ml]) ++ml;
-        const uint32_t lit = (uint32_t)(ip - anchor);
-        const uint32_t mc = (uint32_t)(ml - kMinMatch);
-        out[op++] = (uint8_t)(((lit >= 15u ? 15u : lit) << 4) | (mc >= 15u ? 15u : mc));
-        if (lit >= 15u) op = put_len(out, op, lit);
-        for (uint32_t k = 0; k < lit; ++k) out[op + k] = in[anchor + k];
-        op += lit;
-        out[op++] = (uint8_t)((ip - ref) & 255);
-        out[op++] = (uint8_t)((ip - ref) >> 8);
-        if (mc >= 15u) op = put_len(out, op, mc);
-        ip += ml;
-        anchor = ip;
     }
+last_literals:
+#undef XCH
+#undef PUT
+#undef ENT
+#undef IDX
     if (Large)
-        for (uint32_t k = 0; k < (1u << kHashLog); ++k) __hip_atomic_store(table + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t k = 0; k < 4096u; ++k) __hip_atomic_store(table + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t lit = (uint32_t)(n - anchor);  // last literals
-    out[op++] = (uint8_t)((lit >= 15u ? 15u : lit) << 4);
-    if (lit >= 15u) op = put_len(out, op, lit);
+    if (lit >= 15u) {
+        out[op++] = 15u << 4;
+        op = put_len(out, op, lit - 15u);
+    } else {
+        out[op++] = (uint8_t)(lit << 4);
+    }
     for (uint32_t k = 0; k < lit; ++k) out[op + k] = in[anchor + k];
     return op + lit;
 }
@@ -90,16 +159,16 @@ __global__ void __launch_bounds__(256) k_lz4_encode(const uint8_t* __restrict__ 
                                                     uint32_t stamp_base) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nthreads = gridDim.x * blockDim.x;
-    uint32_t* table = workspace + (size_t)tid * (1u << kHashLog);
+    uint32_t* table = workspace + (size_t)tid * kTableSlots;
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
         const uint32_t len = in_len[c];
-        if (len >= (1u << 25)) {
+        if (len > (1u << 25)) {
             out_len[c] = 0;
             status[c] = NX_ERR_INVALID_ARG;
             continue;
         }
-        out_len[c] = len > 65536u ? encode_block<true>(in + in_off[c], (int32_t)len, out + out_off[c], table, 0u)
+        out_len[c] = (int32_t)len >= k64KLimit ? encode_block<true>(in + in_off[c], (int32_t)len, out + out_off[c], table, 0u)
                                   : encode_block<false>(in + in_off[c], (int32_t)len, out + out_off[c], table, stamp_base + iter + 1u);
         status[c] = NX_OK;
     }
@@ -122,7 +191,7 @@ constexpr uint32_t kMaxStamp = 0xFFFFu;
 extern "C" size_t nx_lz4_max_compressed_length(size_t n) { return n + n / 255 + 16; }
 
 // Replaces LZ4Compressor.compress as Lz4FrameEncoder.flushBufferedData calls it for one block
-// (Lz4FrameEncoder.java:259-275); in_len[i] <= 65536 (the default block size, :59).
+// (Lz4FrameEncoder.java:259-275); in_len[i] <= 2^25 (MAX_BLOCK_SIZE, Lz4Constants.java / :175-178).
 extern "C" int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                        const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream) {
     if (n == 0) return NX_OK;
@@ -133,7 +202,7 @@ extern "C" int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off
     const hipStream_t st = (hipStream_t)stream;
     const size_t want = (size_t)cus * 16 * 64;  // 16 waves per CU, as the Snappy encoder
     const size_t threads = n < want ? ((n + 255) / 256) * 256 : want;
-    const size_t per = (1u << nx::lz4::kHashLog) * sizeof(uint32_t);
+    const size_t per = nx::lz4::kTableSlots * sizeof(uint32_t);
     std::lock_guard<std::mutex> lk(g_lz4_mu);
     Lz4Workspace& W = g_lz4_ws[{dev, st}];
     if (W.ws == nullptr || W.threads < threads) {

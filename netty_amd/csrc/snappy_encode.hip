@@ -335,11 +335,10 @@ __global__ void __launch_bounds__(256, NX_ENC_MINBLK) k_snappy_encode(const uint
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                        const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
                                                        int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
-                                                       uint32_t stamp_base, uint32_t alias) {
+                                                       uint32_t stamp_base) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nthreads = gridDim.x * blockDim.x;
-    // alias != 0 is a timing experiment only (NX_ENC_ALIAS): lanes share tables, output is wrong
-    uint32_t* table = workspace + (size_t)(alias ? tid % alias : tid) * 16384u;
+    uint32_t* table = workspace + (size_t)tid * 16384u;
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
         const uint32_t len = in_len[c];
@@ -392,7 +391,7 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
     int dev = 0, cus = 256;
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    static const unsigned waves_per_cu = getenv("NX_ENC_WAVES") ? (unsigned)atoi(getenv("NX_ENC_WAVES")) : kEncWavesPerCU;
+    constexpr unsigned waves_per_cu = kEncWavesPerCU;
     const hipStream_t st = (hipStream_t)stream;
     const size_t want = (size_t)cus * waves_per_cu * 64;
     const size_t threads = n < want ? ((n + kEncBlock - 1) / kEncBlock) * kEncBlock : want;
@@ -416,10 +415,8 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
             NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.threads * per, st));
             W.stamp = 0;
         }
-        static const uint32_t alias = getenv("NX_ENC_ALIAS") ? (uint32_t)atoi(getenv("NX_ENC_ALIAS")) : 0u;
-        static const bool swap = getenv("NX_ENC_SWAP") ? atoi(getenv("NX_ENC_SWAP")) != 0 : true;
-        hipLaunchKernelGGL(swap ? nx::enc::k_snappy_encode<true> : nx::enc::k_snappy_encode<false>, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
-                           in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp, alias);
+        hipLaunchKernelGGL(nx::enc::k_snappy_encode<true>, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
+                           in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp);
         NX_HIP_CHECK(hipGetLastError());
         W.stamp += iters;
     }

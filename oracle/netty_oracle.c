@@ -862,7 +862,7 @@ size_t orc_lzf_frame_encode(const uint8_t* in, size_t n, int32_t compress_thresh
 #define JR_MASK ((1LL << 48) - 1)
 
 
-/* ================================================================== LZ4 block (parity unpinned) */
+/* ================================================================== LZ4 block */
 int32_t orc_lz4_decompress(const uint8_t* in, int32_t in_len, uint8_t* out, int32_t out_len) {
     int64_t ip = 0, op = 0;
     for (;;) {
@@ -905,53 +905,116 @@ int32_t orc_lz4_decompress(const uint8_t* in, int32_t in_len, uint8_t* out, int3
 
 size_t orc_lz4_max_compressed(size_t n) { return n + n / 255 + 16; }
 
-static size_t lz4_put_len(uint8_t* out, size_t op, int64_t v) { /* extension bytes of a length >= 15 */
-    v -= 15;
-    while (v >= 255) {
-        out[op++] = 255;
-        v -= 255;
-    }
-    out[op++] = (uint8_t)v;
-    return op;
+/* LZ4_compress_default (acceleration 1) of liblz4, the block compressor lz4-java's JNI
+ * fastCompressor() runs for Lz4FrameEncoder (Lz4FrameEncoder.java:125,163,273; lz4-java 1.8.0,
+ * pom.xml:946-950, bundles liblz4 1.9.x): LZ4_compress_fast_extState -> LZ4_compress_generic on a
+ * freshly zeroed state (currentOffset 0, so base = source and a zero entry means position 0).
+ * Blocks shorter than LZ4_64Klimit (65536 + MFLIMIT - 1) use the byU16 table: 8192 u16 indices
+ * hashed from the 4 bytes at p (LZ4_hash4, HASHLOG + 1 = 13 bits), no distance check; longer blocks
+ * use byU32: 4096 u32 indices hashed from the low 5 bytes of the 8 at p (LZ4_hash5, 12 bits) and
+ * matches farther than LZ4_DISTANCE_MAX (65535) are skipped.  Match search steps grow by one every
+ * 64 misses (LZ4_skipTrigger 6), a found match is extended backwards over equal bytes ("catch up")
+ * and forwards up to iend - LASTLITERALS, and after each match the position two bytes back is
+ * inserted and the current one tested at once.  Pinned byte-for-byte against pyarrow's bundled
+ * liblz4 (Codec('lz4_raw')) by tests/test_oracle_kat.py. */
+enum { LZ4_MINMATCH = 4, LZ4_LASTLIT = 5, LZ4_MFLIMIT = 12, LZ4_MINLEN = 13, LZ4_64KLIMIT = 65536 + 11 };
+
+static uint32_t lz4_rd32(const uint8_t* p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static uint32_t lz4_hash(const uint8_t* p, int u16) {
+    if (u16) return (lz4_rd32(p) * 2654435761u) >> (32 - 13);          /* LZ4_hash4, byU16 */
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - 12));     /* LZ4_hash5, byU32 */
 }
 
 int32_t orc_lz4_compress(const uint8_t* in, int32_t n, uint8_t* out) {
-    enum { HBITS = 12, MINMATCH = 4, LASTLITERALS = 5, MFLIMIT = 12 };
-    int32_t table[1 << HBITS];
-    for (int i = 0; i < (1 << HBITS); ++i) table[i] = -1;
+    static uint32_t table[8192];
+    const int u16 = n < LZ4_64KLIMIT;
+    memset(table, 0, sizeof table);
     size_t op = 0;
-    int32_t anchor = 0, ip = 0, search = 64;
-    const int32_t mlimit = n - MFLIMIT;
-    while (n >= MFLIMIT + 1 && ip <= mlimit) {
-        uint32_t w;
-        memcpy(&w, in + ip, 4);
-        const uint32_t h = (w * 2654435761u) >> (32 - HBITS);
-        const int32_t ref = table[h];
-        table[h] = ip;
-        uint32_t rw = 0;
-        if (ref >= 0) memcpy(&rw, in + ref, 4);
-        if (ref < 0 || ip - ref > 65535 || rw != w) {
-            ip += search++ >> 6; /* LZ4's skip acceleration (skipTrigger 6): longer steps over misses */
-            continue;
+    int64_t ip = 0, anchor = 0;
+    const int64_t mflimit_plus_one = (int64_t)n - LZ4_MFLIMIT + 1, matchlimit = (int64_t)n - LZ4_LASTLIT;
+    if (n < LZ4_MINLEN) goto last_literals;
+    table[lz4_hash(in, u16)] = 0;                                          /* first byte */
+    ip = 1;
+    uint32_t forward_h = lz4_hash(in + ip, u16);
+    for (;;) {
+        int64_t match;
+        {   /* find a match */
+            int64_t forward_ip = ip;
+            int32_t step = 1, search_nb = 1 << 6;
+            for (;;) {
+                const uint32_t h = forward_h;
+                const int64_t current = forward_ip;
+                const int64_t match_index = table[h];
+                ip = forward_ip;
+                forward_ip += step;
+                step = search_nb++ >> 6;
+                if (forward_ip > mflimit_plus_one) goto last_literals;
+                match = match_index;
+                forward_h = lz4_hash(in + forward_ip, u16);
+                table[h] = (uint32_t)current;
+                if (!u16 && match_index + 65535 < current) continue;       /* too far */
+                if (lz4_rd32(in + match) == lz4_rd32(in + ip)) break;
+            }
         }
-        search = 64;
-        int32_t ml = MINMATCH;
-        while (ip + ml < n - LASTLITERALS && in[ref + ml] == in[ip + ml]) ++ml;
-        const int64_t lit = ip - anchor;
-        const size_t tok = op++;
-        out[tok] = (uint8_t)(((lit >= 15 ? 15 : lit) << 4) | ((ml - MINMATCH) >= 15 ? 15 : (ml - MINMATCH)));
-        if (lit >= 15) op = lz4_put_len(out, op, lit);
-        memcpy(out + op, in + anchor, (size_t)lit);
-        op += (size_t)lit;
-        out[op++] = (uint8_t)((ip - ref) & 255);
-        out[op++] = (uint8_t)((ip - ref) >> 8);
-        if (ml - MINMATCH >= 15) op = lz4_put_len(out, op, ml - MINMATCH);
-        ip += ml;
-        anchor = ip;
+        while (ip > anchor && match > 0 && in[ip - 1] == in[match - 1]) { --ip; --match; }   /* catch up */
+        size_t token;
+        {   /* literals */
+            const int64_t lit = ip - anchor;
+            token = op++;
+            if (lit >= 15) {
+                out[token] = 15 << 4;
+                int64_t len = lit - 15;
+                for (; len >= 255; len -= 255) out[op++] = 255;
+                out[op++] = (uint8_t)len;
+            } else {
+                out[token] = (uint8_t)(lit << 4);
+            }
+            memcpy(out + op, in + anchor, (size_t)lit);
+            op += (size_t)lit;
+        }
+        for (;;) {  /* _next_match */
+            const int64_t off = ip - match;
+            out[op++] = (uint8_t)off;
+            out[op++] = (uint8_t)(off >> 8);
+            int64_t mc = 0;
+            while (ip + LZ4_MINMATCH + mc < matchlimit && in[ip + LZ4_MINMATCH + mc] == in[match + LZ4_MINMATCH + mc]) ++mc;
+            ip += mc + LZ4_MINMATCH;
+            if (mc >= 15) {
+                out[token] += 15;
+                mc -= 15;
+                for (; mc >= 255; mc -= 255) out[op++] = 255;
+                out[op++] = (uint8_t)mc;
+            } else {
+                out[token] += (uint8_t)mc;
+            }
+            anchor = ip;
+            if (ip >= mflimit_plus_one) goto last_literals;
+            table[lz4_hash(in + ip - 2, u16)] = (uint32_t)(ip - 2);          /* fill table */
+            const uint32_t h = lz4_hash(in + ip, u16);                        /* test next position */
+            const int64_t match_index = table[h];
+            table[h] = (uint32_t)ip;
+            if ((u16 || match_index + 65535 >= ip) && lz4_rd32(in + match_index) == lz4_rd32(in + ip)) {
+                match = match_index;
+                token = op++;
+                out[token] = 0;
+                continue;
+            }
+            break;
+        }
+        forward_h = lz4_hash(in + ++ip, u16);                                 /* prepare next loop */
     }
-    const int64_t lit = n - anchor; /* last literals */
-    out[op++] = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
-    if (lit >= 15) op = lz4_put_len(out, op, lit);
+last_literals:;
+    const int64_t lit = (int64_t)n - anchor;
+    if (lit >= 15) {
+        out[op++] = 15 << 4;
+        int64_t acc = lit - 15;
+        for (; acc >= 255; acc -= 255) out[op++] = 255;
+        out[op++] = (uint8_t)acc;
+    } else {
+        out[op++] = (uint8_t)(lit << 4);
+    }
     memcpy(out + op, in + anchor, (size_t)lit);
     op += (size_t)lit;
     return (int32_t)op;

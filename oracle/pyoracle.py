@@ -193,7 +193,7 @@ def lzf_decode_chunk(body: bytes, out_len: int):
 
 
 def lz4_compress(data: bytes) -> bytes:
-    """A valid LZ4 block for `data` (greedy test compressor; lz4-java's exact output is unpinned)."""
+    """LZ4_compress_default(data) — liblz4's fast block compressor as lz4-java runs it (pinned vs pyarrow lz4_raw)."""
     L = lib()
     out = _buf(L.orc_lz4_max_compressed(len(data)))
     n = L.orc_lz4_compress(bytes(data), len(data), out)

@@ -21,12 +21,12 @@ if [[ $STAGE == all || $STAGE == test ]]; then
   if [[ $rc -ge 2 ]]; then exit $rc; fi
 fi
 if [[ $STAGE == all || $STAGE == bench ]]; then
-  run timeout -k 10 600 python bench.py --chunks "$CHUNKS" --steps 3 --warmup 1 --cpu-seconds 6 > "$OUT/bench.log" 2>&1 || exit 1
+  run timeout -k 10 600 python bench.py --total-chunks "$CHUNKS" --weak-chunks 0 --steps 3 --warmup 1 --cpu-seconds 6 > "$OUT/bench.log" 2>&1 || exit 1
 fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
   export TMPDIR=/tmp
   cd /tmp && run timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-      python "$ROOT/bench.py" --chunks "$CHUNKS" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-alt --no-frame-scan > "$OUT/prof.log" 2>&1 || exit 1
+      python "$ROOT/bench.py" --total-chunks "$CHUNKS" --weak-chunks 0 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-alt --no-frame-scan > "$OUT/prof.log" 2>&1 || exit 1
   cd "$ROOT"
 fi
 if [[ $STAGE == all || $STAGE == pmc ]]; then

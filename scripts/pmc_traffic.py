@@ -1,12 +1,16 @@
-"""Summarise the FETCH_SIZE / WRITE_SIZE passes of scripts/pmc_traffic.sh per kernel (per dispatch,
-and per 64 KiB chunk of one pass: bench.py decodes every chunk twice — the timed step and the
-corrupted-CRC check — and the decoder launches one parse/expand pair per 262 144 frames).  FETCH_SIZE is doubled as MI355X_MICROARCH.md's HBM section prescribes for
-gfx950 (it tallies 128-B read requests at 64 B); WRITE_SIZE is taken as is.  Units: bytes."""
-import collections, csv, glob, json, sys
+"""Summarise the FETCH_SIZE / WRITE_SIZE passes of scripts/pmc_traffic.sh per kernel: HBM bytes per
+dispatch and per 64 KiB chunk.  The passes run bench.py with --total-chunks = --sub-chunks = CHUNKS,
+so every dispatch of the CRC / encode / decode kernels covers exactly CHUNKS chunks.  FETCH_SIZE is
+doubled as MI355X_MICROARCH.md's HBM section prescribes for gfx950 (it tallies 128-B read requests
+at 64 B); WRITE_SIZE is taken as is.  The summary records the digest of the kernel sources it was
+taken on (bench.source_digest()); bench.py uses a summary only when that digest matches.  Units: bytes."""
+import collections, csv, glob, json, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
 root, chunks = sys.argv[1], int(sys.argv[2])
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
-grid = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for f in glob.glob(f"{root}/traffic_{c}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
@@ -15,14 +19,15 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
                 continue
             agg[name][r["Counter_Name"]] += float(r["Counter_Value"]) * 1024.0  # KiB -> bytes
             disp[(name, c)].add(r["Dispatch_Id"])
-out = {"source": f"rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE; bench.py --chunks {chunks} --steps 1 --warmup 0",
-       "fetch_correction": 2.0, "chunks": chunks, "kernels": {}}
+out = {"source": f"rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE; bench.py --total-chunks {chunks} "
+                 f"--sub-chunks {chunks} --steps 1 --warmup 0 --weak-chunks 0",
+       "source_digest": bench.source_digest(), "fetch_correction": 2.0, "chunks_per_dispatch": chunks, "kernels": {}}
 for name, d in agg.items():
     nd = max(len(disp[(name, "FETCH_SIZE")]), len(disp[(name, "WRITE_SIZE")]), 1)
-    per_pass = -(-chunks // 262144) if name.startswith("nx::dec::k_parse") or name.startswith("nx::dec::k_expand") else 1
-    passes = max(nd // per_pass, 1)
     fetch, write = d.get("FETCH_SIZE", 0.0), d.get("WRITE_SIZE", 0.0)
-    out["kernels"][name] = {"dispatches": nd, "passes": passes, "fetch_bytes": fetch, "write_bytes": write,
+    out["kernels"][name] = {"dispatches": nd, "fetch_bytes": fetch, "write_bytes": write,
                             "hbm_bytes_total": 2.0 * fetch + write,
-                            "hbm_bytes_per_chunk": (2.0 * fetch + write) / (chunks * passes)}
+                            "read_bytes_per_chunk": 2.0 * fetch / (chunks * nd),
+                            "write_bytes_per_chunk": write / (chunks * nd),
+                            "hbm_bytes_per_chunk": (2.0 * fetch + write) / (chunks * nd)}
 print(json.dumps(out, indent=1))

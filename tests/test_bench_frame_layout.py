@@ -58,6 +58,11 @@ def test_bench_frame_layout(oracle, monkeypatch):
             seen["chunks"] = k
             raise _Done()
 
+    class Leg:  # the fields of bench.SnappyRoundTrip that bench_frame_scan reads
+        src, dec, sub, n = None, None, m, m
+
+    leg = Leg()
+    leg.enc, leg.eoff, leg.elen, leg.crc = enc, eoff, elen, crc
     with pytest.raises(_Done):
-        bench.bench_frame_scan(torch, FakeB, torch.device("cpu"), None, enc, eoff, elen, crc, None, m, per, reps=1)
+        bench.bench_frame_scan(torch, FakeB, torch.device("cpu"), leg, m, per, reps=1)
     assert seen["chunks"] == m

@@ -1,6 +1,7 @@
 """GPU parity: LZ4 block decode (nx_lz4_decode_batch, §8f row 4) against the oracle's restatement of
-the LZ4 block format (oracle/netty_oracle.c orc_lz4_decompress; parity against lz4-java itself is
-unpinned): bytes and status, through the same parse/expand kernels as Snappy."""
+the LZ4 block format (oracle/netty_oracle.c orc_lz4_decompress), and LZ4 block encode
+(nx_lz4_encode_batch) against the oracle's LZ4_compress_default restatement (pinned against
+liblz4 itself): bytes and status."""
 import random
 
 import pytest

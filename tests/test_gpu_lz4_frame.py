@@ -177,8 +177,8 @@ def test_lz4_frame_large_blocks(dev, B, oracle, block_size):
 
 
 def test_lz4_encode_large_and_small_blocks_mixed(dev, B, oracle):
-    """Blocks over 64 KiB (32-bit table entries, table cleared per block) interleaved with small
-    stamped blocks in one launch: bytes equal the oracle's compressor for every block."""
+    """Blocks over 64 KiB (liblz4's byU32 table, cleared per block) interleaved with small stamped
+    blocks in one launch: bytes equal the oracle's compressor (= liblz4) for every block."""
     data = []
     for i in range(6):
         data.append(oracle.textgen_chunk(300 + i, 200000 + 50000 * i))
@@ -192,6 +192,28 @@ def test_lz4_encode_large_and_small_blocks_mixed(dev, B, oracle):
     outh, oo, ol = out.cpu().numpy().tobytes(), ooff.cpu().tolist(), olen.cpu().tolist()
     for i, d in enumerate(data):
         assert outh[oo[i]:oo[i] + ol[i]] == oracle.lz4_compress(d), i
+
+
+def test_lz4_encode_one_lane_large_then_small(dev, B, oracle):
+    """one lane encoding a large (byU32, raw-index) block and then a stamped small block in
+    the same launch.  The launch has cus * 1024 lanes and lane t encodes blocks t, t + lanes, ...;
+    with lanes + 3 blocks, lane 1 takes the 1 MiB block at index 1 and then the text block at
+    1 + lanes.  Every block must equal liblz4's bytes (the oracle)."""
+    lanes = torch.cuda.get_device_properties(dev).multi_processor_count * 1024
+    small = [b"abcdefghijklmnopq"] * (lanes + 3)
+    small[1] = oracle.textgen_chunk(5, 1 << 20)
+    small[1 + lanes] = oracle.textgen_chunk(6, 40000)
+    small[2] = oracle.textgen_chunk(7, 1 << 25)              # MAX_BLOCK_SIZE itself
+    small[2 + lanes] = oracle.textgen_chunk(8, 65536)
+    inp, off, ln = B.pack(small, dev, align=1)
+    out, ooff = B.out_slots([B.lz4_max_compressed_length(len(d)) for d in small], dev, align=1)
+    olen, st = B.lz4_encode(inp, off, ln, out, ooff)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    oo, ol = ooff.cpu().tolist(), olen.cpu().tolist()
+    for i in (0, 1, 2, 1 + lanes, 2 + lanes, lanes + 2):
+        got = out[oo[i]:oo[i] + ol[i]].cpu().numpy().tobytes()
+        assert got == oracle.lz4_compress(small[i]), i
 
 
 @pytest.mark.parametrize("block_size", [1 << 17, 1 << 20])

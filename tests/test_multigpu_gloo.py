@@ -89,3 +89,86 @@ def test_gloo_world2_offsets_and_stream(tmp_path, oracle):
         o = int(rows[r][2])
         stream[o:o + sizes[r]] = blobs[r]
     assert bytes(stream) == whole
+
+
+# ---------------------------------------------------------------- bench.py's own N>1 path over gloo
+class _OracleLeg:
+    """CPU stand-in for bench.SnappyRoundTrip (test-only: the oracle is the per-rank worker here).
+    It records the chunk range it was given and encodes/decodes those chunks on the CPU."""
+
+    def __init__(self, outdir, rank, first, n):
+        from oracle import pyoracle as O
+        self.O, self.outdir, self.rank, self.first, self.n, self.sub = O, outdir, rank, first, n, n
+        self.blob = b""
+        self.steps = 0
+
+    def step(self, record=False):
+        O = self.O
+        parts = [O.snappy_encode(O.textgen_chunk(i, 65536)) for i in range(self.first, self.first + self.n)]
+        self.blob = b"".join(parts)
+        self.steps += 1
+        self.ok = all(O.snappy_decode(p, 65536)[1] == O.textgen_chunk(i, 65536)
+                      for i, p in zip(range(self.first, self.first + self.n), parts))
+
+    def verify(self, rank):
+        with open(os.path.join(self.outdir, f"b{rank}.bin"), "wb") as f:
+            f.write(self.blob)
+        with open(os.path.join(self.outdir, f"b{rank}.txt"), "w") as f:
+            f.write(f"{self.first} {self.n} {self.steps}\n")
+        return self.ok, True
+
+    def comp_bytes(self):
+        return len(self.blob)
+
+    def kernel_ms_per_step(self, steps):
+        return 1.0, 1.0, 1.0
+
+
+class _LegFactory:
+    def __init__(self, outdir, rank):
+        self.outdir, self.rank = outdir, rank
+
+    def __call__(self, first, n):
+        return _OracleLeg(self.outdir, self.rank, first, n)
+
+
+def _bench_rank(rank, world, port, outdir):
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import bench
+    args = bench.parse(["--gpus", str(world), "--total-chunks", "7", "--steps", "2", "--warmup", "1"])
+    lines = []
+    line, ok = bench.run_rank(args, rank, world, rank, backend="gloo", leg_factory=_LegFactory(outdir, rank),
+                              emit=lines.append)
+    with open(os.path.join(outdir, f"json{rank}.txt"), "w") as f:
+        f.write("\n".join(lines))
+    assert ok
+
+
+def test_bench_run_rank_world2_gloo(tmp_path, oracle):
+    """bench.py's run_rank at world 2 over gloo: disjoint shards that cover every chunk, stream offsets
+    equal to shard.exchange_offsets' (the all-gathered compressed totals), the max-over-ranks timing
+    and exactly one JSON line (rank 0) with n_gpus == 2 and strong scaling over the fixed total."""
+    import json
+    world = 2
+    mp.start_processes(_bench_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    rec = [open(tmp_path / f"b{r}.txt").read().split() for r in range(world)]
+    ranges = [(int(a), int(a) + int(b)) for a, b, _ in rec]
+    assert ranges == [(0, 3), (3, 7)]
+    assert all(int(s) == 3 for _, _, s in rec)  # warmup 1 + steps 2
+    sizes = [len(open(tmp_path / f"b{r}.bin", "rb").read()) for r in range(world)]
+    out0 = open(tmp_path / "json0.txt").read().strip().splitlines()
+    out1 = open(tmp_path / "json1.txt").read().strip()
+    assert len(out0) == 1 and out1 == ""
+    line = json.loads(out0[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["verified"] is True
+    assert line["config"]["global_chunks"] == 7 and line["compressed_bytes_per_rank"] == sizes
+    assert line["shard"] == {"first_chunk": 0, "chunks": 3, "stream_offset": 0, "stream_bytes": sum(sizes)}
+    assert line["value"] > 0 and line["steps"] == 2
+    whole = b"".join(oracle.snappy_encode(oracle.textgen_chunk(i, 65536)) for i in range(7))
+    assert open(tmp_path / "b0.bin", "rb").read() + open(tmp_path / "b1.bin", "rb").read() == whole

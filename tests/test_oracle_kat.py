@@ -233,8 +233,7 @@ def test_snappy_frame_scan_partial_and_skip(oracle):
 
 
 def test_lz4_block_roundtrip_and_errors(oracle):
-    """LZ4 block restatement (parity unpinned against lz4-java, see oracle/netty_oracle.h): round trips
-    and the malformed-input cases the GPU decoder must agree on."""
+    """LZ4 block restatement: round trips and the malformed-input cases the GPU decoder must agree on."""
     import random
     rng = random.Random(4)
     for data in [b"", b"a", b"hello", bytes(100), oracle.textgen_chunk(1, 65536), oracle.java_random_bytes(2, 5000),
@@ -248,6 +247,50 @@ def test_lz4_block_roundtrip_and_errors(oracle):
            (b"\x10a\x02\x00\x50bcdef", 10), (b"\x10a\x01", 10), (b"\xf0", 20), (b"\xf0\xff", 300)]
     for blk, n in bad:
         assert oracle.lz4_decompress(blk, n)[0] == -50, (blk, n)
+
+
+def _lz4_corpus(oracle):
+    import random
+    rng = random.Random(5)
+    corpus = dict(_identity_corpus(oracle))
+    corpus.update({"hello": b"hello", "min_len_12": b"abcdabcdabcd", "min_len_13": b"abcdabcdabcda",
+                   "period7": bytes((i % 7) for i in range(70000)), "blank_64k": bytes(65536)})
+    for k, n in enumerate([17, 100, 4095, 4096, 32767, 65535, 65536, 65546, 65547, 65548, 131072, 300000]):
+        corpus[f"text_{n}"] = oracle.textgen_chunk(1000 + k, n)
+    for k, n in enumerate([13, 64, 1000, 65536, 70000]):
+        corpus[f"random_{n}"] = rng.randbytes(n)
+    for k in range(12):
+        corpus[f"text_rand_{k}"] = oracle.textgen_chunk(2000 + k, rng.randrange(1, 70000))
+    return corpus
+
+
+def test_lz4_compress_equals_liblz4(oracle):
+    """The LZ4 block compressor is liblz4's LZ4_compress_default, the compressor lz4-java's JNI
+    fastCompressor() runs for Lz4FrameEncoder (Lz4FrameEncoder.java:125,163,273): byte-for-byte
+    equal to pyarrow's bundled liblz4 (Codec('lz4_raw')) on both table types (byU16 below
+    65547 bytes, byU32 above), random and text data, and the end-of-block limits."""
+    pa = pytest.importorskip("pyarrow")
+    z = pa.Codec("lz4_raw")
+    for name, data in _lz4_corpus(oracle).items():
+        assert oracle.lz4_compress(data) == z.compress(data).to_pybytes(), name
+        assert oracle.lz4_decompress(oracle.lz4_compress(data), len(data)) == (0, data), name
+
+
+def test_snappy_blocks_decode_with_libsnappy(oracle, kat):
+    """Independent decode cross-check: pyarrow's bundled libsnappy decodes every
+    Netty-format block the oracle encodes (Netty's encoder output differs from libsnappy's, so this
+    checks the format, not the encoder's choices, which the SnappyTest KATs pin)."""
+    pa = pytest.importorskip("pyarrow")
+    sn = pa.Codec("snappy")
+    corpus = _identity_corpus(oracle)
+    corpus["issue_1002"] = bytes.fromhex(kat["identity_inputs"]["issue_1002"])
+    for i in range(8):
+        corpus[f"text_{i}"] = oracle.textgen_chunk(i, 65536)
+    for name, data in corpus.items():
+        for L in {min(len(data), 65536), min(len(data), 32767), min(len(data), 65535)}:
+            blk = data[:L]
+            enc = oracle.snappy_encode(blk)
+            assert sn.decompress(enc, decompressed_size=L).to_pybytes() == blk, (name, L)
 
 
 # ---- LZ4 frame (§8f row 4): Lz4FrameEncoder / Lz4FrameDecoder / Lz4XXHash32 ----
