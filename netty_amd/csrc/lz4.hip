@@ -54,7 +54,7 @@ __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint
 #define XCH(h, v) __hip_atomic_exchange(table + (h), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #define PUT(h, v) __hip_atomic_store(table + (h), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #define ENT(i) (Large ? (uint32_t)(i) : (stag | (uint32_t)(i)))
-#define IDX(e) (Large ? (int32_t)(e) : (((e) & 0xFFFF0000u) == stag ? (int32_t)((e) & 0xFFFFu) : 0))
+    auto idx = [stag](uint32_t e) -> int32_t { return Large ? (int32_t)e : ((e & 0xFFFF0000u) == stag ? (int32_t)(e & 0xFFFFu) : 0); };
     if (Large)
         for (uint32_t k = 0; k < 4096u; ++k) PUT(k, 0u);
     uint32_t op = 0;
@@ -76,7 +76,7 @@ __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint
                     step = search_nb++ >> 6;
                     if (forward_ip > mflimit_plus_one) goto last_literals;
                     forward_h = hash_at<Large>(in + forward_ip);
-                    match = IDX(XCH(h, ENT(current)));
+                    match = idx(XCH(h, ENT(current)));
                     if (Large && match + 65535 < current) continue;  // too far
                     if (ld32(in + match) == ld32(in + ip)) break;
                 }
@@ -122,7 +122,7 @@ __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint
                 anchor = ip;
                 if (ip >= mflimit_plus_one) goto last_literals;
                 PUT(hash_at<Large>(in + ip - 2), ENT(ip - 2));  // fill table
-                const int32_t mi = IDX(XCH(hash_at<Large>(in + ip), ENT(ip)));  // test next position
+                const int32_t mi = idx(XCH(hash_at<Large>(in + ip), ENT(ip)));  // test next position
                 if ((!Large || mi + 65535 >= ip) && ld32(in + mi) == ld32(in + ip)) {
                     match = mi;
                     token = op++;
@@ -138,7 +138,6 @@ last_literals:
 #undef XCH
 #undef PUT
 #undef ENT
-#undef IDX
     if (Large)
         for (uint32_t k = 0; k < 4096u; ++k) __hip_atomic_store(table + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t lit = (uint32_t)(n - anchor);  // last literals
