@@ -95,5 +95,7 @@
 #define NX_ERR_INVALID_ARG                (-100)
 #define NX_ERR_HIP                        (-101)
 #define NX_ERR_NO_DEVICE                  (-102)
+/* A kernel's own loop bound tripped (a bug guard: the kernel stopped instead of spinning). */
+#define NX_ERR_INTERNAL                   (-103)
 
 #endif

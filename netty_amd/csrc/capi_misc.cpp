@@ -41,6 +41,7 @@ extern "C" const char* nx_status_string(int32_t s) {
         case NX_ERR_INVALID_ARG: return "invalid argument";
         case NX_ERR_HIP: return "HIP runtime error";
         case NX_ERR_NO_DEVICE: return "no GPU device";
+        case NX_ERR_INTERNAL: return "kernel loop guard tripped (internal error)";
         default: return "unknown status";
     }
 }

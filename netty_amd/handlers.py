@@ -93,7 +93,7 @@ class _Decoder:
         out = [C.string_at(msgs[i].data, msgs[i].len) if msgs[i].len else b"" for i in range(nmsg.value)]
         del self._cum[:consumed.value]
         if rc != 0:
-            if rc in (-100, -101, -102):
+            if rc in (-100, -101, -102, -103):
                 raise RuntimeError(f"{type(self).__name__}: native failure {rc} ({_lib.status_string(rc)})")
             msg = err.value.decode() if err.value else _lib.status_string(rc)
             e = DecompressionException(msg)

@@ -18,4 +18,4 @@ for _ in range(R):
     a.record(); B.snappy_encode(src, off, ln, enc, eoff, out_len=elen, status=est); b.record(); torch.cuda.synchronize()
     t.append(a.elapsed_time(b))
 ms = min(t)
-print(f"encode n={n} waves={os.environ.get('NX_ENC_WAVES','16')} ms={ms:.1f} GiB/s={n*L/ms/1e3/2**30*1e3:.2f} C={int(elen.sum())}", flush=True)
+print(f"encode n={n} ms={ms:.1f} GiB/s={n*L/ms/1e3/2**30*1e3:.2f} C={int(elen.sum())}", flush=True)
