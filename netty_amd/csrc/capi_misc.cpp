@@ -34,7 +34,8 @@ extern "C" const char* nx_status_string(int32_t s) {
         case NX_ERR_SNAPPY_SKIPPABLE_BEFORE_ID: return "Received RESERVED_SKIPPABLE tag before STREAM_IDENTIFIER";
         case NX_ERR_SNAPPY_UNCOMPRESSED_TOO_LARGE: return "Received UNCOMPRESSED_DATA larger than 65540 bytes";
         case NX_ERR_SNAPPY_DECOMPRESSED_TOO_LARGE: return "Received COMPRESSED_DATA that contains uncompressed data that exceeds 65536 bytes";
-        case NX_ERR_SNAPPY_CHUNK_TOO_SHORT: return "Received a data chunk shorter than its checksum";
+        case NX_ERR_SNAPPY_CHUNK_TOO_SHORT:  // not a DecompressionException: ByteBuf fails (SnappyFrameDecoder.java:171-215)
+            return "java.lang.IllegalArgumentException: data chunk shorter than its 4-byte checksum (ByteBuf read past the chunk)";
         case NX_ERR_SNAPPY_UNSKIPPABLE: return "Found reserved unskippable chunk type";
         case NX_ERR_LZ4_MALFORMED: return "Malformed LZ4 input";
         case NX_SCAN_LIST_FULL: return "chunk list full (call again from consumed)";

@@ -217,6 +217,13 @@ extern "C" nx_snappy_frame_decoder* nx_snappy_frame_decoder_new(int32_t validate
 extern "C" void nx_snappy_frame_decoder_free(nx_snappy_frame_decoder* d) { delete d; }
 
 namespace {
+// AbstractByteBuf.checkReadableBytes0's IndexOutOfBoundsException (AbstractByteBuf.java:1465-1471), as
+// ByteToMessageDecoder's DecoderException(cause) reports it; the buffer's toString() is omitted.
+const char* bytebuf_oob(char* buf, size_t cap, size_t reader, int len, size_t writer) {
+    snprintf(buf, cap, "java.lang.IndexOutOfBoundsException: readerIndex(%zu) + length(%d) exceeds writerIndex(%zu)", reader, len,
+             writer);
+    return buf;
+}
 enum class SAct { Stream, Skip, Uncomp, Comp, Error };
 struct SnappyAction {
     SAct kind;
@@ -231,7 +238,8 @@ struct SnappyAction {
 
 // One SnappyFrameDecoder.decode() call over in[p..n) (SnappyFrameDecoder.java:85-231), with the
 // chunk work deferred.  Returns false when decode() would return without consuming (need more).
-bool snappy_parse_one(const uint8_t* in, size_t n, size_t& p, bool& started, uint64_t& skip, std::vector<SnappyAction>& acts) {
+bool snappy_parse_one(const uint8_t* in, size_t n, size_t& p, bool& started, uint64_t& skip, bool validate,
+                      std::vector<SnappyAction>& acts) {
     if (skip) {  // :91-99
         uint64_t s = skip < (uint64_t)(n - p) ? skip : (uint64_t)(n - p);
         p += s;
@@ -273,7 +281,33 @@ bool snappy_parse_one(const uint8_t* in, size_t n, size_t& p, bool& started, uin
     if (type == 0) {  // COMPRESSED_DATA (:180-224)
         if (!started) return fail("Received COMPRESSED_DATA tag before STREAM_IDENTIFIER");
         if (inSize < 4 + (size_t)chunkLength) return false;
-        if (chunkLength < 4) return fail("Received COMPRESSED_DATA shorter than its checksum");
+        if (chunkLength < 4) {
+            // No DecompressionException in the reference: skipBytes(4) then readIntLE() run past the
+            // chunk (:194-195), and the negative slice fails in ByteBuf (:208 / :215), wrapped as a
+            // DecoderException (ByteToMessageDecoder.java:297-300).  The preamble check comes first.
+            if (inSize < 8) return fail(bytebuf_oob(buf, sizeof buf, p + 4, 4, n));
+            uint32_t pre = 0;
+            int bi = 0;
+            bool done = false;
+            for (size_t q = p + 8; q < n; ++q) {
+                pre |= (uint32_t)(in[q] & 0x7f) << (bi++ * 7);
+                if (!(in[q] & 0x80)) {
+                    done = true;
+                    break;
+                }
+                if (bi >= 4) return fail("Preamble is greater than 4 bytes");
+            }
+            if (done && pre > 65536) return fail("Received COMPRESSED_DATA that contains uncompressed data that exceeds 65536 bytes");
+            if (validate) {  // in.writerIndex(readerIndex + chunkLength - 4) below the reader index (:208)
+                snprintf(buf, sizeof buf,
+                         "java.lang.IndexOutOfBoundsException: readerIndex: %zu, writerIndex: %zu "
+                         "(expected: 0 <= readerIndex <= writerIndex <= capacity)", p + 8, p + 4 + (size_t)chunkLength);
+                return fail(buf);
+            }
+            snprintf(buf, sizeof buf, "java.lang.IllegalArgumentException: minimumReadableBytes : %d (expected: >= 0)",
+                     (int)chunkLength - 4);  // in.readSlice(chunkLength - 4) (:215)
+            return fail(buf);
+        }
         a.crc = le32(in + p + 4);
         // snappy.getPreamble(in): the varint is read from the cumulation (Snappy.java:404-441)
         uint32_t ulen = 0;
@@ -302,7 +336,21 @@ bool snappy_parse_one(const uint8_t* in, size_t n, size_t& p, bool& started, uin
         if (!started) return fail("Received UNCOMPRESSED_DATA tag before STREAM_IDENTIFIER");
         if (chunkLength > 65536 + 4) return fail("Received UNCOMPRESSED_DATA larger than 65540 bytes");
         if (inSize < 4 + (size_t)chunkLength) return false;
-        if (chunkLength < 4) return fail("Received UNCOMPRESSED_DATA shorter than its checksum");
+        if (chunkLength < 4) {
+            // (:171-178) readIntLE / skipBytes(4) run past the chunk; with validation the CRC32C of a
+            // negative length is the empty CRC (Crc32c.update's loop does not run, mask(0) =
+            // 0xa282ead8, DecompressionException unless the 4 bytes read happen to equal it); then
+            // readRetainedSlice(chunkLength - 4) fails in ByteBuf.  Heap-buffer behaviour.
+            if (inSize < 8) return fail(bytebuf_oob(buf, sizeof buf, p + 4, 4, n));
+            const uint32_t ck = le32(in + p + 4);
+            if (validate && ck != 0xa282ead8u) {
+                snprintf(buf, sizeof buf, "mismatching checksum: a282ead8 (expected: %x)", ck);
+                return fail(buf);
+            }
+            snprintf(buf, sizeof buf, "java.lang.IllegalArgumentException: minimumReadableBytes : %d (expected: >= 0)",
+                     (int)chunkLength - 4);
+            return fail(buf);
+        }
         a.kind = SAct::Uncomp;
         a.crc = le32(in + p + 4);
         a.data = p + 8;
@@ -357,7 +405,7 @@ extern "C" int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, co
         size_t p = rd;
         bool started = d->started;
         uint64_t skip = d->skip;
-        while (p < n && snappy_parse_one(in, n, p, started, skip, acts)) {
+        while (p < n && snappy_parse_one(in, n, p, started, skip, d->validate, acts)) {
         }
         // ---- one GPU batch: decode every compressed chunk; CRC every uncompressed one if validating
         std::vector<int> comp_idx, unc_idx;

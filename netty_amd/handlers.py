@@ -96,7 +96,9 @@ class _Decoder:
             if rc in (-100, -101, -102, -103):
                 raise RuntimeError(f"{type(self).__name__}: native failure {rc} ({_lib.status_string(rc)})")
             msg = err.value.decode() if err.value else _lib.status_string(rc)
-            e = DecompressionException(msg)
+            # a ByteBuf failure (IndexOutOfBounds / IllegalArgument) reaches the pipeline as the
+            # DecoderException ByteToMessageDecoder wraps it in (ByteToMessageDecoder.java:297-300)
+            e = DecoderException(msg) if msg.startswith("java.lang.") else DecompressionException(msg)
             e.decoded = out  # messages fired before the failing chunk
             e.status = rc
             raise e

@@ -85,6 +85,37 @@ def test_snappy_decoder_corrupted_is_sticky(nx):
     assert not ch.write_inbound(bytes.fromhex("ff060000734e61507059010900006f982eb96e65747479"))
 
 
+SID = bytes.fromhex("ff060000734e61507059")
+
+
+@pytest.mark.parametrize("validate", [False, True])
+def test_snappy_decoder_chunk_shorter_than_checksum(nx, validate):
+    """A data chunk whose length is below its 4-byte checksum is no DecompressionException in the
+    reference: readIntLE / skipBytes run past the chunk and the negative slice length fails inside
+    ByteBuf (SnappyFrameDecoder.java:171-178, 194-215), which ByteToMessageDecoder wraps in a
+    DecoderException (ByteToMessageDecoder.java:297-300).  Heap-buffer messages."""
+    tail = b"\x00" * 8  # bytes after the short chunk, so the 4-byte reads succeed
+    # UNCOMPRESSED_DATA of length 2: readRetainedSlice(-2) (with validation the empty CRC differs first)
+    with pytest.raises(nx.DecoderException) as ei:
+        nx.EmbeddedChannel(nx.SnappyFrameDecoder(validate)).write_inbound(SID + b"\x01\x02\x00\x00ab" + tail)
+    if validate:
+        assert isinstance(ei.value, nx.DecompressionException)
+        assert str(ei.value) == "mismatching checksum: a282ead8 (expected: 6261)"
+    else:
+        assert not isinstance(ei.value, nx.DecompressionException)
+        assert str(ei.value) == "java.lang.IllegalArgumentException: minimumReadableBytes : -2 (expected: >= 0)"
+    # COMPRESSED_DATA of length 1: readSlice(-3), or writerIndex below readerIndex when validating
+    with pytest.raises(nx.DecoderException) as ei:
+        nx.EmbeddedChannel(nx.SnappyFrameDecoder(validate)).write_inbound(SID + b"\x00\x01\x00\x00a" + tail)
+    assert not isinstance(ei.value, nx.DecompressionException)
+    assert str(ei.value).startswith("java.lang.IndexOutOfBoundsException" if validate else
+                                    "java.lang.IllegalArgumentException: minimumReadableBytes : -3")
+    # too few bytes after the header for the 4-byte checksum read: IndexOutOfBoundsException
+    with pytest.raises(nx.DecoderException) as ei:
+        nx.EmbeddedChannel(nx.SnappyFrameDecoder(validate)).write_inbound(SID + b"\x00\x01\x00\x00a")
+    assert str(ei.value) == "java.lang.IndexOutOfBoundsException: readerIndex(14) + length(4) exceeds writerIndex(15)"
+
+
 @pytest.mark.parametrize("jumbo", [False, True])
 def test_snappy_identity_and_parity(nx, oracle, kat, jumbo):
     for name, data in _corpus(oracle, kat).items():
