@@ -242,3 +242,30 @@ def test_pack_batch_gathers_slots():
         want = torch.cat([src[int(o):int(o) + int(l)] for o, l in zip(src_off, lens)])
         got = dst.cpu()[shift:shift + want.numel()]
         assert torch.equal(got, want)
+
+
+def test_snappy_encode_stamp_wrap_many_chunks_per_lane(dev, B, oracle):
+    """one encoder lane encodes more than 14 chunks, so the host splits the batch
+    into launches and re-zeroes the 4-bit-stamped table workspace before the stamps wrap
+    (snappy_encode.hip nx_snappy_encode_batch).  Lane t encodes chunks t, t + lanes, ...; the chunks of
+    the first and last lane in every launch, and a random sample, must equal the oracle's bytes."""
+    lanes = torch.cuda.get_device_properties(dev).multi_processor_count * 16 * 64
+    n, L = lanes * 15 + 7, 160
+    src = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    B.textgen(src, 0, n, L)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * L
+    ln = torch.full((n,), L, dtype=torch.int32, device=dev)
+    cap = (B.snappy_max_compressed_length(L) + 15) // 16 * 16
+    out = torch.empty(n * cap, dtype=torch.uint8, device=dev)
+    ooff = torch.arange(n, dtype=torch.int64, device=dev) * cap
+    olen, st = B.snappy_encode(src, off, ln, out, ooff)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    rng = random.Random(5)
+    pick = sorted({k * lanes + t for k in range(16) for t in (0, lanes - 1)} | {rng.randrange(n) for _ in range(300)})
+    pick = [i for i in pick if i < n]
+    ol = olen[pick].cpu().tolist()
+    for i, m in zip(pick, ol):
+        got = out[i * cap:i * cap + m].cpu().numpy().tobytes()
+        assert got == oracle.snappy_encode(oracle.textgen_chunk(i, L)), i
+    del src, out
