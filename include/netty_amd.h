@@ -304,6 +304,40 @@ void nx_lz4_frame_decoder_free(nx_lz4_frame_decoder* d);
 int32_t nx_lz4_frame_decoder_decode(nx_lz4_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
                                     const nx_msg** msgs, size_t* n_msgs, const char** err_msg);
 
+/* ------------------------------------------------------------------ (3) asynchronous cross-channel batcher
+ * Netty calls one handler per channel on that channel's event loop (ByteToMessageDecoder.java:194-196),
+ * which must never block (BlockHound, common/.../internal/Hidden.java:38), and one call carries only a
+ * few chunks.  A batcher turns the encode()/decode() calls of MANY handles into jobs of one GPU launch:
+ * submit() runs the handle's framing at once (its stream state advances in call order) and returns a
+ * ticket without touching the GPU; flush() launches every pending job (CRC32C + Snappy.encode of all
+ * encoder slices, Snappy.decode + CRC verify of all decoder chunks, one finish kernel writing each
+ * job's result straight into mapped pinned host memory); poll() never blocks; result() gives zero-copy
+ * views valid until release().  Thread-safe. */
+typedef struct nx_batcher nx_batcher;
+nx_batcher* nx_batcher_new(void);
+void nx_batcher_free(nx_batcher* b);
+/* Page-lock a pooled direct ByteBuf's memory (ByteBuf.memoryAddress(), ByteBuf.java:2395-2403) so
+ * encoder inputs in it are DMA'd to the device without a staging copy. */
+int32_t nx_host_register(void* ptr, size_t len);
+int32_t nx_host_unregister(void* ptr);
+/* SnappyFrameEncoder.encode(ctx, in, out) as a job.  in_registered != 0: `in` lies in registered
+ * memory and stays valid until the job completes (DMA'd at flush); else it is copied now (the caller
+ * may release it, as MessageToByteEncoder.java:109 does).  Result: one message, the framed bytes.
+ * Returns the ticket (> 0) or a negative status. */
+int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx_batcher* b, const uint8_t* in, size_t n,
+                                       int32_t in_registered);
+/* SnappyFrameDecoder.decode(ctx, in, out) over the cumulation in[0..n) as a job: *consumed = bytes the
+ * caller discards now (the chunk payloads are copied).  Result: the decoded messages in order, then
+ * (status < 0) the first failure's message; a failed job marks the decoder corrupted (:227-230). */
+int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
+                                       size_t* consumed);
+int32_t nx_batcher_flush(nx_batcher* b);
+int32_t nx_batcher_poll(nx_batcher* b, int64_t ticket);  /* 1 done, 0 pending, < 0 error; never blocks */
+int32_t nx_batcher_wait(nx_batcher* b, int64_t ticket);  /* blocks (flushes first if needed): NX_OK */
+int32_t nx_batcher_result(nx_batcher* b, int64_t ticket, const nx_msg** msgs, size_t* n_msgs, const char** err_msg);
+int32_t nx_batcher_release(nx_batcher* b, int64_t ticket);
+int32_t nx_batcher_stats(nx_batcher* b, uint64_t* flushes, uint64_t* launches, uint64_t* chunks);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,7 @@ the reference's handler API (see ``netty_amd.handlers``) and a device-resident b
 """
 from ._lib import load as _load_lib  # noqa: F401  (raises if the HIP library is not built)
 from .handlers import (  # noqa: F401
+    Batcher,
     CompressionException,
     DecoderException,
     DecompressionException,

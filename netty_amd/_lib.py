@@ -57,6 +57,19 @@ _SIGS = {
     "nx_memcpy_h2d": (i32, [vp, vp, sz, vp]),
     "nx_memcpy_d2h": (i32, [vp, vp, sz, vp]),
     "nx_stream_sync": (i32, [vp]),
+    # asynchronous cross-channel batcher
+    "nx_batcher_new": (vp, []),
+    "nx_batcher_free": (None, [vp]),
+    "nx_host_register": (i32, [vp, sz]),
+    "nx_host_unregister": (i32, [vp]),
+    "nx_snappy_frame_encoder_submit": (i64, [vp, vp, vp, sz, i32]),
+    "nx_snappy_frame_decoder_submit": (i64, [vp, vp, vp, sz, C.POINTER(sz)]),
+    "nx_batcher_flush": (i32, [vp]),
+    "nx_batcher_poll": (i32, [vp, i64]),
+    "nx_batcher_wait": (i32, [vp, i64]),
+    "nx_batcher_result": (i32, [vp, i64, C.POINTER(C.POINTER(NxMsg)), C.POINTER(sz), C.POINTER(C.c_char_p)]),
+    "nx_batcher_release": (i32, [vp, i64]),
+    "nx_batcher_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]),
     # host handler layer
     "nx_snappy_frame_encoder_new": (vp, [i32]),
     "nx_snappy_frame_encoder_free": (None, [vp]),

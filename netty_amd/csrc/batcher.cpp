@@ -1,0 +1,717 @@
+// batcher.cpp — asynchronous, cross-channel batching executor for the Snappy frame handlers.
+//
+// Netty runs one SnappyFrameEncoder / SnappyFrameDecoder per channel on that channel's event loop
+// (ByteToMessageDecoder.java:194-196) and the event loop must not block (BlockHound,
+// common/.../internal/Hidden.java:38).  One encode()/decode() call carries ~1-33 chunks, far too few
+// to fill an MI355X, so the batcher turns those calls into jobs of one shared GPU launch:
+//
+//   submit  (event loop, non-blocking)  the handler's framing runs on the host at once — the stream
+//           identifier and slice split of SnappyFrameEncoder.encode (SnappyFrameEncoder.java:79-117),
+//           the chunk-header walk of SnappyFrameDecoder.decode (:85-231) — so the handle's state
+//           advances in call order; the chunk payloads are copied into a pinned staging arena
+//           (MessageToByteEncoder releases `in` when encode() returns, :109), or, for an encoder input
+//           the caller registered with nx_host_register and keeps alive, DMA'd straight from it.
+//   flush   one H2D copy of the staging arena, then ONE launch per kernel for every job of every
+//           channel: CRC32C + Snappy.encode of all encoder slices, Snappy.decode (+ CRC verify) of all
+//           compressed chunks, CRC32C of uncompressed chunks, and a finish kernel that writes each
+//           job's result — framed encoder output, or the decoder's messages — straight into mapped
+//           pinned host memory (only the result bytes cross PCIe; no D2H of capacity-sized slots).
+//   poll    hipEventQuery: 1 when the job's batch is done (never blocks); wait() blocks (tests).
+//   result  zero-copy views of the job's output in the pinned arena, valid until release().
+//
+// Results are applied in submission order per decoder: a failing chunk marks the decoder corrupted
+// (:227-230) and the jobs submitted after it on that decoder deliver nothing (Java skips all later
+// input, :86-89).  Limitation of the asynchronous path: a validating decoder whose compressed chunk
+// decodes fewer bytes than its length (the leftover is re-parsed as a chunk header in Java, :206-212)
+// fails that job with NX_ERR_FRAME_CORRUPT; the synchronous nx_snappy_frame_decoder_decode is exact.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+#include "../../include/netty_amd.h"
+#include "frame_parse.hpp"
+#include "handles.hpp"
+#include "nx_common.hpp"
+
+namespace nx {
+namespace bt {
+
+struct EncSlice {  // one SnappyFrameEncoder slice (:99-112) or the small-message unencoded chunk (:114-124)
+    uint64_t in_off;
+    uint64_t slot_off;
+    uint32_t len;
+    uint32_t comp;
+};
+struct EncJob {
+    uint64_t out_off;  // in the mapped output arena
+    uint32_t s0, ns;   // slices
+    uint32_t stream_start;
+    uint32_t pad;
+};
+struct DecAct {  // one UNCOMPRESSED_DATA (kind 1) or COMPRESSED_DATA (kind 2) chunk, in stream order
+    uint64_t in_off;  // payload in the device input arena
+    uint32_t len;     // payload bytes
+    uint32_t kind;
+    uint32_t chunk;   // kind 2: index into the decode batch; kind 1: index into the uncompressed-CRC batch
+    uint32_t crc;     // stored masked CRC32C
+};
+struct DecJob {
+    uint64_t out_off;
+    uint32_t a0, na;
+    uint32_t validate;
+    uint32_t pad;
+};
+struct DecRes {  // per action, written by k_dec_finish
+    uint64_t off;    // message bytes in the output arena
+    uint32_t len;
+    int32_t status;  // NX_OK or the chunk's error
+    uint32_t crc;    // computed masked CRC32C (uncompressed chunks; compressed: see decode crc_out)
+    uint32_t cons;   // compressed: input bytes consumed
+};
+
+// Copy n bytes device -> mapped host with the whole wave: 16-byte stores at 16-byte-aligned
+// destinations (one PCIe write per lane), bytes at the ragged ends.
+__device__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n, int lane) {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    typedef v4 __attribute__((aligned(1))) v4u;
+    const uint32_t head = (uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u) < n ? (uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u) : n;
+    if ((uint32_t)lane < head) dst[lane] = src[lane];
+    const uint32_t nv = (n - head) >> 4;
+    for (uint32_t i = lane; i < nv; i += 64)
+        *reinterpret_cast<v4*>(dst + head + 16u * i) = *reinterpret_cast<const v4u*>(src + head + 16u * i);
+    const uint32_t t = head + (nv << 4);
+    if (t + (uint32_t)lane < n) dst[t + lane] = src[t + lane];
+}
+
+// one wave per encoder job: [stream identifier] then [type][len+4: u24 LE][masked crc LE][payload] per slice
+__global__ void __launch_bounds__(256) k_enc_finish(const uint8_t* __restrict__ din, const uint8_t* __restrict__ slots,
+                                                    const EncSlice* __restrict__ sl, const uint32_t* __restrict__ clen,
+                                                    const uint32_t* __restrict__ crc, const EncJob* __restrict__ jobs, uint32_t njobs,
+                                                    uint8_t* __restrict__ out, uint64_t* __restrict__ res_len) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= njobs) return;
+    const EncJob J = jobs[j];
+    uint8_t* o = out + J.out_off;
+    uint64_t pos = 0;
+    if (J.stream_start) {  // ff 06 00 00 "sNaPpY" (SnappyFrameEncoder.java:52-54)
+        const uint64_t v = lane < 8 ? (0x50614e73000006ffull >> (8 * lane)) : (0x5970ull >> (8 * (lane - 8)));  // LE bytes
+        if (lane < 10) o[lane] = (uint8_t)v;
+        pos = 10;
+    }
+    for (uint32_t s = J.s0; s < J.s0 + J.ns; ++s) {
+        const EncSlice S = sl[s];
+        const uint32_t L = S.comp ? clen[s] : S.len;
+        const uint32_t cl = L + 4;  // setChunkLength (:126-132) / writeUnencodedChunk (:119-124)
+        const uint32_t c = crc[s];
+        if (lane < 8) {
+            const uint32_t b = lane == 0 ? (S.comp ? 0u : 1u) : lane < 4 ? (cl >> (8 * (lane - 1))) & 0xFF : (c >> (8 * (lane - 4))) & 0xFF;
+            o[pos + lane] = (uint8_t)b;
+        }
+        wave_copy(o + pos + 8, S.comp ? slots + S.slot_off : din + S.in_off, L, lane);
+        pos += 8 + L;
+    }
+    if (lane == 0) res_len[j] = pos;
+}
+
+// one wave per decoder job: the decoded messages back to back, stopping at the first failing chunk
+__global__ void __launch_bounds__(256) k_dec_finish(const uint8_t* __restrict__ din, const uint8_t* __restrict__ slots,
+                                                    const DecAct* __restrict__ acts, const DecJob* __restrict__ jobs, uint32_t njobs,
+                                                    const uint32_t* __restrict__ dlen, const uint32_t* __restrict__ dcons,
+                                                    const int32_t* __restrict__ dstat, const uint32_t* __restrict__ dcrc,
+                                                    const uint32_t* __restrict__ ucrc, uint8_t* __restrict__ out,
+                                                    DecRes* __restrict__ res) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= njobs) return;
+    const DecJob J = jobs[j];
+    uint64_t pos = J.out_off;
+    for (uint32_t a = J.a0; a < J.a0 + J.na; ++a) {
+        const DecAct A = acts[a];
+        DecRes R{pos, 0, NX_OK, 0, 0};
+        if (A.kind == 1) {
+            R.crc = ucrc[A.chunk];
+            R.len = A.len;
+            if (J.validate && R.crc != A.crc) R.status = NX_ERR_SNAPPY_CRC_MISMATCH;  // (:171-175)
+            else wave_copy(out + pos, din + A.in_off, A.len, lane);
+        } else {
+            R.status = dstat[A.chunk];
+            // the decode launch verifies CRCs when any decoder of the batch validates; a decoder
+            // built without validateChecksums ignores them (:205-216)
+            if (R.status == NX_ERR_SNAPPY_CRC_MISMATCH && !J.validate) R.status = NX_OK;
+            R.len = dlen[A.chunk];
+            R.crc = dcrc[A.chunk];
+            R.cons = dcons[A.chunk];
+            if (R.status == NX_OK) wave_copy(out + pos, slots + (uint64_t)A.chunk * 65536u, R.len, lane);
+        }
+        if (lane == 0) res[a] = R;
+        if (R.status != NX_OK) break;
+        pos += R.len;
+    }
+}
+
+}  // namespace bt
+}  // namespace nx
+
+using nx::bt::DecAct;
+using nx::bt::DecJob;
+using nx::bt::DecRes;
+using nx::bt::EncJob;
+using nx::bt::EncSlice;
+using nx::fr::SAct;
+using nx::fr::SnappyAction;
+
+namespace {
+
+struct Pinned {  // hipHostMalloc'd, mapped into the device address space; grows keeping its bytes
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    size_t cap = 0;
+    bool ensure(size_t n, size_t keep) {
+        if (n <= cap) return true;
+        size_t c = cap ? cap : (1u << 20);
+        while (c < n) c *= 2;
+        uint8_t *nh = nullptr, *nd = nullptr;
+        if (hipHostMalloc((void**)&nh, c, hipHostMallocMapped) != hipSuccess) return false;
+        if (hipHostGetDevicePointer((void**)&nd, nh, 0) != hipSuccess) {
+            (void)hipHostFree(nh);
+            return false;
+        }
+        if (h && keep) memcpy(nh, h, keep < cap ? keep : cap);
+        if (h) (void)hipHostFree(h);
+        h = nh;
+        d = nd;
+        cap = c;
+        return true;
+    }
+    ~Pinned() {
+        if (h) (void)hipHostFree(h);
+    }
+};
+
+struct Job {
+    uint64_t ticket = 0;
+    int kind = 0;  // 0 encode, 1 decode
+    nx_snappy_frame_decoder* dec = nullptr;
+    uint32_t index = 0;  // EncJob / DecJob index in its batch
+    std::vector<SnappyAction> acts;  // decode: the parsed actions (host copy, stream order)
+    std::string parse_err;           // decode: the header-level error after them, if any
+    bool has_parse_err = false;
+    bool applied = false;
+    int32_t status = NX_OK;
+    std::vector<nx_msg> msgs;
+    std::string err;
+};
+
+struct Batch {
+    Pinned staging;  // chunk payloads, then the device arrays (one H2D copy at flush)
+    size_t st_used = 0;
+    struct Direct {
+        const uint8_t* src;
+        size_t len;
+        uint64_t din_off;
+    };
+    std::vector<Direct> direct;  // registered encoder inputs, DMA'd at flush
+    std::vector<EncSlice> esl;
+    std::vector<EncJob> ejob;
+    uint64_t eslots = 0;
+    std::vector<DecAct> dact;
+    std::vector<DecJob> djob;
+    std::vector<uint64_t> dc_off;  // compressed chunks: payload offsets / lengths / expected CRC
+    std::vector<uint32_t> dc_len, dc_crc;
+    bool dc_validate = false;
+    std::vector<uint64_t> du_off;  // uncompressed chunks (CRC32C)
+    std::vector<uint32_t> du_len;
+    Pinned out;  // mapped result arena: job outputs, then the result records
+    uint64_t out_used = 0, res_enc = 0, res_dec = 0;
+    std::vector<Job*> jobs;
+    nx::h::DevBuf din, slots;
+    hipEvent_t ev = nullptr;
+    bool inflight = false, done = false;
+    size_t live = 0;  // jobs not yet released
+    void reset() {
+        st_used = 0;
+        direct.clear();
+        esl.clear();
+        ejob.clear();
+        eslots = 0;
+        dact.clear();
+        djob.clear();
+        dc_off.clear();
+        dc_len.clear();
+        dc_crc.clear();
+        dc_validate = false;
+        du_off.clear();
+        du_len.clear();
+        out_used = res_enc = res_dec = 0;
+        for (Job* j : jobs) delete j;
+        jobs.clear();
+        inflight = done = false;
+        live = 0;
+    }
+    uint8_t* stage(size_t n, uint64_t* din_off) {  // reserve n staging bytes (16-aligned)
+        const size_t at = (st_used + 15) & ~(size_t)15;
+        if (!staging.ensure(at + n + 16, st_used)) return nullptr;
+        st_used = at + n;
+        *din_off = at;
+        return staging.h + at;
+    }
+    bool reserve_out(size_t n, uint64_t* off) {
+        const uint64_t at = (out_used + 15) & ~15ull;
+        if (!out.ensure(at + n + 16, out_used)) return false;
+        out_used = at + n;
+        *off = at;
+        return true;
+    }
+    ~Batch() {
+        for (Job* j : jobs) delete j;
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
+
+}  // namespace
+
+struct nx_batcher {
+    std::mutex mu;
+    hipStream_t s = nullptr;
+    std::deque<Batch*> all;  // every batch object (collecting, in flight, or done)
+    Batch* cur = nullptr;    // the collecting batch
+    std::unordered_map<uint64_t, std::pair<Batch*, Job*>> tickets;
+    uint64_t next_ticket = 1;
+    uint64_t launches = 0, chunks = 0, flushes = 0;
+};
+
+namespace {
+
+Batch* fresh_batch(nx_batcher* b) {
+    for (Batch* x : b->all) {
+        if (x->inflight && x->live == 0 && hipEventQuery(x->ev) == hipSuccess) x->inflight = false;  // released unpolled
+        if (!x->inflight && x->live == 0 && x != b->cur) {
+            x->reset();
+            return x;
+        }
+    }
+    Batch* x = new Batch();
+    if (hipEventCreateWithFlags(&x->ev, hipEventDisableTiming) != hipSuccess) {
+        delete x;
+        return nullptr;
+    }
+    b->all.push_back(x);
+    return x;
+}
+
+Batch* collecting(nx_batcher* b) {
+    if (!b->cur) b->cur = fresh_batch(b);
+    return b->cur;
+}
+
+// Launch everything `bt` collected (batcher lock held).
+int32_t launch(nx_batcher* b, Batch* bt) {
+    const hipStream_t s = b->s;
+    const uint32_t nes = (uint32_t)bt->esl.size(), nej = (uint32_t)bt->ejob.size(), nda = (uint32_t)bt->dact.size();
+    const uint32_t ndj = (uint32_t)bt->djob.size(), ndc = (uint32_t)bt->dc_off.size(), ndu = (uint32_t)bt->du_off.size();
+    struct Lay {
+        uint64_t at = 0;
+        uint64_t put(uint64_t n) {
+            const uint64_t r = (at + 15) & ~15ull;
+            at = r + n;
+            return r;
+        }
+    } Lh, Ld;
+    // arrays the host fills (uploaded inside the staging arena)
+    const uint64_t o_esl = Lh.put(sizeof(EncSlice) * nes), o_ein = Lh.put(8ull * nes), o_eslot = Lh.put(8ull * nes),
+                   o_elen = Lh.put(4ull * nes), o_ejob = Lh.put(sizeof(EncJob) * nej), o_dact = Lh.put(sizeof(DecAct) * nda),
+                   o_djob = Lh.put(sizeof(DecJob) * ndj), o_dcoff = Lh.put(8ull * ndc), o_dclen = Lh.put(4ull * ndc),
+                   o_dccrc = Lh.put(4ull * ndc), o_dslot = Lh.put(8ull * ndc), o_duoff = Lh.put(8ull * ndu), o_dulen = Lh.put(4ull * ndu);
+    // arrays the kernels fill (device only)
+    const uint64_t o_eclen = Ld.put(4ull * nes), o_est = Ld.put(4ull * nes), o_ecrc = Ld.put(4ull * nes), o_dlen = Ld.put(4ull * ndc),
+                   o_dcons = Ld.put(4ull * ndc), o_dst = Ld.put(4ull * ndc), o_dcrc = Ld.put(4ull * ndc), o_ducrc = Ld.put(4ull * ndu);
+    uint64_t st_arr = 0;
+    uint8_t* h = bt->stage(Lh.at + 16, &st_arr);
+    if (!h) return NX_ERR_HIP;
+    std::vector<uint64_t> ein(nes), eslot(nes), dslot(ndc);
+    std::vector<uint32_t> elen(nes);
+    for (uint32_t i = 0; i < nes; ++i) {
+        ein[i] = bt->esl[i].in_off;
+        eslot[i] = bt->esl[i].slot_off;
+        elen[i] = bt->esl[i].len;
+    }
+    for (uint32_t i = 0; i < ndc; ++i) dslot[i] = (uint64_t)i * 65536u;
+    auto cp = [&](uint64_t off, const void* src, size_t n) {
+        if (n) memcpy(h + off, src, n);
+    };
+    cp(o_esl, bt->esl.data(), sizeof(EncSlice) * nes);
+    cp(o_ein, ein.data(), 8ull * nes);
+    cp(o_eslot, eslot.data(), 8ull * nes);
+    cp(o_elen, elen.data(), 4ull * nes);
+    cp(o_ejob, bt->ejob.data(), sizeof(EncJob) * nej);
+    cp(o_dact, bt->dact.data(), sizeof(DecAct) * nda);
+    cp(o_djob, bt->djob.data(), sizeof(DecJob) * ndj);
+    cp(o_dcoff, bt->dc_off.data(), 8ull * ndc);
+    cp(o_dclen, bt->dc_len.data(), 4ull * ndc);
+    cp(o_dccrc, bt->dc_crc.data(), 4ull * ndc);
+    cp(o_dslot, dslot.data(), 8ull * ndc);
+    cp(o_duoff, bt->du_off.data(), 8ull * ndu);
+    cp(o_dulen, bt->du_len.data(), 4ull * ndu);
+    // result records in the mapped arena, after the job outputs
+    if (!bt->reserve_out(8ull * nej + 8, &bt->res_enc) || !bt->reserve_out(sizeof(DecRes) * nda + 8, &bt->res_dec)) return NX_ERR_HIP;
+    if (!bt->din.ensure(bt->st_used + 16) || !bt->slots.ensure(bt->eslots + (uint64_t)ndc * 65536u + Ld.at + 64)) return NX_ERR_HIP;
+    uint8_t* din = bt->din.as<uint8_t>();
+    uint8_t* slots = bt->slots.as<uint8_t>();
+    uint8_t* dslots = slots + bt->eslots;
+    uint8_t* D = dslots + (uint64_t)ndc * 65536u;
+    D = reinterpret_cast<uint8_t*>(((uintptr_t)D + 15) & ~(uintptr_t)15);
+    if (hipMemcpyAsync(din, bt->staging.h, bt->st_used, hipMemcpyHostToDevice, s) != hipSuccess) return NX_ERR_HIP;
+    for (const Batch::Direct& dd : bt->direct)
+        if (hipMemcpyAsync(din + dd.din_off, dd.src, dd.len, hipMemcpyHostToDevice, s) != hipSuccess) return NX_ERR_HIP;
+    const uint8_t* A = din + st_arr;
+    int32_t r;
+    if (nes) {  // CRC32C + Snappy.encode of every encoder slice of every channel
+        r = nx_crc32c_masked_batch(din, (const uint64_t*)(A + o_ein), (const uint32_t*)(A + o_elen), (uint32_t*)(D + o_ecrc), nes, s);
+        if (r != NX_OK) return r;
+        r = nx_snappy_encode_batch(din, (const uint64_t*)(A + o_ein), (const uint32_t*)(A + o_elen), slots, (const uint64_t*)(A + o_eslot),
+                                   (uint32_t*)(D + o_eclen), (int32_t*)(D + o_est), nes, s);
+        if (r != NX_OK) return r;
+        hipLaunchKernelGGL(nx::bt::k_enc_finish, dim3((nej + 3) / 4), dim3(256), 0, s, din, slots, (const EncSlice*)(A + o_esl),
+                           (const uint32_t*)(D + o_eclen), (const uint32_t*)(D + o_ecrc), (const EncJob*)(A + o_ejob), nej, bt->out.d,
+                           (uint64_t*)(bt->out.d + bt->res_enc));
+        if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
+        b->launches += 3;
+        b->chunks += nes;
+    }
+    if (ndj) {  // Snappy.decode (+ fused CRC verify) of every compressed chunk, CRC32C of uncompressed ones
+        if (ndc) {
+            r = nx_snappy_decode_batch(din, (const uint64_t*)(A + o_dcoff), (const uint32_t*)(A + o_dclen), dslots,
+                                       (const uint64_t*)(A + o_dslot), nullptr, (uint32_t*)(D + o_dlen), (uint32_t*)(D + o_dcons),
+                                       (int32_t*)(D + o_dst), bt->dc_validate ? (const uint32_t*)(A + o_dccrc) : nullptr,
+                                       (uint32_t*)(D + o_dcrc), ndc, s);
+            if (r != NX_OK) return r;
+            b->launches += 1;
+        }
+        if (ndu) {
+            r = nx_crc32c_masked_batch(din, (const uint64_t*)(A + o_duoff), (const uint32_t*)(A + o_dulen), (uint32_t*)(D + o_ducrc), ndu, s);
+            if (r != NX_OK) return r;
+            b->launches += 1;
+        }
+        hipLaunchKernelGGL(nx::bt::k_dec_finish, dim3((ndj + 3) / 4), dim3(256), 0, s, din, dslots, (const DecAct*)(A + o_dact),
+                           (const DecJob*)(A + o_djob), ndj, (const uint32_t*)(D + o_dlen), (const uint32_t*)(D + o_dcons),
+                           (const int32_t*)(D + o_dst), (const uint32_t*)(D + o_dcrc), (const uint32_t*)(D + o_ducrc), bt->out.d,
+                           (DecRes*)(bt->out.d + bt->res_dec));
+        if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
+        b->launches += 1;
+        b->chunks += ndc + ndu;
+    }
+    if (hipEventRecord(bt->ev, s) != hipSuccess) return NX_ERR_HIP;
+    bt->inflight = true;
+    b->flushes += 1;
+    return NX_OK;
+}
+
+// The batch is complete: turn the result records into each job's messages, in submission order.
+void apply(Batch* bt) {
+    const uint64_t* res_len = reinterpret_cast<const uint64_t*>(bt->out.h + bt->res_enc);
+    const DecRes* dres = reinterpret_cast<const DecRes*>(bt->out.h + bt->res_dec);
+    char buf[160];
+    for (Job* j : bt->jobs) {
+        if (j->kind == 0) {
+            const EncJob& E = bt->ejob[j->index];
+            j->msgs.push_back({bt->out.h + E.out_off, (size_t)res_len[j->index]});
+            j->applied = true;
+            continue;
+        }
+        nx_snappy_frame_decoder* d = j->dec;
+        j->applied = true;
+        if (d->corrupted) continue;  // an earlier job of this decoder failed: Java skips later input (:86-89)
+        const DecJob& J = bt->djob[j->index];
+        uint32_t a = J.a0;
+        bool failed = false;
+        for (const SnappyAction& act : j->acts) {
+            if (act.kind != SAct::Uncomp && act.kind != SAct::Comp) {
+                if (act.kind == SAct::Stream) d->started = true;
+                continue;
+            }
+            const DecRes& R = dres[a];
+            const DecAct& A = bt->dact[a];
+            ++a;
+            if (R.status != NX_OK) {
+                j->status = R.status;
+                if (R.status == NX_ERR_SNAPPY_CRC_MISMATCH) {
+                    snprintf(buf, sizeof buf, "mismatching checksum: %x (expected: %x)", R.crc, A.crc);
+                    j->err = buf;
+                } else {
+                    j->err = nx_status_string(R.status);
+                }
+                failed = true;
+                break;
+            }
+            j->msgs.push_back({bt->out.h + R.off, (size_t)R.len});
+            if (A.kind == 2 && J.validate && R.cons < A.len) {  // validating-mode leftover (:206-212): see header
+                j->status = NX_ERR_FRAME_CORRUPT;
+                j->err = "asynchronous validating decode: compressed chunk shorter than its length (use the synchronous decoder)";
+                failed = true;
+                break;
+            }
+        }
+        if (!failed && j->has_parse_err) {
+            j->status = NX_ERR_FRAME_CORRUPT;
+            j->err = j->parse_err;
+            failed = true;
+        }
+        if (failed) d->corrupted = true;  // (:227-230)
+    }
+    bt->done = true;
+}
+
+bool poll_batch(Batch* bt, bool block) {
+    if (bt->done) return true;
+    if (!bt->inflight) return false;
+    const hipError_t e = block ? hipEventSynchronize(bt->ev) : hipEventQuery(bt->ev);
+    if (e == hipErrorNotReady) return false;
+    if (e != hipSuccess) return false;
+    apply(bt);
+    bt->inflight = false;
+    return true;
+}
+
+}  // namespace
+
+// ======================================================================= C-ABI
+extern "C" nx_batcher* nx_batcher_new(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return nullptr;
+    if (nx::crc_tables_init() != NX_OK) return nullptr;
+    auto* b = new nx_batcher();
+    if (hipStreamCreateWithFlags(&b->s, hipStreamNonBlocking) != hipSuccess) {
+        delete b;
+        return nullptr;
+    }
+    return b;
+}
+
+extern "C" void nx_batcher_free(nx_batcher* b) {
+    if (!b) return;
+    (void)hipStreamSynchronize(b->s);
+    for (Batch* x : b->all) delete x;
+    (void)hipStreamDestroy(b->s);
+    delete b;
+}
+
+extern "C" int32_t nx_host_register(void* p, size_t n) {
+    if (!p || !n) return NX_ERR_INVALID_ARG;
+    return hipHostRegister(p, n, hipHostRegisterPortable | hipHostRegisterMapped) == hipSuccess ? NX_OK : NX_ERR_HIP;
+}
+
+extern "C" int32_t nx_host_unregister(void* p) {
+    if (!p) return NX_ERR_INVALID_ARG;
+    return hipHostUnregister(p) == hipSuccess ? NX_OK : NX_ERR_HIP;
+}
+
+extern "C" int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx_batcher* b, const uint8_t* in, size_t n,
+                                                  int32_t in_registered) {
+    if (!e || !b || (!in && n)) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    Batch* bt = collecting(b);
+    if (!bt) return NX_ERR_HIP;
+    Job* j = new Job();
+    j->ticket = b->next_ticket++;
+    j->kind = 0;
+    EncJob E{};
+    E.s0 = (uint32_t)bt->esl.size();
+    if (!bt->reserve_out(nx_snappy_frame_max_encoded_length(n), &E.out_off)) {
+        delete j;
+        return NX_ERR_HIP;
+    }
+    if (n) {  // SnappyFrameEncoder.encode (:79-117): !in.isReadable() writes nothing
+        E.stream_start = e->started ? 0u : 1u;
+        e->started = true;
+        uint64_t base = 0;
+        if (in_registered) {
+            base = (bt->st_used + 15) & ~15ull;  // DMA'd into the device arena at flush
+            bt->st_used = base + n;
+            bt->direct.push_back({in, n, base});
+        } else {
+            uint8_t* st = bt->stage(n, &base);
+            if (!st) {
+                delete j;
+                return NX_ERR_HIP;
+            }
+            memcpy(st, in, n);
+        }
+        auto add = [&](uint64_t off, uint32_t len, bool comp) {
+            EncSlice S{base + off, bt->eslots, len, comp ? 1u : 0u};
+            bt->eslots += (nx_snappy_max_compressed_length(len) + 15) & ~(size_t)15;
+            bt->esl.push_back(S);
+        };
+        int64_t dl = (int64_t)n;
+        if (dl > 18) {  // MIN_COMPRESSIBLE_LENGTH (:46,90-113)
+            uint64_t pos = 0;
+            for (;;) {
+                if (dl < 18) {
+                    add(pos, (uint32_t)dl, false);
+                    break;
+                }
+                const uint32_t len = dl > e->slice ? (uint32_t)e->slice : (uint32_t)dl;
+                add(pos, len, true);
+                pos += len;
+                if (dl > e->slice) dl -= e->slice;
+                else break;
+            }
+        } else {
+            add(0, (uint32_t)n, false);
+        }
+    }
+    E.ns = (uint32_t)bt->esl.size() - E.s0;
+    j->index = (uint32_t)bt->ejob.size();
+    bt->ejob.push_back(E);
+    bt->jobs.push_back(j);
+    bt->live += 1;
+    b->tickets[j->ticket] = {bt, j};
+    return (int64_t)j->ticket;
+}
+
+extern "C" int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
+                                                  size_t* consumed) {
+    if (!d || !b || (!in && n) || !consumed) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    Batch* bt = collecting(b);
+    if (!bt) return NX_ERR_HIP;
+    Job* j = new Job();
+    j->ticket = b->next_ticket++;
+    j->kind = 1;
+    j->dec = d;
+    size_t p = 0;
+    if (d->corrupted) {  // (:86-89)
+        p = n;
+    } else {
+        // the chunk-header walk runs now, so the decoder's started/skip state advances in call order
+        bool started = d->started;
+        uint64_t skip = d->skip;
+        while (p < n && nx::fr::snappy_parse_one(in, n, p, started, skip, d->validate, j->acts)) {
+        }
+        if (!j->acts.empty() && j->acts.back().kind == SAct::Error) {
+            j->has_parse_err = true;
+            j->parse_err = j->acts.back().err;
+            p = j->acts.back().end;
+            j->acts.pop_back();
+        }
+        d->started = started;
+        d->skip = skip;
+        if (j->has_parse_err) d->corrupted = true;  // later submits skip their input (:227-230)
+    }
+    *consumed = p;
+    DecJob J{};
+    J.a0 = (uint32_t)bt->dact.size();
+    J.validate = d->validate ? 1u : 0u;
+    size_t out_need = 0;
+    for (const SnappyAction& a : j->acts) {
+        if (a.kind != SAct::Uncomp && a.kind != SAct::Comp) continue;
+        uint64_t off = 0;
+        uint8_t* st = bt->stage(a.dlen, &off);
+        if (!st) {
+            delete j;
+            return NX_ERR_HIP;
+        }
+        memcpy(st, in + a.data, a.dlen);
+        DecAct A{off, a.dlen, 0, 0, a.crc};
+        if (a.kind == SAct::Comp) {
+            A.kind = 2;
+            A.chunk = (uint32_t)bt->dc_off.size();
+            bt->dc_off.push_back(off);
+            bt->dc_len.push_back(a.dlen);
+            bt->dc_crc.push_back(a.crc);
+            if (d->validate) bt->dc_validate = true;
+            out_need += 65536;
+        } else {
+            A.kind = 1;
+            A.chunk = (uint32_t)bt->du_off.size();
+            bt->du_off.push_back(off);
+            bt->du_len.push_back(a.dlen);
+            out_need += a.dlen;
+        }
+        bt->dact.push_back(A);
+    }
+    J.na = (uint32_t)bt->dact.size() - J.a0;
+    if (!bt->reserve_out(out_need + 16, &J.out_off)) {
+        delete j;
+        return NX_ERR_HIP;
+    }
+    j->index = (uint32_t)bt->djob.size();
+    bt->djob.push_back(J);
+    bt->jobs.push_back(j);
+    bt->live += 1;
+    b->tickets[j->ticket] = {bt, j};
+    return (int64_t)j->ticket;
+}
+
+extern "C" int32_t nx_batcher_flush(nx_batcher* b) {
+    if (!b) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    Batch* bt = b->cur;
+    if (!bt || bt->jobs.empty()) return NX_OK;
+    b->cur = nullptr;
+    return launch(b, bt);
+}
+
+extern "C" int32_t nx_batcher_poll(nx_batcher* b, int64_t ticket) {
+    if (!b) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    auto it = b->tickets.find((uint64_t)ticket);
+    if (it == b->tickets.end()) return NX_ERR_INVALID_ARG;
+    return poll_batch(it->second.first, false) ? 1 : 0;
+}
+
+extern "C" int32_t nx_batcher_wait(nx_batcher* b, int64_t ticket) {
+    if (!b) return NX_ERR_INVALID_ARG;
+    Batch* bt;
+    {
+        std::lock_guard<std::mutex> lk(b->mu);
+        auto it = b->tickets.find((uint64_t)ticket);
+        if (it == b->tickets.end()) return NX_ERR_INVALID_ARG;
+        bt = it->second.first;
+        if (bt == b->cur) {  // not flushed yet: flush now
+            b->cur = nullptr;
+            const int32_t r = launch(b, bt);
+            if (r != NX_OK) return r;
+        }
+    }
+    if (hipEventSynchronize(bt->ev) != hipSuccess) return NX_ERR_HIP;
+    std::lock_guard<std::mutex> lk(b->mu);
+    return poll_batch(bt, true) ? NX_OK : NX_ERR_HIP;
+}
+
+extern "C" int32_t nx_batcher_result(nx_batcher* b, int64_t ticket, const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {
+    if (!b || !msgs || !n_msgs) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    auto it = b->tickets.find((uint64_t)ticket);
+    if (it == b->tickets.end()) return NX_ERR_INVALID_ARG;
+    Job* j = it->second.second;
+    if (!j->applied) return NX_ERR_INVALID_ARG;  // poll() / wait() first
+    *msgs = j->msgs.data();
+    *n_msgs = j->msgs.size();
+    if (err_msg) *err_msg = j->err.empty() ? nullptr : j->err.c_str();
+    return j->status;
+}
+
+extern "C" int32_t nx_batcher_release(nx_batcher* b, int64_t ticket) {
+    if (!b) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    auto it = b->tickets.find((uint64_t)ticket);
+    if (it == b->tickets.end()) return NX_ERR_INVALID_ARG;
+    Batch* bt = it->second.first;
+    b->tickets.erase(it);
+    if (bt->live) bt->live -= 1;
+    return NX_OK;
+}
+
+extern "C" int32_t nx_batcher_stats(nx_batcher* b, uint64_t* flushes, uint64_t* launches, uint64_t* chunks) {
+    if (!b) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (flushes) *flushes = b->flushes;
+    if (launches) *launches = b->launches;
+    if (chunks) *chunks = b->chunks;
+    return NX_OK;
+}

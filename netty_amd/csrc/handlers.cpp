@@ -19,52 +19,18 @@
 #include <vector>
 #include "../../include/netty_amd.h"
 #include "nx_common.hpp"
+#include "frame_parse.hpp"
+#include "handles.hpp"
 
 extern "C" int32_t nx_snappy_decode_batch(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*, const uint64_t*,
                                           const uint32_t*, uint32_t*, uint32_t*, int32_t*, const uint32_t*, uint32_t*, uint32_t,
                                           void*);
 
 namespace {
-
-// ------------------------------------------------------------------ device context
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    bool ensure(size_t n) {
-        if (n <= cap) return true;
-        size_t c = cap ? cap : 4096;
-        while (c < n) c += c / 2 + 4096;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        if (hipMalloc(&p, c) != hipSuccess) return false;
-        cap = c;
-        return true;
-    }
-    template <class T>
-    T* as() const { return static_cast<T*>(p); }
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-};
-
-struct Gpu {
-    hipStream_t s = nullptr;
-    bool ok = false;
-    DevBuf din, dout, a0, a1, a2, a3, a4, a5, a6;
-    Gpu() {
-        int n = 0;
-        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return;
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
-        ok = nx::crc_tables_init() == NX_OK;
-    }
-    ~Gpu() {
-        if (s) (void)hipStreamDestroy(s);
-    }
-    bool h2d(void* d, const void* h, size_t n) { return n == 0 || hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s) == hipSuccess; }
-    bool d2h(void* h, const void* d, size_t n) { return n == 0 || hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s) == hipSuccess; }
-    bool sync() { return hipStreamSynchronize(s) == hipSuccess; }
-};
+using nx::h::DevBuf;
+using nx::h::Gpu;
+using nx::h::MsgList;
+using nx::h::kStreamStart;
 
 inline uint32_t le24(const uint8_t* p) { return p[0] | (p[1] << 8) | ((uint32_t)p[2] << 16); }
 inline uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
@@ -72,27 +38,9 @@ inline uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
 inline uint32_t be24(const uint8_t* p) { return ((uint32_t)p[0] << 16) | ((uint32_t)p[1] << 8) | p[2]; }
 inline uint32_t be32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
 
-struct MsgList {
-    std::vector<nx_msg> msgs;
-    std::vector<std::vector<uint8_t>> owned;  // decoded payloads (stable storage)
-    std::string err;
-    void clear() {
-        msgs.clear();
-        owned.clear();
-        err.clear();
-    }
-};
-
-const uint8_t kStreamStart[10] = {0xff, 0x06, 0x00, 0x00, 0x73, 0x4e, 0x61, 0x50, 0x70, 0x59};
-
 }  // namespace
 
 // ======================================================================= Snappy frame encoder
-struct nx_snappy_frame_encoder {
-    Gpu g;
-    bool started = false;
-    int32_t slice;
-};
 
 extern "C" nx_snappy_frame_encoder* nx_snappy_frame_encoder_new(int32_t jumbo) {
     auto* e = new nx_snappy_frame_encoder();
@@ -196,14 +144,6 @@ extern "C" int64_t nx_snappy_frame_encoder_encode(nx_snappy_frame_encoder* e, co
 }
 
 // ======================================================================= Snappy frame decoder
-struct nx_snappy_frame_decoder {
-    Gpu g;
-    bool validate;
-    bool started = false;
-    bool corrupted = false;
-    uint64_t skip = 0;  // numBytesToSkip
-    MsgList ml;
-};
 
 extern "C" nx_snappy_frame_decoder* nx_snappy_frame_decoder_new(int32_t validate) {
     auto* d = new nx_snappy_frame_decoder();
@@ -216,166 +156,9 @@ extern "C" nx_snappy_frame_decoder* nx_snappy_frame_decoder_new(int32_t validate
 }
 extern "C" void nx_snappy_frame_decoder_free(nx_snappy_frame_decoder* d) { delete d; }
 
-namespace {
-// AbstractByteBuf.checkReadableBytes0's IndexOutOfBoundsException (AbstractByteBuf.java:1465-1471), as
-// ByteToMessageDecoder's DecoderException(cause) reports it; the buffer's toString() is omitted.
-const char* bytebuf_oob(char* buf, size_t cap, size_t reader, int len, size_t writer) {
-    snprintf(buf, cap, "java.lang.IndexOutOfBoundsException: readerIndex(%zu) + length(%d) exceeds writerIndex(%zu)", reader, len,
-             writer);
-    return buf;
-}
-enum class SAct { Stream, Skip, Uncomp, Comp, Error };
-struct SnappyAction {
-    SAct kind;
-    size_t data = 0;     // payload position (after the 4-byte masked checksum)
-    uint32_t dlen = 0;   // payload bytes
-    uint32_t crc = 0;    // stored masked checksum
-    size_t end = 0;      // reader index after this action
-    uint64_t skip = 0;   // numBytesToSkip after this action
-    int job = -1;        // GPU job index
-    std::string err;     // Error action: the reference exception message
-};
-
-// One SnappyFrameDecoder.decode() call over in[p..n) (SnappyFrameDecoder.java:85-231), with the
-// chunk work deferred.  Returns false when decode() would return without consuming (need more).
-bool snappy_parse_one(const uint8_t* in, size_t n, size_t& p, bool& started, uint64_t& skip, bool validate,
-                      std::vector<SnappyAction>& acts) {
-    if (skip) {  // :91-99
-        uint64_t s = skip < (uint64_t)(n - p) ? skip : (uint64_t)(n - p);
-        p += s;
-        skip -= s;
-        SnappyAction a{SAct::Skip};
-        a.end = p;
-        a.skip = skip;
-        acts.push_back(a);
-        return s > 0;
-    }
-    const size_t inSize = n - p;
-    if (inSize < 4) return false;
-    const uint8_t type = in[p];
-    const uint32_t chunkLength = le24(in + p + 1);
-    SnappyAction a{SAct::Error};
-    a.end = p;
-    a.skip = skip;
-    char buf[160];
-    auto fail = [&](const char* msg) {
-        a.kind = SAct::Error;
-        a.err = msg;
-        acts.push_back(a);
-        return false;
-    };
-    if (type == 0xff) {  // STREAM_IDENTIFIER (:115-136)
-        if (chunkLength != 6) {
-            snprintf(buf, sizeof buf, "Unexpected length of stream identifier: %u", chunkLength);
-            return fail(buf);
-        }
-        if (inSize < 10) return false;
-        a.end = p + 10;
-        if (memcmp(in + p + 4, "sNaPpY", 6) != 0) return fail("Unexpected stream identifier contents. Mismatched snappy protocol version?");
-        started = true;
-        p += 10;
-        a.kind = SAct::Stream;
-        acts.push_back(a);
-        return true;
-    }
-    if (type == 0) {  // COMPRESSED_DATA (:180-224)
-        if (!started) return fail("Received COMPRESSED_DATA tag before STREAM_IDENTIFIER");
-        if (inSize < 4 + (size_t)chunkLength) return false;
-        if (chunkLength < 4) {
-            // No DecompressionException in the reference: skipBytes(4) then readIntLE() run past the
-            // chunk (:194-195), and the negative slice fails in ByteBuf (:208 / :215), wrapped as a
-            // DecoderException (ByteToMessageDecoder.java:297-300).  The preamble check comes first.
-            if (inSize < 8) return fail(bytebuf_oob(buf, sizeof buf, p + 4, 4, n));
-            uint32_t pre = 0;
-            int bi = 0;
-            bool done = false;
-            for (size_t q = p + 8; q < n; ++q) {
-                pre |= (uint32_t)(in[q] & 0x7f) << (bi++ * 7);
-                if (!(in[q] & 0x80)) {
-                    done = true;
-                    break;
-                }
-                if (bi >= 4) return fail("Preamble is greater than 4 bytes");
-            }
-            if (done && pre > 65536) return fail("Received COMPRESSED_DATA that contains uncompressed data that exceeds 65536 bytes");
-            if (validate) {  // in.writerIndex(readerIndex + chunkLength - 4) below the reader index (:208)
-                snprintf(buf, sizeof buf,
-                         "java.lang.IndexOutOfBoundsException: readerIndex: %zu, writerIndex: %zu "
-                         "(expected: 0 <= readerIndex <= writerIndex <= capacity)", p + 8, p + 4 + (size_t)chunkLength);
-                return fail(buf);
-            }
-            snprintf(buf, sizeof buf, "java.lang.IllegalArgumentException: minimumReadableBytes : %d (expected: >= 0)",
-                     (int)chunkLength - 4);  // in.readSlice(chunkLength - 4) (:215)
-            return fail(buf);
-        }
-        a.crc = le32(in + p + 4);
-        // snappy.getPreamble(in): the varint is read from the cumulation (Snappy.java:404-441)
-        uint32_t ulen = 0;
-        int bi = 0;
-        bool complete = false;
-        for (size_t q = p + 8; q < n; ++q) {
-            const uint32_t cur = in[q];
-            ulen |= (cur & 0x7f) << (bi++ * 7);
-            if ((cur & 0x80) == 0) {
-                complete = true;
-                break;
-            }
-            if (bi >= 4) return fail("Preamble is greater than 4 bytes");
-        }
-        if (!complete) ulen = 0;
-        if (ulen > 65536) return fail("Received COMPRESSED_DATA that contains uncompressed data that exceeds 65536 bytes");
-        a.kind = SAct::Comp;
-        a.data = p + 8;
-        a.dlen = chunkLength - 4;
-        p += 4 + chunkLength;
-        a.end = p;
-        acts.push_back(a);
-        return true;
-    }
-    if (type == 1) {  // UNCOMPRESSED_DATA (:158-179)
-        if (!started) return fail("Received UNCOMPRESSED_DATA tag before STREAM_IDENTIFIER");
-        if (chunkLength > 65536 + 4) return fail("Received UNCOMPRESSED_DATA larger than 65540 bytes");
-        if (inSize < 4 + (size_t)chunkLength) return false;
-        if (chunkLength < 4) {
-            // (:171-178) readIntLE / skipBytes(4) run past the chunk; with validation the CRC32C of a
-            // negative length is the empty CRC (Crc32c.update's loop does not run, mask(0) =
-            // 0xa282ead8, DecompressionException unless the 4 bytes read happen to equal it); then
-            // readRetainedSlice(chunkLength - 4) fails in ByteBuf.  Heap-buffer behaviour.
-            if (inSize < 8) return fail(bytebuf_oob(buf, sizeof buf, p + 4, 4, n));
-            const uint32_t ck = le32(in + p + 4);
-            if (validate && ck != 0xa282ead8u) {
-                snprintf(buf, sizeof buf, "mismatching checksum: a282ead8 (expected: %x)", ck);
-                return fail(buf);
-            }
-            snprintf(buf, sizeof buf, "java.lang.IllegalArgumentException: minimumReadableBytes : %d (expected: >= 0)",
-                     (int)chunkLength - 4);
-            return fail(buf);
-        }
-        a.kind = SAct::Uncomp;
-        a.crc = le32(in + p + 4);
-        a.data = p + 8;
-        a.dlen = chunkLength - 4;
-        p += 4 + chunkLength;
-        a.end = p;
-        acts.push_back(a);
-        return true;
-    }
-    if (type & 0x80) {  // RESERVED_SKIPPABLE (:137-150)
-        if (!started) return fail("Received RESERVED_SKIPPABLE tag before STREAM_IDENTIFIER");
-        p += 4;
-        const uint64_t s = chunkLength < (uint64_t)(n - p) ? chunkLength : (uint64_t)(n - p);
-        p += s;
-        if (s != chunkLength) skip = chunkLength - s;
-        a.kind = SAct::Skip;
-        a.end = p;
-        a.skip = skip;
-        acts.push_back(a);
-        return true;
-    }
-    snprintf(buf, sizeof buf, "Found reserved unskippable chunk type: 0x%x", (unsigned)type);  // :151-157
-    return fail(buf);
-}
-}  // namespace
+using nx::fr::SAct;
+using nx::fr::SnappyAction;
+using nx::fr::snappy_parse_one;
 
 extern "C" int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
                                                   const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {

@@ -1,0 +1,83 @@
+// handles.hpp — device context and the Snappy handler handles shared by the synchronous handler layer
+// (handlers.cpp) and the asynchronous cross-channel batcher (batcher.cpp).  Private to the library.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+#include "../../include/netty_amd.h"
+#include "nx_common.hpp"
+
+namespace nx {
+namespace h {
+
+// ------------------------------------------------------------------ device context
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool ensure(size_t n) {
+        if (n <= cap) return true;
+        size_t c = cap ? cap : 4096;
+        while (c < n) c += c / 2 + 4096;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, c) != hipSuccess) return false;
+        cap = c;
+        return true;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct Gpu {
+    hipStream_t s = nullptr;
+    bool ok = false;
+    DevBuf din, dout, a0, a1, a2, a3, a4, a5, a6;
+    Gpu() {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
+        ok = nx::crc_tables_init() == NX_OK;
+    }
+    ~Gpu() {
+        if (s) (void)hipStreamDestroy(s);
+    }
+    bool h2d(void* d, const void* h, size_t n) { return n == 0 || hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s) == hipSuccess; }
+    bool d2h(void* h, const void* d, size_t n) { return n == 0 || hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s) == hipSuccess; }
+    bool sync() { return hipStreamSynchronize(s) == hipSuccess; }
+};
+
+struct MsgList {
+    std::vector<nx_msg> msgs;
+    std::vector<std::vector<uint8_t>> owned;  // decoded payloads (stable storage)
+    std::string err;
+    void clear() {
+        msgs.clear();
+        owned.clear();
+        err.clear();
+    }
+};
+
+inline constexpr uint8_t kStreamStart[10] = {0xff, 0x06, 0x00, 0x00, 0x73, 0x4e, 0x61, 0x50, 0x70, 0x59};
+
+}  // namespace h
+}  // namespace nx
+
+struct nx_snappy_frame_encoder {
+    nx::h::Gpu g;
+    bool started = false;
+    int32_t slice;
+};
+
+struct nx_snappy_frame_decoder {
+    nx::h::Gpu g;
+    bool validate;
+    bool started = false;
+    bool corrupted = false;
+    uint64_t skip = 0;  // numBytesToSkip
+    nx::h::MsgList ml;
+};

@@ -304,3 +304,96 @@ class EmbeddedChannel:
 
     def finish(self) -> bool:
         return bool(self._outbound or self._inbound)
+
+
+class Batcher:
+    """Asynchronous cross-channel batching executor (include/netty_amd.h section 3, csrc/batcher.cpp):
+    encode()/decode() calls of many SnappyFrameEncoder / SnappyFrameDecoder instances become jobs of
+    one GPU launch per flush().  submit_* never touches the GPU; poll() never blocks."""
+
+    def __init__(self):
+        self._h = _new(_lib.load().nx_batcher_new(), "Batcher")
+
+    def close(self):
+        if self._h:
+            _lib.load().nx_batcher_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def submit_encode(self, encoder: "SnappyFrameEncoder", data, registered_ptr: int | None = None) -> int:
+        """SnappyFrameEncoder.encode as a job.  With registered_ptr (an address inside memory passed to
+        register()), the bytes are DMA'd from there at flush and must stay valid until completion."""
+        L = _lib.load()
+        if registered_ptr is not None:
+            t = L.nx_snappy_frame_encoder_submit(encoder._h, self._h, C.c_void_p(registered_ptr), len(data), 1)
+        else:
+            buf = bytes(data)
+            t = L.nx_snappy_frame_encoder_submit(encoder._h, self._h, buf, len(buf), 0)
+        if t < 0:
+            raise RuntimeError(f"nx_snappy_frame_encoder_submit: {_lib.status_string(t)}")
+        return t
+
+    def submit_decode(self, decoder: "SnappyFrameDecoder", data) -> int:
+        """SnappyFrameDecoder.decode over the decoder's cumulation + data as a job; the consumed bytes
+        leave the cumulation now (ByteToMessageDecoder.channelRead)."""
+        L = _lib.load()
+        decoder._cum += bytes(data)
+        buf = bytes(decoder._cum)
+        consumed = C.c_size_t(0)
+        t = L.nx_snappy_frame_decoder_submit(decoder._h, self._h, buf, len(buf), C.byref(consumed))
+        if t < 0:
+            raise RuntimeError(f"nx_snappy_frame_decoder_submit: {_lib.status_string(t)}")
+        del decoder._cum[:consumed.value]
+        return t
+
+    def flush(self):
+        r = _lib.load().nx_batcher_flush(self._h)
+        if r != 0:
+            raise RuntimeError(f"nx_batcher_flush: {_lib.status_string(r)}")
+
+    def poll(self, ticket: int) -> bool:
+        r = _lib.load().nx_batcher_poll(self._h, ticket)
+        if r < 0:
+            raise RuntimeError(f"nx_batcher_poll: {_lib.status_string(r)}")
+        return r == 1
+
+    def wait(self, ticket: int):
+        r = _lib.load().nx_batcher_wait(self._h, ticket)
+        if r != 0:
+            raise RuntimeError(f"nx_batcher_wait: {_lib.status_string(r)}")
+
+    def result(self, ticket: int, release: bool = True):
+        """The job's messages (list of bytes); a failed decoder job raises like decode() would, with
+        the messages decoded before the failure attached as .decoded."""
+        L = _lib.load()
+        msgs = C.POINTER(_lib.NxMsg)()
+        n = C.c_size_t(0)
+        err = C.c_char_p()
+        rc = L.nx_batcher_result(self._h, ticket, C.byref(msgs), C.byref(n), C.byref(err))
+        out = [C.string_at(msgs[i].data, msgs[i].len) if msgs[i].len else b"" for i in range(n.value)]
+        if release:
+            L.nx_batcher_release(self._h, ticket)
+        if rc != 0:
+            if rc in (-100, -101, -102, -103):
+                raise RuntimeError(f"Batcher: native failure {rc} ({_lib.status_string(rc)})")
+            msg = err.value.decode() if err.value else _lib.status_string(rc)
+            e = DecoderException(msg) if msg.startswith("java.lang.") else DecompressionException(msg)
+            e.decoded = out
+            raise e
+        return out
+
+    def stats(self) -> dict:
+        f, l_, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        _lib.load().nx_batcher_stats(self._h, C.byref(f), C.byref(l_), C.byref(c))
+        return {"flushes": f.value, "launches": l_.value, "chunks": c.value}
+
+    @staticmethod
+    def register(ptr: int, n: int):
+        r = _lib.load().nx_host_register(C.c_void_p(ptr), n)
+        if r != 0:
+            raise RuntimeError(f"nx_host_register: {_lib.status_string(r)}")
+
+    @staticmethod
+    def unregister(ptr: int):
+        _lib.load().nx_host_unregister(C.c_void_p(ptr))
