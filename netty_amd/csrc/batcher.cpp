@@ -28,6 +28,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -85,6 +86,26 @@ __device__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__
         *reinterpret_cast<v4*>(dst + head + 16u * i) = *reinterpret_cast<const v4u*>(src + head + 16u * i);
     const uint32_t t = head + (nv << 4);
     if (t + (uint32_t)lane < n) dst[t + lane] = src[t + lane];
+}
+
+// Registered host inputs -> the device input arena: one wave per input range, 16-byte loads from the
+// mapped host pages (one launch instead of one DMA command per pooled-buffer message).
+struct GatherOp {
+    const uint8_t* src;  // device address of registered host memory
+    uint64_t dst;        // offset in the device input arena
+    uint64_t len;
+};
+__global__ void __launch_bounds__(256) k_gather_host(const GatherOp* __restrict__ ops, uint32_t n, uint8_t* __restrict__ din) {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    typedef v4 __attribute__((aligned(1))) v4u;
+    const int lane = threadIdx.x & 63;
+    const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= n) return;
+    const GatherOp g = ops[k];
+    uint8_t* d = din + g.dst;  // 16-byte aligned
+    const uint64_t nv = g.len >> 4;
+    for (uint64_t i = lane; i < nv; i += 64) *reinterpret_cast<v4*>(d + 16 * i) = *reinterpret_cast<const v4u*>(g.src + 16 * i);
+    for (uint64_t i = (nv << 4) + lane; i < g.len; i += 64) d[i] = g.src[i];
 }
 
 // one wave per encoder job: [stream identifier] then [type][len+4: u24 LE][masked crc LE][payload] per slice
@@ -176,7 +197,9 @@ struct Pinned {  // hipHostMalloc'd, mapped into the device address space; grows
         size_t c = cap ? cap : (1u << 20);
         while (c < n) c *= 2;
         uint8_t *nh = nullptr, *nd = nullptr;
-        if (hipHostMalloc((void**)&nh, c, hipHostMallocMapped) != hipSuccess) return false;
+        // coarse-grained (host-cached) pinned memory: the GPU's writes are visible once the batch's
+        // event completes, and host reads of the results run at cache speed
+        if (hipHostMalloc((void**)&nh, c, hipHostMallocMapped | hipHostMallocNonCoherent) != hipSuccess) return false;
         if (hipHostGetDevicePointer((void**)&nd, nh, 0) != hipSuccess) {
             (void)hipHostFree(nh);
             return false;
@@ -211,12 +234,15 @@ struct Batch {
     Pinned staging;  // chunk payloads, then the device arrays (one H2D copy at flush)
     size_t st_used = 0;
     struct Direct {
-        const uint8_t* src;
+        const uint8_t* src;  // host address (adjacency test)
+        const uint8_t* dsrc; // its device address (mapped registration)
         size_t len;
         uint64_t din_off;
     };
-    std::vector<Direct> direct;  // registered encoder inputs, DMA'd at flush
+    std::vector<Direct> direct;  // registered encoder inputs, DMA'd at flush (din_off in the direct region)
+    uint64_t direct_used = 0;
     std::vector<EncSlice> esl;
+    std::vector<uint8_t> esl_direct;  // slice input lies in the direct region
     std::vector<EncJob> ejob;
     uint64_t eslots = 0;
     std::vector<DecAct> dact;
@@ -229,14 +255,16 @@ struct Batch {
     Pinned out;  // mapped result arena: job outputs, then the result records
     uint64_t out_used = 0, res_enc = 0, res_dec = 0;
     std::vector<Job*> jobs;
-    nx::h::DevBuf din, slots;
+    nx::h::DevBuf din, slots, gops;
     hipEvent_t ev = nullptr;
     bool inflight = false, done = false;
     size_t live = 0;  // jobs not yet released
     void reset() {
         st_used = 0;
         direct.clear();
+        direct_used = 0;
         esl.clear();
+        esl_direct.clear();
         ejob.clear();
         eslots = 0;
         dact.clear();
@@ -273,6 +301,21 @@ struct Batch {
     }
 };
 
+}  // namespace
+
+namespace {
+// nx_host_register'd ranges: host base -> (length, device address of the mapping)
+std::mutex g_reg_mu;
+std::map<uintptr_t, std::pair<size_t, uint8_t*>> g_reg;
+const uint8_t* registered_device_ptr(const uint8_t* p, size_t n) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.upper_bound((uintptr_t)p);
+    if (it == g_reg.begin()) return nullptr;
+    --it;
+    const uintptr_t off = (uintptr_t)p - it->first;
+    if (off + n > it->second.first) return nullptr;
+    return it->second.second + off;
+}
 }  // namespace
 
 struct nx_batcher {
@@ -333,6 +376,10 @@ int32_t launch(nx_batcher* b, Batch* bt) {
     uint64_t st_arr = 0;
     uint8_t* h = bt->stage(Lh.at + 16, &st_arr);
     if (!h) return NX_ERR_HIP;
+    // device input arena: [staging bytes][direct region]
+    const uint64_t d0 = (bt->st_used + 15) & ~15ull;
+    for (uint32_t i = 0; i < nes; ++i)
+        if (bt->esl_direct[i]) bt->esl[i].in_off += d0;
     std::vector<uint64_t> ein(nes), eslot(nes), dslot(ndc);
     std::vector<uint32_t> elen(nes);
     for (uint32_t i = 0; i < nes; ++i) {
@@ -359,15 +406,24 @@ int32_t launch(nx_batcher* b, Batch* bt) {
     cp(o_dulen, bt->du_len.data(), 4ull * ndu);
     // result records in the mapped arena, after the job outputs
     if (!bt->reserve_out(8ull * nej + 8, &bt->res_enc) || !bt->reserve_out(sizeof(DecRes) * nda + 8, &bt->res_dec)) return NX_ERR_HIP;
-    if (!bt->din.ensure(bt->st_used + 16) || !bt->slots.ensure(bt->eslots + (uint64_t)ndc * 65536u + Ld.at + 64)) return NX_ERR_HIP;
+    if (!bt->din.ensure(d0 + bt->direct_used + 16) || !bt->slots.ensure(bt->eslots + (uint64_t)ndc * 65536u + Ld.at + 64)) return NX_ERR_HIP;
     uint8_t* din = bt->din.as<uint8_t>();
     uint8_t* slots = bt->slots.as<uint8_t>();
     uint8_t* dslots = slots + bt->eslots;
     uint8_t* D = dslots + (uint64_t)ndc * 65536u;
     D = reinterpret_cast<uint8_t*>(((uintptr_t)D + 15) & ~(uintptr_t)15);
     if (hipMemcpyAsync(din, bt->staging.h, bt->st_used, hipMemcpyHostToDevice, s) != hipSuccess) return NX_ERR_HIP;
-    for (const Batch::Direct& dd : bt->direct)
-        if (hipMemcpyAsync(din + dd.din_off, dd.src, dd.len, hipMemcpyHostToDevice, s) != hipSuccess) return NX_ERR_HIP;
+    if (!bt->direct.empty()) {  // registered inputs: one gather launch reading the mapped host pages
+        const uint32_t ng = (uint32_t)bt->direct.size();
+        std::vector<nx::bt::GatherOp> ops(ng);
+        for (uint32_t k = 0; k < ng; ++k) ops[k] = {bt->direct[k].dsrc, d0 + bt->direct[k].din_off, bt->direct[k].len};
+        if (!bt->gops.ensure(sizeof(nx::bt::GatherOp) * ng) ||
+            hipMemcpyAsync(bt->gops.p, ops.data(), sizeof(nx::bt::GatherOp) * ng, hipMemcpyHostToDevice, s) != hipSuccess)
+            return NX_ERR_HIP;
+        hipLaunchKernelGGL(nx::bt::k_gather_host, dim3((ng + 3) / 4), dim3(256), 0, s, bt->gops.as<const nx::bt::GatherOp>(), ng, din);
+        if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
+        b->launches += 1;
+    }
     const uint8_t* A = din + st_arr;
     int32_t r;
     if (nes) {  // CRC32C + Snappy.encode of every encoder slice of every channel
@@ -502,11 +558,23 @@ extern "C" void nx_batcher_free(nx_batcher* b) {
 
 extern "C" int32_t nx_host_register(void* p, size_t n) {
     if (!p || !n) return NX_ERR_INVALID_ARG;
-    return hipHostRegister(p, n, hipHostRegisterPortable | hipHostRegisterMapped) == hipSuccess ? NX_OK : NX_ERR_HIP;
+    if (hipHostRegister(p, n, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) return NX_ERR_HIP;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+        (void)hipHostUnregister(p);
+        return NX_ERR_HIP;
+    }
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[(uintptr_t)p] = {n, (uint8_t*)d};
+    return NX_OK;
 }
 
 extern "C" int32_t nx_host_unregister(void* p) {
     if (!p) return NX_ERR_INVALID_ARG;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        g_reg.erase((uintptr_t)p);
+    }
     return hipHostUnregister(p) == hipSuccess ? NX_OK : NX_ERR_HIP;
 }
 
@@ -529,10 +597,22 @@ extern "C" int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx
         E.stream_start = e->started ? 0u : 1u;
         e->started = true;
         uint64_t base = 0;
-        if (in_registered) {
-            base = (bt->st_used + 15) & ~15ull;  // DMA'd into the device arena at flush
-            bt->st_used = base + n;
-            bt->direct.push_back({in, n, base});
+        const uint8_t* dsrc = in_registered ? registered_device_ptr(in, n) : nullptr;
+        if (in_registered && !dsrc) {
+            delete j;
+            return NX_ERR_INVALID_ARG;  // not inside an nx_host_register'd range
+        }
+        const bool direct = dsrc != nullptr;
+        if (direct) {  // DMA'd into the device arena's direct region at flush; adjacent inputs share one copy
+            Batch::Direct* last = bt->direct.empty() ? nullptr : &bt->direct.back();
+            if (last && last->src + last->len == in && last->din_off + last->len == bt->direct_used) {
+                base = bt->direct_used;
+                last->len += n;
+            } else {
+                base = (bt->direct_used + 15) & ~15ull;
+                bt->direct.push_back({in, dsrc, n, base});
+            }
+            bt->direct_used = base + n;
         } else {
             uint8_t* st = bt->stage(n, &base);
             if (!st) {
@@ -545,6 +625,7 @@ extern "C" int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx
             EncSlice S{base + off, bt->eslots, len, comp ? 1u : 0u};
             bt->eslots += (nx_snappy_max_compressed_length(len) + 15) & ~(size_t)15;
             bt->esl.push_back(S);
+            bt->esl_direct.push_back(direct ? 1 : 0);
         };
         int64_t dl = (int64_t)n;
         if (dl > 18) {  // MIN_COMPRESSIBLE_LENGTH (:46,90-113)
