@@ -54,7 +54,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (H2D/D2H) end-to-end measurement")
-    ap.add_argument("--e2e-chunks", type=int, default=131072, help="chunks through the host pipeline (8 GiB)")
+    ap.add_argument("--e2e-channels", type=int, default=256, help="C-ABI end-to-end: channels (handler pairs)")
+    ap.add_argument("--e2e-messages", type=int, default=256, help="C-ABI end-to-end: 64 KiB messages per channel")
+    ap.add_argument("--e2e-chunks", type=int, default=131072, help="chunks through the torch host pipeline (8 GiB)")
     ap.add_argument("--e2e-sub", type=int, default=65536, help="chunks per pipelined sub-batch")
     ap.add_argument("--no-alt", action="store_true", help="skip the FastLZ/LZF/LZ4 (configs[3]) measurement")
     ap.add_argument("--alt-chunks", type=int, default=262144)
@@ -460,9 +462,11 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
             line["alt_codecs"] = bench_alt_codecs(torch, B, dev, args.alt_chunks)
             torch.cuda.empty_cache()
         if not args.no_e2e:
-            # host-memory path (pinned ByteBuf-like buffers, H2D → kernels → D2H, two streams); never `value`
+            # host memory in, host memory out, through the C-ABI a JNI caller binds (never `value`)
+            line["end_to_end"] = e2e_capi(args.e2e_channels, args.e2e_messages)
+            # the same round trip driven from torch (pinned tensors, two streams): netty_amd/pipeline.py
             from netty_amd import pipeline as P
-            line["end_to_end"] = P.measure(dev, n=args.e2e_chunks, sub=args.e2e_sub)
+            line["end_to_end_torch_pipeline"] = P.measure(dev, n=args.e2e_chunks, sub=args.e2e_sub)
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         line["verified"] = ok
@@ -476,6 +480,28 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
 
 
 # ---------------------------------------------------------------------------------------- extra legs
+def e2e_capi(channels: int, messages: int, timeout: float = 240.0):
+    """Host-to-host Snappy frame round trip through the asynchronous batcher C-ABI
+    (netty_amd/tools/e2e_capi.cpp): `channels` SnappyFrameEncoder/Decoder pairs, `messages` 65535-byte
+    text messages each in registered host memory, one flush per direction.  Run as a child process
+    (its own HIP context); returns its JSON, or the failure."""
+    import subprocess
+    exe = os.path.join(ROOT, "netty_amd", "e2e_capi")
+    if not os.path.exists(exe):
+        return {"error": "netty_amd/e2e_capi not built (make -C netty_amd)"}
+    try:
+        r = subprocess.run([exe, str(channels), str(messages), "65535", "3"], capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout}s"}
+    try:
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+    d["path"] = ("pooled-direct-ByteBuf stand-in (registered host memory) -> nx_snappy_frame_encoder_submit x N -> one flush "
+                 "-> framed bytes in mapped pinned memory -> nx_snappy_frame_decoder_submit x N -> one flush -> messages")
+    return d
+
+
 def bench_frame_scan(torch, B, dev, leg, m: int, per_stream: int, reps: int = 3):
     """§8f row 1: the first sub-batch's encoded chunks laid out as SnappyFrameEncoder streams in HBM
     (stream identifier, then one COMPRESSED_DATA chunk per 64 KiB: type 0, 24-bit length, masked CRC,
