@@ -1,0 +1,1252 @@
+// snappy_decode.hip — Snappy block decoder + fused CRC32C verify (gfx950).
+//
+// Replaces Snappy.decode (Snappy.java:315-650) as SnappyFrameDecoder drives it for one complete
+// COMPRESSED_DATA chunk (SnappyFrameDecoder.java:194-224), fused with Snappy.validateChecksum
+// (Snappy.java:700-707) over the produced bytes.  Bit-exact, including the reference's silent
+// partial output on truncated input and its error precedence (offset 0 / negative / beyond,
+// output overflow, invalid literal length, preamble > 4 bytes).
+//
+// Two kernels per sub-batch of frames:
+//
+//   k_parse  — one LANE per frame runs Snappy.decode's tag state machine (all of Java's checks,
+//              in stream order) without touching output bytes.  It emits one 32-bit RECORD per
+//              output-producing tag (literals longer than 64 bytes are split into 64-byte records):
+//                  bit 31 copy | bits 30..25 length-1 | bits 24..0 input position (literal) or offset (copy)
+//              into a per-frame slot of kRecCap records, and the frame's out_len / consumed /
+//              status.  A tag costs ~30 lane instructions, i.e. half a wave instruction per tag
+//              with 64 frames per wave — the serial part of decoding is paid once per frame, not
+//              once per lane of a cooperating wave.
+//   k_expand — one WAVE per frame executes the records, 64 at a time, with the output history in
+//              LDS and coalesced HBM stores:
+//     pieces — the batch's output is cut into PIECES: the intersection of a record with an aligned
+//              output dword.  A pass gives one piece to each lane; the piece's record comes from a
+//              piece-start bitmask (mbcnt + max-scan), its 1-4 bytes from one unaligned 4-byte read
+//              of the input stage (literal), the ring (copy <= 4 KiB back) or HBM (older output of
+//              this frame, already flushed and drained), and it is written with one ds_mskor.
+//     rounds — a copy whose source bytes are produced in the same pass waits until the pieces
+//              producing them (found through a per-pass byte -> piece map) are done; overlapping
+//              copies (offset < length) replicate their period.
+//     flush  — each completed 512 B block leaves the ring with one 8-byte store per lane; each
+//              lane folds its 8 bytes into a per-lane CRC accumulator (slicing-by-4, then "shift by
+//              512 B"), and the 64 accumulators are combined once per frame (GF(2) shift tree), so
+//              the verify costs neither an HBM pass nor a per-block reduction.
+//
+// Frames whose records do not fit the slot (or whose input is >= 32 MiB) are marked by k_parse and
+// decoded by k_decode_fused, the single-kernel form in which the wave also parses: lane l decodes
+// "a tag at W+l" of a 64-byte window speculatively, pointer doubling finds the real tag chain,
+// and the same piece expansion runs on the window's tags.
+//
+// HBM traffic per frame = compressed bytes read twice (parse, literal stage) + records written and
+// read once (4 B per tag) + output written once (+ far-copy re-reads, mostly served from MALL).
+#include <stddef.h>
+#include <stdlib.h>
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include "nx_common.hpp"
+
+namespace nx {
+namespace dec {
+
+constexpr int kWaves = 12;        // waves per workgroup (2 workgroups per CU → 24 waves/CU)
+constexpr int kRing = 4096;       // decoded-output history per wave
+constexpr int kStage = 1024;      // compressed-input ring per wave
+constexpr int kFB = 512;          // flush block (64 lanes x 8 B)
+constexpr int32_t kGuardTrip = -99;
+constexpr uint32_t kRecCap = 16384;      // records per frame slot (64 KiB)
+constexpr int32_t kNeedFused = -1000;    // internal status: the frame goes to k_decode_fused
+constexpr uint32_t kSubBatch = 262144;   // frames per parse/expand launch pair (16 GiB of record slots)
+
+// CRC tables staged in LDS per workgroup: slicing-by-4 (4 KiB) and shift-by-512 B (4 KiB).  The
+// nibble tables of the once-per-frame fold are read from global memory.
+constexpr int kTabWords = 4 * 256 + 4 * 256;
+constexpr int kTabBytes = kTabWords * 4;
+
+struct WaveLds {
+    uint32_t ring[kRing / 4];    // dword 0 .. 1023
+    uint32_t stage[kStage / 4];  // dword 1024 .. 1279
+    // tag records {start (absolute output position), x (bit31 = copy; low 31 bits = literal source
+    // position or copy offset)}; the start of record r+1 is the end of record r (sentinel after the last)
+    uint32_t tagw[2 * 64 + 2];
+    uint32_t scratch[64];        // parse: tag-start marks; expand: first-piece marks, then byte -> piece map
+    uint32_t pad[2];
+};
+static_assert(sizeof(WaveLds) % 16 == 0, "keep per-wave LDS 16-byte aligned");
+static_assert(2 * (kTabBytes + kWaves * sizeof(WaveLds)) <= 160 * 1024, "two workgroups per CU");
+
+typedef uint32_t __attribute__((aligned(1))) u32u;
+typedef __attribute__((address_space(1))) const uint8_t gu8;
+typedef __attribute__((address_space(1))) const u32u gu32u;
+
+__device__ __forceinline__ uint32_t shift_byte_tab(const uint32_t* __restrict__ S, uint32_t c) {
+    return S[c & 0xFF] ^ S[256 + ((c >> 8) & 0xFF)] ^ S[512 + ((c >> 16) & 0xFF)] ^ S[768 + (c >> 24)];
+}
+
+__device__ __forceinline__ uint32_t shift_nib_tab(const uint32_t* __restrict__ N, uint32_t c) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r ^= N[k * 16 + ((c >> (4 * k)) & 15u)];
+    return r;
+}
+
+// raw CRC (state 0) of 8 bytes (two LE dwords), slicing-by-4 twice
+__device__ __forceinline__ uint32_t raw8(const uint32_t* __restrict__ T, uint32_t w0, uint32_t w1) {
+    uint32_t c = w0;
+    c = T[3 * 256 + (c & 0xFF)] ^ T[2 * 256 + ((c >> 8) & 0xFF)] ^ T[1 * 256 + ((c >> 16) & 0xFF)] ^ T[c >> 24];
+    c ^= w1;
+    c = T[3 * 256 + (c & 0xFF)] ^ T[2 * 256 + ((c >> 8) & 0xFF)] ^ T[1 * 256 + ((c >> 16) & 0xFF)] ^ T[c >> 24];
+    return c;
+}
+
+// Wave-uniform value → SGPR (values loaded by vector memory ops or shuffles are otherwise VGPRs and
+// every branch on them becomes exec-masked divergent code).
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// Cross-lane hand-off through LDS inside one wave: without it the compiler may forward a lane's
+// own earlier store to its later load (single-thread semantics) instead of reading what other
+// lanes wrote.  Same pattern as rocPRIM's wave_barrier().
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint64_t lanemask_le(int lane) { return lane == 63 ? ~0ull : ((2ull << lane) - 1ull); }
+
+// Inclusive prefix sum over the 64 lanes (DPP row shifts + row broadcasts; all lanes active).
+__device__ __forceinline__ uint32_t incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
+// Inclusive max-scan over the 64 lanes (same DPP pattern as incl_scan).
+__device__ __forceinline__ uint32_t incl_max_scan(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t g_ld32u(const uint8_t* p) { return *(gu32u*)(p); }  // unaligned global dword
+__device__ __forceinline__ uint32_t g_ld8(const uint8_t* p) { return *(gu8*)(p); }
+
+struct Frame {
+    const uint8_t* src;
+    uint32_t in_len;
+    uint8_t* dst;
+    uint32_t cap;
+};
+
+// Per-frame state of a decoding wave: the compressed-input stage, the output ring and its flush
+// to HBM with the per-lane CRC accumulators.
+struct FrameIO {
+    WaveLds& L;
+    const uint8_t* __restrict__ src;
+    uint8_t* __restrict__ dst;
+    const uint32_t* __restrict__ sT;
+    const uint32_t* __restrict__ sSH;
+    uint32_t in_len;
+    uint32_t a;        // src & 7: position p of the chunk is stage coordinate p + a
+    uint32_t aend;
+    uint32_t sbase;    // stage holds stage coordinates [sbase, sbase + kStage)
+    uint2 pf;          // register prefetch of the next 512 B stage block
+    uint32_t flushed;  // output bytes stored to HBM
+    uint32_t acc;      // this lane's CRC accumulator over its 8-byte slot of every flushed block
+    bool dst8, do_crc;
+    int lane;
+
+    __device__ __forceinline__ FrameIO(WaveLds& L_, const Frame& f, const uint32_t* T, const uint32_t* SH, bool crc, int ln)
+        : L(L_), src(f.src), dst(f.dst), sT(T), sSH(SH), in_len(uni(f.in_len)), sbase(0), pf(make_uint2(0, 0)), flushed(0),
+          acc(0), do_crc(crc), lane(ln) {
+        a = (uint32_t)((uintptr_t)src & 7u);
+        aend = a + in_len;
+        dst8 = (((uintptr_t)dst) & 7u) == 0;
+    }
+    __device__ __forceinline__ uint2 load8(uint32_t apos) const {
+        return apos < aend ? *reinterpret_cast<const uint2*>(src - a + apos) : make_uint2(0, 0);
+    }
+    __device__ __forceinline__ void put8(uint32_t apos, uint2 v) {
+        *reinterpret_cast<uint2*>(&reinterpret_cast<uint8_t*>(L.stage)[apos & (kStage - 1)]) = v;
+    }
+    __device__ __forceinline__ void prime(uint32_t wa) {
+        sbase = wa & ~511u;
+        put8(sbase + 8u * lane, load8(sbase + 8u * lane));
+        put8(sbase + 512u + 8u * lane, load8(sbase + 512u + 8u * lane));
+        pf = load8(sbase + 1024u + 8u * lane);
+    }
+    // make stage coordinate wa (monotone over calls) the start of the staged range
+    __device__ __forceinline__ void advance(uint32_t wa) {
+        while (wa >= sbase + 512u) {
+            if (wa >= sbase + 1536u) {
+                prime(wa);
+                break;
+            }
+            put8(sbase + 1024u + 8u * lane, pf);
+            sbase += 512u;
+            pf = load8(sbase + 1024u + 8u * lane);
+        }
+    }
+    // flush every complete 512 B block that ends at or below `limit`
+    __device__ __forceinline__ void flush_to(uint32_t limit) {
+        const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);
+        while (flushed + (uint32_t)kFB <= limit) {
+            wave_sync();
+            // Far reads target q + 4 <= flushed - 1024, i.e. blocks at least two flushes older than
+            // the newest; vmcnt counts in issue order, so vmcnt(1) retires every store but (at
+            // most) the newest vector-memory op.
+            asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+            const uint2 d = *reinterpret_cast<const uint2*>(&ring8[(flushed + 8u * lane) & (kRing - 1)]);
+            uint8_t* o = dst + flushed + 8u * lane;
+#ifdef NX_EXP_NOSTORE
+            if (d.x == 0x12345678u && d.y == 0x9abcdef0u) {
+#else
+            if (dst8) {
+#endif
+                *reinterpret_cast<uint2*>(o) = d;
+            } else {
+#ifndef NX_EXP_NOSTORE
+#pragma unroll
+                for (int i = 0; i < 8; ++i) o[i] = (uint8_t)((i < 4 ? d.x : d.y) >> (8 * (i & 3)));
+#endif
+            }
+            if (do_crc) acc = shift_byte_tab(sSH, acc) ^ raw8(sT, d.x, d.y);
+            flushed += (uint32_t)kFB;
+        }
+    }
+    // store what is left in the ring and return the CRC32C of output bytes [0, O)
+    __device__ uint32_t finish(uint32_t O, const uint32_t* __restrict__ gNS) {
+        const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);
+        flush_to(O);
+        wave_sync();
+        uint32_t crc = 0;
+        const uint32_t rem = O - flushed;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t b0 = 8u * lane;
+        const uint32_t end = b0 + 8u < rem ? b0 + 8u : rem;
+        uint32_t c = 0;
+        for (uint32_t i = b0; i < end; ++i) {
+            const uint8_t by = ring8[(flushed + i) & (kRing - 1)];
+            dst[flushed + i] = by;
+            c = (c >> 8) ^ sT[(c ^ by) & 0xFFu];
+        }
+        if (do_crc) {
+            // full blocks: total = XOR_l acc_l * x^(8*8*(63-l)) — 6-level tree with the nibble tables
+            uint32_t fa = acc;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const uint32_t other = __shfl_xor(fa, 1 << j);
+                const bool is_lo = ((lane >> j) & 1) == 0;
+                fa = shift_nib_tab(gNS + j * 128, is_lo ? fa : other) ^ (is_lo ? other : fa);
+            }
+            // tail bytes: per-lane raw CRC shifted by the bytes after its slot
+            const uint32_t after = end > b0 ? rem - end : 0u;
+            c = end > b0 ? gf_multmodp(gf_x8n(after), c) : 0u;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) c ^= __shfl_xor(c, 1 << j);
+            // raw(M) = fold(full) * x^(8*rem) ^ raw(tail); crc = ~(~0 * x^(8|M|) ^ raw(M))
+            const uint32_t raw = gf_multmodp(gf_x8n(rem), fa) ^ c;
+            crc = ~(gf_multmodp(gf_x8n(O), 0xFFFFFFFFu) ^ raw);
+        }
+        return crc;
+    }
+};
+
+// Expand output [O, E) from the producing tags on lanes `prodm` (lane order = stream order):
+// tag on lane l starts at output position ostart, xv = bit31 copy | offset, or the literal's input
+// position.  Returns false if the round guard tripped (never on valid input: the lowest pending
+// piece always has its producers done).
+__device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t E, bool prod, uint64_t prodm, uint32_t ostart,
+                            uint32_t xv, int lane) {
+    WaveLds& L = io.L;
+    const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);
+    const uint32_t* lds32 = L.ring;  // ring at dwords [0, 1024), stage at [1024, 1280)
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(prodm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)prodm, 0u));
+    if (prod) *reinterpret_cast<uint2*>(&L.tagw[2 * rank]) = make_uint2(ostart, xv);
+    if (lane == 0) L.tagw[2 * (uint32_t)__popcll(prodm)] = E;  // sentinel: end of the last tag
+    // first piece of each tag: pieces before it = dwords from floor(O/4) to floor(start/4), plus
+    // one for every producing tag after the first that starts inside a dword
+    const uint64_t unal = __ballot(prod && (ostart & 3u) != 0u);
+    const uint64_t first_bit = prodm & (~prodm + 1ull);
+    const uint32_t pbase = (ostart >> 2) - (O >> 2) + (uint32_t)__popcll(unal & lanemask_le(lane) & ~first_bit);
+    const uint32_t Ptot = ((E + 3u) >> 2) - (O >> 2) + (uint32_t)__popcll(unal & ~first_bit);
+    uint32_t rc = 0;   // rank of the last tag started in an earlier pass
+    uint32_t pbc = 0;  // its first piece
+    for (uint32_t P0 = 0; P0 < Ptot; P0 += 64u) {
+        // piece -> tag: each tag marks its first piece, then a max-scan over the lanes
+        L.scratch[lane] = 0u;
+        wave_sync();
+        if (prod && pbase >= P0 && pbase < P0 + 64u) L.scratch[pbase - P0] = ((rank + 1u) << 6) | (pbase - P0);
+        wave_sync();
+        const uint32_t mk = incl_max_scan(L.scratch[lane]);
+        const uint32_t P = P0 + lane;
+        const bool valid = P < Ptot;
+        uint32_t r = mk ? (mk >> 6) - 1u : rc;
+        const uint32_t k = mk ? (uint32_t)lane - (mk & 63u) : P - pbc;
+        r = valid ? r : 0u;
+        {
+            const uint32_t mlast = uni((uint32_t)__builtin_amdgcn_readlane((int)mk, 63));
+            if (mlast) {
+                rc = (mlast >> 6) - 1u;
+                pbc = P0 + (mlast & 63u);
+            }
+        }
+        // record r and the start of record r+1 (= its end)
+        const uint32_t tstart = L.tagw[2 * r], tx = L.tagw[2 * r + 1], tend = L.tagw[2 * r + 2];
+        const uint32_t A = ((tstart >> 2) + k) << 2;
+        const uint32_t x0 = A > tstart ? A : tstart;
+        const uint32_t x1 = (A + 4u) < tend ? A + 4u : tend;
+        const uint32_t last = (Ptot - P0) < 64u ? (Ptot - P0 - 1u) : 63u;
+        const uint32_t ps = uni((uint32_t)__builtin_amdgcn_readlane((int)x0, 0));
+        const uint32_t pe = uni((uint32_t)__builtin_amdgcn_readlane((int)x1, (int)last));
+        io.flush_to(ps);
+        // source of the piece's first byte x0
+        const bool lit = (tx & 0x80000000u) == 0u;
+        const uint32_t xo = tx & 0x7FFFFFFFu;
+        const uint32_t tlen = tend - tstart;
+        const bool overlap = !lit && xo < tlen;  // copy reads bytes it produces
+        const uint32_t pin = xo + (x0 - tstart);  // literal: input position
+        uint32_t sp, lbase, lmask;  // LDS read: dwords lbase + ((sp >> 2) [+1] & lmask)
+        bool gl;
+        if (lit) {
+            sp = pin + io.a;
+            gl = (sp - io.sbase) > (uint32_t)(kStage - 8);  // outside the stage: read the input from HBM
+            lbase = kRing / 4;
+            lmask = kStage / 4 - 1;
+        } else {
+            sp = x0 - xo;
+#ifdef NX_EXP_NOFAR
+            gl = false;
+#else
+            gl = !overlap && pe > (uint32_t)kRing && sp < pe - (uint32_t)kRing;  // far copy
+#endif
+            lbase = 0;
+            lmask = kRing / 4 - 1;
+        }
+        const uint32_t nbytes = x1 - x0;
+        const uint32_t sh = 8u * (x0 & 3u);
+        const uint32_t bmask = (nbytes >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nbytes)) - 1u)) << sh;
+        const uint32_t waddr = lds_base + 4u * ((x0 >> 2) & (kRing / 4 - 1));
+        // Producer map: byte x of this pass holds the lane (piece) that writes it.  A copy whose
+        // source bytes lie in this pass depends on the contiguous piece range that produces them,
+        // and runs in the first round after all of those are done.  The map aliases `scratch`
+        // (its piece marks were consumed above).
+        const uint32_t psal = ps & ~3u;
+        uint64_t need = 0;
+        wave_sync();
+        {
+            const uint32_t mm = valid ? bmask : 0u;
+            const uint32_t maddr = lds_base + (uint32_t)offsetof(WaveLds, scratch) + (valid ? 4u * ((x0 >> 2) - (psal >> 2)) : 0u);
+            asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(maddr), "v"(mm), "v"(((uint32_t)lane * 0x01010101u) & mm) : "memory");
+        }
+        wave_sync();
+        if (valid && !lit && !gl) {
+            const uint32_t lo0 = overlap ? tstart - xo : sp;
+            const uint32_t hi = overlap ? tstart : sp + nbytes;
+            if (hi > ps) {
+                const uint8_t* M8 = reinterpret_cast<const uint8_t*>(L.scratch);
+                const uint32_t lo = lo0 > ps ? lo0 : ps;
+                const uint32_t pa = M8[lo - psal], pb = M8[hi - 1u - psal];
+                need = (pb >= 63u ? ~0ull : ((2ull << pb) - 1ull)) & ~((1ull << (pa & 63u)) - 1ull);
+            }
+        }
+        // Sources that do not depend on this pass, fetched once before the rounds: far copies (the
+        // frame's own flushed output) and literal bytes outside the stage, from HBM.  (Guarded by
+        // wave-uniform branches so that passes without such pieces skip them entirely.)
+        uint32_t gval = 0;
+        if (__ballot(valid && gl)) {
+            if (valid && gl) {
+                if (!lit) {
+                    gval = g_ld32u(io.dst + sp);  // flushed and drained output of this frame
+                } else if (pin + 4u <= io.in_len) {
+                    gval = g_ld32u(io.src + pin);
+                } else {
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i)
+                        if (pin + i < io.in_len) gval |= g_ld8(io.src + pin + i) << (8 * i);
+                }
+            }
+        }
+        // Overlapping copies (offset < length): out[x] = out[tstart - xo + ((x - tstart) mod xo)],
+        // xo < tlen <= 64; the four ring byte addresses, packed 4 x 12 bits into two dwords.
+        const bool has_ov = __ballot(valid && overlap) != 0ull;
+        uint32_t ova = 0, ovb = 0;
+        if (has_ov) {
+            if (valid && overlap) {
+                const uint32_t n0 = x0 - tstart;
+                const uint32_t inv = (uint32_t)(__builtin_amdgcn_rcpf((float)xo) * 65536.0f) + 1u;  // floor(n0/xo) exact for n0, xo < 64
+                const uint32_t m0 = n0 - xo * ((n0 * inv) >> 16);
+                const uint32_t q = tstart - xo;
+                uint32_t ad[4];
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i) {
+                    uint32_t mi = m0 + i;
+                    mi -= mi >= xo ? xo : 0u;
+                    mi -= mi >= xo ? xo : 0u;
+                    mi -= mi >= xo ? xo : 0u;
+                    ad[i] = (q + mi) & (kRing - 1);
+                }
+                ova = ad[0] | (ad[1] << 16);
+                ovb = ad[2] | (ad[3] << 16);
+            }
+        }
+        uint64_t pending = __ballot(valid);
+        uint64_t done = ~pending;
+        for (int round = 0; pending; ++round) {
+            if (round > 64) return false;
+            const bool ready = ((pending >> lane) & 1ull) != 0 && (need & ~done) == 0ull;
+            // stage (literal) or ring (near copy): one unaligned 4-byte read, all lanes
+            const uint32_t w = sp >> 2;
+            const uint32_t lo = lds32[lbase + (w & lmask)];
+            const uint32_t hi = lds32[lbase + ((w + 1u) & lmask)];
+            uint32_t val = gl ? gval : __builtin_amdgcn_alignbyte(hi, lo, sp & 3u);
+            if (has_ov && __ballot(ready && overlap)) {
+                if (ready && overlap) {
+                    val = (uint32_t)ring8[ova & 0xFFFFu] | ((uint32_t)ring8[ova >> 16] << 8) | ((uint32_t)ring8[ovb & 0xFFFFu] << 16) |
+                          ((uint32_t)ring8[ovb >> 16] << 24);
+                }
+            }
+            // one masked atomic write per lane: the piece's bytes, or nothing (mask 0)
+            const uint32_t m = ready ? bmask : 0u;
+            asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(waddr), "v"(m), "v"((val << sh) & m) : "memory");
+            const uint64_t rb = __ballot(ready);
+            pending &= ~rb;
+            done |= rb;
+        }
+    }
+    return true;
+}
+
+__device__ __forceinline__ void write_result(int lane, uint32_t crc, int32_t st, bool check, uint32_t expect, uint32_t O,
+                                             uint32_t consumed, uint32_t* out_len_p, uint32_t* consumed_p, int32_t* status_p,
+                                             uint32_t* crc_p) {
+    if (lane == 0) {
+        const uint32_t m = mask_checksum(crc);
+        if (st == NX_OK && check && m != expect) st = NX_ERR_SNAPPY_CRC_MISMATCH;
+        *out_len_p = O;
+        if (consumed_p) *consumed_p = consumed;
+        *status_p = st;
+        if (crc_p) *crc_p = m;
+    }
+}
+
+// =====================================================================================
+// Fused single-kernel form: the wave parses 64-byte windows of the compressed stream itself.
+// =====================================================================================
+__device__ void decode_frame_fused(WaveLds& L, uint32_t lds_base, const Frame& f, const uint32_t* __restrict__ sT,
+                                   const uint32_t* __restrict__ sSH, const uint32_t* __restrict__ gNS, bool do_crc, uint32_t expect,
+                                   bool check, uint32_t* out_len_p, uint32_t* consumed_p, int32_t* status_p, uint32_t* crc_p,
+                                   int lane) {
+    FrameIO io(L, f, sT, sSH, do_crc, lane);
+    const uint8_t* __restrict__ src = f.src;
+    const uint32_t in_len = io.in_len;
+    const uint32_t cap = uni(f.cap < (1u << 24) ? f.cap : (1u << 24));
+    int32_t st = NX_OK;
+    uint32_t consumed = 0;
+    uint32_t O = 0;  // output frontier (bytes final)
+
+    // ---- preamble (Snappy.readPreamble, :404-420) — uniform
+    uint32_t W = 0;
+    bool go = false;
+    if (in_len > 0) {
+        uint32_t ulen = 0;
+        int bi = 0;
+        bool complete = false;
+        while (W < in_len) {
+            const uint32_t cur = uni(src[W++]);
+            ulen |= (cur & 0x7fu) << (bi++ * 7);
+            if ((cur & 0x80u) == 0) {
+                complete = true;
+                break;
+            }
+            if (bi >= 4) {
+                st = NX_ERR_SNAPPY_PREAMBLE_TOO_LONG;
+                break;
+            }
+        }
+        if (st == NX_OK && complete && ulen != 0) {
+            if (ulen > cap) st = NX_ERR_SNAPPY_OUTPUT_OVERFLOW; else go = true;
+        }
+        consumed = W;
+    }
+    W = uni(W);
+    if (go) io.prime(W + io.a);
+
+    bool stop = !go;
+    uint32_t windows = 0;
+    while (!stop && W < in_len) {
+        if (++windows > in_len + 2) {
+            st = kGuardTrip;
+            break;
+        }
+        io.advance(W + io.a);
+        wave_sync();  // stage bytes written by other lanes
+        // ---------------- parse: branch-free speculative tag decode at W + lane (bytes from the stage)
+        const uint32_t p = W + lane;
+        const uint32_t avail = p < in_len ? in_len - p : 0u;
+        uint64_t v;
+        {
+            const uint32_t pa = p + io.a;
+            const uint32_t w0 = L.stage[(pa >> 2) & (kStage / 4 - 1)];
+            const uint32_t w1 = L.stage[((pa >> 2) + 1) & (kStage / 4 - 1)];
+            v = (((uint64_t)w1 << 32) | w0) >> (8 * (pa & 3u));
+            if (avail < 5) v &= (1ull << (8 * avail)) - 1ull;  // bytes past the input read as 0
+        }
+        const uint32_t b0 = (uint32_t)v & 0xFFu;
+        const uint32_t type = b0 & 3u;
+        const uint32_t ops = (uint32_t)(v >> 8);  // operand bytes b1..b4, little-endian
+        // literal (decodeLiteral, :454-494)
+        const uint32_t code = b0 >> 2;
+        const uint32_t nb = code >= 60u ? code - 59u : 0u;
+        const uint32_t hdr = 1u + nb;
+        const uint32_t field = nb == 0 ? 0u : (nb == 4 ? ops : (ops & ((1u << (8 * nb)) - 1u)));
+        const uint32_t lj = nb == 0 ? code + 1u : field + 1u;  // Java int `length + 1` (wraps for nb == 4)
+        const bool lneg = nb == 4 && (int32_t)lj < 0;          // IllegalArgumentException (:480-492)
+        const bool lhdr_nei = avail < hdr;
+        const bool l_nei = lhdr_nei || (!lneg && (avail - hdr) < lj);
+        // copies (decodeCopyWith{1,2,4}ByteOffset, :509-626)
+        const uint32_t csize = type == 1u ? 2u : (type == 2u ? 3u : 5u);
+        const uint32_t colen = type == 1u ? 4u + ((b0 >> 2) & 7u) : 1u + (b0 >> 2);
+        const uint32_t coff = type == 1u ? (((b0 & 0xe0u) << 3) | (ops & 0xFFu)) : (type == 2u ? (ops & 0xFFFFu) : ops);
+        const bool c_nei = avail < csize;
+        const bool is_copy = type != 0u;
+        const bool nei = is_copy ? c_nei : l_nei;
+        int32_t err = 0;
+        if (is_copy) {
+            if (!c_nei && coff == 0u) err = NX_ERR_SNAPPY_OFFSET_ZERO;                    // validateOffset (:637-650)
+            else if (!c_nei && type == 3u && (int32_t)coff < 0) err = NX_ERR_SNAPPY_OFFSET_NEGATIVE;
+        } else if (!lhdr_nei && lneg) {
+            err = NX_ERR_SNAPPY_LITERAL_LEN_INVALID;
+        }
+        uint32_t size;  // bytes of this tag in the stream (saturating)
+        uint32_t olen;  // output length (clamped to cap+1)
+        if (is_copy) {
+            size = csize;
+            olen = colen;
+        } else {
+            const uint64_t sz = (uint64_t)hdr + (lneg ? 0ull : (uint64_t)lj);
+            size = sz > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)sz;
+            olen = lneg ? 0u : (lj > cap ? cap + 1u : lj);
+        }
+        const uint32_t xv = is_copy ? (0x80000000u | (coff & 0x7FFFFFFFu)) : ((p + hdr) & 0x7FFFFFFFu);
+        const uint32_t nxt = (uint32_t)lane + size;  // relative position of the following tag
+
+        // ---------------- tag chain by pointer doubling
+        // J0[l] = next tag position if a tag starts at l (64 = leaves the window); positions at or
+        // past the end of the input are fixed points.  Jk = J0^(2^k); lane m then composes the Jk
+        // selected by the bits of m, so lane m ends on the position of the m-th tag.  Those lanes
+        // mark their positions in LDS, and every lane reads back whether a tag starts at it: tags
+        // stay on their own lanes (lane = stream position).
+        const uint32_t lim = uni((in_len - W) < 64u ? (in_len - W) : 64u);
+        uint32_t Jk[6];
+        Jk[0] = (uint32_t)lane >= lim ? (uint32_t)lane : (nxt < 64u ? nxt : 64u);
+#pragma unroll
+        for (int k = 1; k < 6; ++k) {
+            const uint32_t prev = Jk[k - 1];
+            const uint32_t g = (uint32_t)__shfl((int)prev, (int)(prev & 63u));
+            Jk[k] = prev >= 64u ? 64u : g;
+        }
+        uint32_t pos = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t g = (uint32_t)__shfl((int)Jk[k], (int)(pos & 63u));
+            if (((uint32_t)lane >> k) & 1u) pos = pos >= 64u ? 64u : g;
+        }
+        const bool tvm = pos < lim;  // lane m holds the position of tag m
+        const uint32_t T = (uint32_t)__popcll(__ballot(tvm));
+        const uint32_t lastpos = uni((uint32_t)__builtin_amdgcn_readlane((int)pos, (int)(T - 1)));
+        const uint32_t exitrel = uni((uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)lastpos));
+        L.scratch[lane] = 0;
+        wave_sync();
+        if (tvm) L.scratch[pos] = 1u;
+        wave_sync();
+        const bool tv = L.scratch[lane] != 0u;
+
+        // ---------------- ordering: bytes written before each tag, per-tag checks (stream order = lane order)
+        const uint32_t mylen = tv ? olen : 0u;
+        const uint32_t incl = incl_scan(mylen);
+        const uint32_t ostart = O + incl - mylen;
+        if (tv && is_copy && !nei && err == 0 && (coff & 0x7FFFFFFFu) > ostart) err = NX_ERR_SNAPPY_OFFSET_BEYOND;
+        if (tv && !nei && err == 0 && (uint64_t)ostart + olen > cap) err = NX_ERR_SNAPPY_OUTPUT_OVERFLOW;
+        const uint64_t badm = __ballot(tv && (nei || err != 0));
+        const uint32_t Wnext = uni(W + exitrel);
+        uint32_t fb = 64;  // first failing tag (lane); tags on lanes below it execute
+        uint32_t E;
+        if (badm) {
+            fb = (uint32_t)(__ffsll((long long)badm) - 1);
+            const int32_t e = __builtin_amdgcn_readlane(err, (int)fb);
+            if (e != 0) {
+                st = e;
+                consumed = W + uni((uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)fb));
+            } else {
+                consumed = W + fb + 1;  // NOT_ENOUGH_INPUT: tag byte consumed, operands left unread
+            }
+            stop = true;
+            E = uni((uint32_t)__builtin_amdgcn_readlane((int)ostart, (int)fb));
+        } else {
+            consumed = Wnext < in_len ? Wnext : in_len;
+            E = O + uni((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
+        }
+        const bool prod = tv && (uint32_t)lane < fb && olen > 0;  // an output-producing tag
+        const uint64_t prodm = __ballot(prod);
+        if (prodm && !expand_tags(io, lds_base, O, E, prod, prodm, ostart, xv, lane)) {
+            st = kGuardTrip + 2;
+            break;
+        }
+        O = E;
+        W = Wnext;
+    }
+    const uint32_t crc = io.finish(O, gNS);
+    write_result(lane, crc, st, check, expect, O, consumed, out_len_p, consumed_p, status_p, crc_p);
+}
+
+// Loads the workgroup's CRC tables into LDS and yields (wave's LDS block, its LDS byte address, wave index).
+struct WaveSetup {
+    uint32_t* sT;
+    uint32_t* sSH;
+    WaveLds* L;
+    uint32_t lds_base;
+    uint32_t wave;
+};
+__device__ __forceinline__ WaveSetup wave_setup(uint8_t* smem, const CrcTables* __restrict__ tabs, bool do_crc) {
+    WaveSetup s;
+    s.sT = reinterpret_cast<uint32_t*>(smem);  // T8[0..3]
+    s.sSH = s.sT + 4 * 256;                    // SH[5] = shift by 512 B
+    if (do_crc) {
+        for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) s.sT[i] = (&tabs->T8[0][0])[i];
+        for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) s.sSH[i] = (&tabs->SH[5][0][0])[i];
+    }
+    __syncthreads();
+    // wave index as an SGPR: divergence analysis cannot see that threadIdx.x >> 6 is wave-uniform,
+    // and everything derived from it (the frame, its pointers, sizes, positions) would otherwise
+    // live in VGPRs with exec-masked control flow
+    s.wave = uni(threadIdx.x >> 6);
+    s.L = reinterpret_cast<WaveLds*>(smem + kTabBytes + s.wave * sizeof(WaveLds));
+    // LDS byte address of L for the inline-asm atomics: the low 32 bits of a flat pointer into the
+    // LDS aperture are the LDS offset
+    s.lds_base = (uint32_t)(uintptr_t)s.L;
+    return s;
+}
+
+// filter: decode only frames whose status holds kNeedFused (the fallback after k_parse)
+__global__ void __launch_bounds__(kWaves * 64, 6)
+    k_decode_fused(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
+                   uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+                   uint32_t* __restrict__ out_len, uint32_t* __restrict__ consumed, int32_t* __restrict__ status,
+                   const uint32_t* __restrict__ expect, uint32_t* __restrict__ crc_out, uint32_t n, const CrcTables* __restrict__ tabs,
+                   int filter) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const bool do_crc = (expect != nullptr) || (crc_out != nullptr);
+    const WaveSetup s = wave_setup(smem, tabs, do_crc);
+    const int lane = threadIdx.x & 63;
+    // static wave -> frame assignment, neighbouring waves on neighbouring frames
+    const uint32_t nw = gridDim.x * kWaves;
+    for (uint32_t c = blockIdx.x * kWaves + s.wave; c < n; c += nw) {
+        if (filter && uni((uint32_t)status[c]) != (uint32_t)kNeedFused) continue;
+        Frame f{in + in_off[c], in_len[c], out + out_off[c], out_cap ? out_cap[c] : 65536u};
+        decode_frame_fused(*s.L, s.lds_base, f, s.sT, s.sSH, &tabs->NS[0][0][0], do_crc, expect ? expect[c] : 0u, expect != nullptr,
+                           &out_len[c], consumed ? &consumed[c] : nullptr, &status[c], crc_out ? &crc_out[c] : nullptr, lane);
+    }
+}
+
+// =====================================================================================
+// k_parse: one lane per frame — Snappy.decode's state machine (Snappy.java:315-393) emitting records
+// =====================================================================================
+
+// Burst window: 64 bytes of the lane's compressed stream staged in LDS (17-dword lane stride:
+// conflict-free across the wave).  The parse runs in bursts: every lane whose next tag header is
+// not in its window reloads it (four 16-byte aligned loads; a 16-byte block holding at least one
+// byte of the chunk never crosses a page, blocks wholly past the end are not loaded), the wave
+// waits once, then each lane parses tags until its window runs out.  One memory latency per ~20
+// tags instead of one per tag for whichever lane happens to cross a block.
+constexpr int kParseBlock = 256;
+constexpr int kWinDw = 17;
+struct BurstWin {
+    const uint8_t* origin;  // chunk start rounded down to 16 bytes
+    uint32_t pad, end;      // chunk start - origin; chunk end, origin-relative
+    uint32_t base;          // window = origin-relative [base, base + 64)
+    uint32_t* w;            // this lane's LDS window
+    __device__ __forceinline__ void init(const uint8_t* in, uint32_t length, uint32_t* lds) {
+        origin = reinterpret_cast<const uint8_t*>((uintptr_t)in & ~(uintptr_t)15);
+        pad = (uint32_t)((uintptr_t)in & 15u);
+        end = pad + length;
+        base = 0xFFFFFF00u;
+        w = lds;
+    }
+    // are the (up to) 5 header bytes at chunk position p in the window?
+    __device__ __forceinline__ bool has(uint32_t p) const {
+        const uint32_t q = p + pad;
+        return q >= base && (q + 5u <= base + 64u || base + 64u >= end);
+    }
+    __device__ __forceinline__ void load(uint32_t p) {
+        base = (p + pad) & ~15u;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            if (base + 16u * k < end) {
+                const uint4 x = *reinterpret_cast<const uint4*>(origin + base + 16u * k);
+                w[4 * k] = x.x;
+                w[4 * k + 1] = x.y;
+                w[4 * k + 2] = x.z;
+                w[4 * k + 3] = x.w;
+            }
+        }
+    }
+    // 8 bytes at chunk position p, has(p) (bytes at or past the chunk end are unspecified)
+    __device__ __forceinline__ uint64_t get8(uint32_t p) const {
+        const uint32_t off = p + pad - base;
+        const uint32_t i = off >> 2, s = off & 3u;
+        const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2];
+        return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
+    }
+};
+
+// Record writer: 4 records per 16-byte store into the frame's slot.
+struct RecWriter {
+    uint4* slot;
+    uint32_t n;  // records emitted
+    uint32_t q0, q1, q2, q3;
+    __device__ __forceinline__ bool put(uint32_t r) {
+        if (n >= kRecCap) return false;
+        const uint32_t k = n & 3u;
+        q0 = k == 0 ? r : q0;
+        q1 = k == 1 ? r : q1;
+        q2 = k == 2 ? r : q2;
+        q3 = r;
+        if (k == 3) slot[n >> 2] = make_uint4(q0, q1, q2, q3);
+        ++n;
+        return true;
+    }
+    __device__ __forceinline__ void finish() {
+        if (n & 3u) slot[n >> 2] = make_uint4(q0, q1, q2, q3);
+    }
+};
+
+__global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                       const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ out_cap,
+                                                       uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
+                                                       uint32_t* __restrict__ out_len, uint32_t* __restrict__ consumed_a,
+                                                       int32_t* __restrict__ status, uint32_t n) {
+    __shared__ uint32_t wins[kParseBlock * kWinDw + 4];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint32_t in_len = in_len_a[c];
+    uint32_t cap = out_cap ? out_cap[c] : 65536u;
+    cap = cap < (1u << 24) ? cap : (1u << 24);
+    if (in_len >= (1u << 25)) {  // literal positions need 25 bits
+        status[c] = kNeedFused;
+        return;
+    }
+    BurstWin win;
+    win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
+    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), 0, 0, 0, 0, 0};
+    uint32_t ip = 0, op = 0;
+    int32_t st = NX_OK;
+    bool run = false;
+    // ---- preamble (readPreamble, :404-420): at most 4 bytes
+    if (in_len > 0) {
+        win.load(0);
+        const uint64_t v = win.get8(0);
+        uint32_t ulen = 0;
+        int bi = 0;
+        bool complete = false;
+        while (ip < in_len) {
+            const uint32_t cur = (uint32_t)(v >> (8 * ip)) & 0xFFu;
+            ++ip;
+            ulen |= (cur & 0x7fu) << (bi++ * 7);
+            if ((cur & 0x80u) == 0) {
+                complete = true;
+                break;
+            }
+            if (bi >= 4) {
+                st = NX_ERR_SNAPPY_PREAMBLE_TOO_LONG;
+                break;
+            }
+        }
+        if (st == NX_OK && complete && ulen != 0) {
+            if (ulen > cap) st = NX_ERR_SNAPPY_OUTPUT_OVERFLOW; else run = true;
+        }
+    }
+    // ---- tags (:328-392, decodeLiteral :454-494, decodeCopyWith*ByteOffset :509-626, validateOffset :637-650)
+    for (;;) {
+        run = run && ip < in_len;
+        if (!__any(run)) break;
+        if (run && !win.has(ip)) win.load(ip);  // burst reload: one wait for the whole wave
+        while (run && win.has(ip)) {
+            // one tag, branch-free: both interpretations are computed and selected by the type
+            const uint64_t v = win.get8(ip);
+            const uint32_t tag = (uint32_t)v & 0xFFu;
+            const uint32_t ops = (uint32_t)(v >> 8);  // operand bytes (valid where < in_len)
+            const uint32_t after_tag = ip + 1u;
+            const uint32_t avail = in_len - after_tag;
+            const uint32_t type = tag & 3u;
+            const bool isl = type == 0u;
+            const uint32_t code = tag >> 2;
+            // literal (decodeLiteral): nb length bytes after the tag, Java int length + 1
+            const uint32_t nb = (isl && code >= 60u) ? code - 59u : 0u;
+            const uint32_t fmask = nb >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
+            const uint32_t lj = nb == 0u ? code + 1u : (ops & fmask) + 1u;
+            // copy (decodeCopyWith{1,2,4}ByteOffset)
+            const uint32_t csize = type == 1u ? 1u : (type == 2u ? 2u : 4u);
+            const uint32_t clen = type == 1u ? 4u + (code & 7u) : 1u + code;
+            const uint32_t coff = type == 1u ? (((tag & 0xe0u) << 3) | (ops & 0xFFu)) : (type == 2u ? (ops & 0xFFFFu) : ops);
+            const uint32_t hdr = isl ? nb : csize;
+            const uint32_t dpos = after_tag + hdr;
+            const bool lneg = isl && (int32_t)lj < 0;
+            // NOT_ENOUGH_INPUT (silent stop, the tag byte consumed): operands, or the literal's bytes
+            const bool nei = avail < hdr || (isl && !lneg && in_len - dpos < lj);
+            const uint32_t len = isl ? lj : clen;
+            int32_t err = 0;
+            if (isl) {
+                err = lneg ? NX_ERR_SNAPPY_LITERAL_LEN_INVALID : 0;
+            } else {
+                err = coff == 0u ? NX_ERR_SNAPPY_OFFSET_ZERO
+                                 : ((int32_t)coff < 0 ? NX_ERR_SNAPPY_OFFSET_NEGATIVE : (coff > op ? NX_ERR_SNAPPY_OFFSET_BEYOND : 0));
+            }
+            if (err == 0 && (uint64_t)op + len > cap) err = NX_ERR_SNAPPY_OUTPUT_OVERFLOW;
+            if (nei || err != 0) {  // rare: the frame stops here
+                ip = nei ? after_tag : dpos;
+                st = nei ? NX_OK : err;
+                run = false;
+                continue;
+            }
+            const uint32_t m0 = lj < 64u ? lj : 64u;
+            const uint32_t r = isl ? (((m0 - 1u) << 25) | dpos) : (0x80000000u | ((clen - 1u) << 25) | coff);
+            bool fit = (isl && lj == 0u) || rw.put(r);  // a zero-length literal (field 0xFFFFFFFF) emits nothing
+            if (isl && lj > 64u) {  // literals longer than 64 bytes: one record per 64 bytes
+                for (uint32_t k = 64u; k < lj && fit; k += 64u) {
+                    const uint32_t m = lj - k < 64u ? lj - k : 64u;
+                    fit = rw.put(((m - 1u) << 25) | (dpos + k));
+                }
+            }
+            if (!fit) {
+                st = kNeedFused;
+                run = false;
+                continue;
+            }
+            ip = dpos + (isl ? lj : 0u);
+            op += len;
+            run = ip < in_len;
+        }
+    }
+    if (st == kNeedFused) {
+        status[c] = kNeedFused;
+        return;
+    }
+    rw.finish();
+    nrec[c] = rw.n;
+    out_len[c] = op;
+    if (consumed_a) consumed_a[c] = ip;
+    status[c] = st;
+}
+
+// =====================================================================================
+// k_expand: one wave per frame executes the frame's records
+// =====================================================================================
+__global__ void __launch_bounds__(kWaves * 64, 6)
+    k_expand(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
+             uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ rec,
+             const uint32_t* __restrict__ nrec, uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
+             const uint32_t* __restrict__ expect, uint32_t* __restrict__ crc_out, uint32_t n, const CrcTables* __restrict__ tabs) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const bool do_crc = (expect != nullptr) || (crc_out != nullptr);
+    const WaveSetup s = wave_setup(smem, tabs, do_crc);
+    const int lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * kWaves;
+    for (uint32_t c = blockIdx.x * kWaves + s.wave; c < n; c += nw) {
+        int32_t st = (int32_t)uni((uint32_t)status[c]);
+        if (st == kNeedFused) continue;
+        const uint32_t N = uni(nrec[c]);
+        const uint32_t Ofin = uni(out_len[c]);
+        Frame f{in + in_off[c], in_len[c], out + out_off[c], 0u};
+        FrameIO io(*s.L, f, s.sT, s.sSH, do_crc, lane);
+        const uint32_t* __restrict__ R = rec + (size_t)c * kRecCap;
+        uint32_t O = 0;
+        bool primed = false;
+        uint32_t rnext = (uint32_t)lane < N ? R[lane] : 0u;
+        for (uint32_t b = 0; b < N; b += 64u) {
+            const uint32_t r = rnext;
+            rnext = b + 64u + (uint32_t)lane < N ? R[b + 64u + lane] : 0u;  // prefetch the next batch
+            const bool valid = b + (uint32_t)lane < N;
+            const bool isc = (r >> 31) != 0u;
+            const uint32_t len = valid ? ((r >> 25) & 63u) + 1u : 0u;
+            const uint32_t x = r & 0x1FFFFFFu;
+            const uint32_t incl = incl_scan(len);
+            const uint32_t ostart = O + incl - len;
+            const uint32_t E = O + uni((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
+            // the stage follows the first literal of the batch (literal positions are monotone)
+            const uint64_t litm = __ballot(valid && !isc);
+            if (litm) {
+                const uint32_t w = uni((uint32_t)__builtin_amdgcn_readlane((int)x, __ffsll((long long)litm) - 1));
+                if (!primed) {
+                    io.prime(w + io.a);
+                    primed = true;
+                } else {
+                    io.advance(w + io.a);
+                }
+                wave_sync();  // stage bytes written by other lanes
+            }
+            const uint32_t xv = isc ? (0x80000000u | x) : x;
+            if (!expand_tags(io, s.lds_base, O, E, valid, __ballot(valid), ostart, xv, lane)) {
+                st = kGuardTrip + 2;
+                break;
+            }
+            O = E;
+        }
+        if (st == kGuardTrip + 2) O = Ofin;  // unreachable on a consistent record stream
+        const uint32_t crc = io.finish(O, &tabs->NS[0][0][0]);
+        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],
+                     crc_out ? &crc_out[c] : nullptr);
+    }
+}
+
+// =====================================================================================
+// LZ4 blocks through the same record expander
+// =====================================================================================
+// The LZ4 block format (lz4-java 1.8.0 as Lz4FrameDecoder.java:203-208 drives it: the decompressor
+// must produce exactly decompressedLength bytes): sequences of token | literal-length extension |
+// literals | 2-byte LE offset | match-length extension (+4); the last sequence is literals only.
+// k_parse_lz4 walks a block per lane and emits the same 32-bit records as k_parse (literal runs and
+// matches split at 64 bytes: a match's bytes repeat at its distance, so the split is exact); k_expand
+// produces the bytes.  Checks (each NX_ERR_LZ4_MALFORMED, oracle/netty_oracle.c orc_lz4_decompress):
+// reading past the block, an offset of 0 or beyond the bytes produced, output past want, and a block
+// that ends with the output short of want.
+__device__ __forceinline__ uint32_t win_byte(BurstWin& win, uint32_t p) {
+    if (!win.has(p)) win.load(p);
+    return (uint32_t)win.get8(p) & 0xFFu;
+}
+
+__global__ void __launch_bounds__(kParseBlock) k_parse_lz4(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                           const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ want_a,
+                                                           uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
+                                                           uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t n) {
+    __shared__ uint32_t wins[kParseBlock * kWinDw + 4];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint32_t in_len = in_len_a[c];
+    const uint32_t want = want_a[c];
+    // literal positions need 25 bits; blocks of more than 64 KiB output (Lz4FrameEncoder block sizes
+    // above the default, :158-166) go to the lane-serial kernel, which has no window limit
+    if (in_len >= (1u << 25) || want > 65536u) {
+        status[c] = kNeedFused;
+        return;
+    }
+    BurstWin win;
+    win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
+    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), 0, 0, 0, 0, 0};
+    uint32_t ip = 0, op = 0;
+    int32_t st = NX_OK;
+    bool fit = true;
+    for (;;) {
+        if (ip >= in_len) {  // a block ends after a literal run, never before a token
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        const uint32_t token = win_byte(win, ip++);
+        uint32_t lit = token >> 4;
+        if (lit == 15u) {
+            uint32_t b = 255u;
+            while (b == 255u && ip < in_len) {
+                b = win_byte(win, ip++);
+                lit += b;  // < 15 + 255 * 2^25: no wrap
+            }
+            if (b == 255u) {
+                st = NX_ERR_LZ4_MALFORMED;
+                break;
+            }
+        }
+        if (lit > in_len - ip || lit > want - op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        for (uint32_t k = 0; k < lit && fit; k += 64u) {
+            const uint32_t m = lit - k < 64u ? lit - k : 64u;
+            fit = rw.put(((m - 1u) << 25) | (ip + k));
+        }
+        if (!fit) break;
+        ip += lit;
+        op += lit;
+        if (ip == in_len) break;  // the last sequence
+        if (in_len - ip < 2u) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        const uint32_t off = win_byte(win, ip) | (win_byte(win, ip + 1u) << 8);
+        ip += 2u;
+        if (off == 0u || off > op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        uint32_t ml = token & 15u;
+        if (ml == 15u) {
+            uint32_t b = 255u;
+            while (b == 255u && ip < in_len) {
+                b = win_byte(win, ip++);
+                ml += b;
+            }
+            if (b == 255u) {
+                st = NX_ERR_LZ4_MALFORMED;
+                break;
+            }
+        }
+        ml += 4u;
+        if (ml > want - op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        for (uint32_t k = 0; k < ml && fit; k += 64u) {
+            const uint32_t m = ml - k < 64u ? ml - k : 64u;
+            fit = rw.put(0x80000000u | ((m - 1u) << 25) | off);
+        }
+        if (!fit) break;
+        op += ml;
+    }
+    if (!fit) {
+        status[c] = kNeedFused;
+        return;
+    }
+    if (st == NX_OK && op != want) st = NX_ERR_LZ4_MALFORMED;
+    rw.finish();
+    nrec[c] = rw.n;
+    out_len[c] = op;
+    status[c] = st;
+}
+
+// Blocks k_parse_lz4 could not slot (more than kRecCap records, or >= 32 MiB): one lane decodes the
+// block byte by byte, same checks.
+__global__ void __launch_bounds__(256) k_lz4_serial(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                    const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ want_a,
+                                                    uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                                    int32_t* __restrict__ status, uint32_t n) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n || status[c] != kNeedFused) return;
+    const uint8_t* s = in + in_off[c];
+    uint8_t* d = out + out_off[c];
+    const uint64_t in_len = in_len_a[c], want = want_a[c];
+    uint64_t ip = 0, op = 0;
+    int32_t st = NX_OK;
+    for (;;) {
+        if (ip >= in_len) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        const uint32_t token = s[ip++];
+        uint64_t lit = token >> 4;
+        if (lit == 15u) {
+            uint32_t b = 255u;
+            while (b == 255u && ip < in_len) {
+                b = s[ip++];
+                lit += b;
+            }
+            if (b == 255u) {
+                st = NX_ERR_LZ4_MALFORMED;
+                break;
+            }
+        }
+        if (lit > in_len - ip || lit > want - op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        for (uint64_t k = 0; k < lit; ++k) d[op + k] = s[ip + k];
+        ip += lit;
+        op += lit;
+        if (ip == in_len) break;
+        if (in_len - ip < 2u) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        const uint64_t off = (uint64_t)s[ip] | ((uint64_t)s[ip + 1] << 8);
+        ip += 2;
+        if (off == 0u || off > op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        uint64_t ml = token & 15u;
+        if (ml == 15u) {
+            uint32_t b = 255u;
+            while (b == 255u && ip < in_len) {
+                b = s[ip++];
+                ml += b;
+            }
+            if (b == 255u) {
+                st = NX_ERR_LZ4_MALFORMED;
+                break;
+            }
+        }
+        ml += 4u;
+        if (ml > want - op) {
+            st = NX_ERR_LZ4_MALFORMED;
+            break;
+        }
+        for (uint64_t k = 0; k < ml; ++k) d[op + k] = d[op + k - off];
+        op += ml;
+    }
+    if (st == NX_OK && op != want) st = NX_ERR_LZ4_MALFORMED;
+    status[c] = st;
+}
+
+}  // namespace dec
+}  // namespace nx
+
+namespace {
+// Record workspace for the parse/expand pair, one per (device, stream): launches on one stream
+// are ordered and may share it; launches on different streams may overlap and must not.
+struct DecWorkspace {
+    uint32_t* rec = nullptr;
+    uint32_t* nrec = nullptr;
+    uint32_t* olen = nullptr;  // LZ4: bytes produced per block (the caller's lengths are inputs)
+    size_t frames = 0;
+};
+std::mutex g_dws_mu;
+std::map<std::pair<int, hipStream_t>, DecWorkspace> g_dws;
+}  // namespace
+
+// Dynamic-LDS limit of the wave kernels, set once per process.
+static hipError_t wave_kernel_attrs(size_t lds) {
+    static std::once_flag once;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [&] {
+        for (const void* k : {(const void*)nx::dec::k_decode_fused, (const void*)nx::dec::k_expand})
+            if (attr_err == hipSuccess) attr_err = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    });
+    return attr_err;
+}
+
+// The (device, stream) record workspace with room for `sb` frames; caller holds g_dws_mu.
+static hipError_t dec_workspace(int dev, hipStream_t st, uint32_t sb, DecWorkspace** out) {
+    DecWorkspace& W = g_dws[{dev, st}];
+#define NX_HIP_CHECK_E(x)                \
+    do {                                 \
+        hipError_t e_ = (x);             \
+        if (e_ != hipSuccess) return e_; \
+    } while (0)
+    if (W.rec == nullptr || W.frames < sb) {
+        if (W.rec) NX_HIP_CHECK_E(hipFree(W.rec));  // hipFree synchronises with pending work
+        if (W.nrec) NX_HIP_CHECK_E(hipFree(W.nrec));
+        if (W.olen) NX_HIP_CHECK_E(hipFree(W.olen));
+        W.rec = nullptr;
+        W.nrec = nullptr;
+        W.olen = nullptr;
+        NX_HIP_CHECK_E(hipMalloc(&W.rec, (size_t)sb * nx::dec::kRecCap * sizeof(uint32_t)));
+        NX_HIP_CHECK_E(hipMalloc(&W.nrec, (size_t)sb * sizeof(uint32_t)));
+        NX_HIP_CHECK_E(hipMalloc(&W.olen, (size_t)sb * sizeof(uint32_t)));
+        W.frames = sb;
+    }
+#undef NX_HIP_CHECK_E
+    *out = &W;
+    return hipSuccess;
+}
+
+static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
+                            const uint32_t* out_cap, uint32_t* out_len, uint32_t* consumed, int32_t* status,
+                            const uint32_t* expected_masked_crc, uint32_t* crc_out, uint32_t n, void* stream, bool fused_only) {
+    using namespace nx::dec;
+    if (n == 0) return NX_OK;
+    if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
+    if (nx::crc_tables_init() != NX_OK) return NX_ERR_HIP;
+    int dev = 0, cus = 256;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const size_t lds = kTabBytes + kWaves * sizeof(WaveLds);
+    NX_HIP_CHECK(wave_kernel_attrs(lds));
+    unsigned blocks_per_cu = (unsigned)(160 * 1024 / lds);
+    if (blocks_per_cu < 1) blocks_per_cu = 1;
+    const hipStream_t st = (hipStream_t)stream;
+    const uint64_t want = (uint64_t)cus * blocks_per_cu;
+    auto wave_grid = [&](uint32_t m) {
+        const uint64_t need = (m + kWaves - 1) / kWaves;
+        return (unsigned)(need < want ? need : want);
+    };
+    if (fused_only) {
+        hipLaunchKernelGGL(k_decode_fused, dim3(wave_grid(n)), dim3(kWaves * 64), lds, st, in, in_off, in_len, out, out_off, out_cap,
+                           out_len, consumed, status, expected_masked_crc, crc_out, n, nx::crc_tables_dev(), 0);
+        NX_HIP_CHECK(hipGetLastError());
+        return NX_OK;
+    }
+    const uint32_t sb = n < kSubBatch ? n : kSubBatch;
+    std::lock_guard<std::mutex> lk(g_dws_mu);
+    DecWorkspace* Wp = nullptr;
+    NX_HIP_CHECK(dec_workspace(dev, st, sb, &Wp));
+    DecWorkspace& W = *Wp;
+    for (uint32_t base = 0; base < n; base += sb) {
+        const uint32_t m = n - base < sb ? n - base : sb;
+        hipLaunchKernelGGL(k_parse, dim3((m + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, st, in, in_off + base, in_len + base,
+                           out_cap ? out_cap + base : nullptr, W.rec, W.nrec, out_len + base, consumed ? consumed + base : nullptr,
+                           status + base, m);
+        NX_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_expand, dim3(wave_grid(m)), dim3(kWaves * 64), lds, st, in, in_off + base, in_len + base, out,
+                           out_off + base, W.rec, W.nrec, out_len + base, status + base,
+                           expected_masked_crc ? expected_masked_crc + base : nullptr, crc_out ? crc_out + base : nullptr, m,
+                           nx::crc_tables_dev());
+        NX_HIP_CHECK(hipGetLastError());
+        // frames k_parse could not slot (more than kRecCap records, or input >= 32 MiB)
+        hipLaunchKernelGGL(k_decode_fused, dim3(wave_grid(m)), dim3(kWaves * 64), lds, st, in, in_off + base, in_len + base, out,
+                           out_off + base, out_cap ? out_cap + base : nullptr, out_len + base, consumed ? consumed + base : nullptr,
+                           status + base, expected_masked_crc ? expected_masked_crc + base : nullptr,
+                           crc_out ? crc_out + base : nullptr, m, nx::crc_tables_dev(), 1);
+        NX_HIP_CHECK(hipGetLastError());
+    }
+    return NX_OK;
+}
+
+extern "C" int32_t nx_snappy_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                          const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len,
+                                          uint32_t* consumed, int32_t* status, const uint32_t* expected_masked_crc,
+                                          uint32_t* crc_out, uint32_t n, void* stream) {
+    return decode_batch(in, in_off, in_len, out, out_off, out_cap, out_len, consumed, status, expected_masked_crc, crc_out, n, stream,
+                        false);
+}
+
+extern "C" int32_t nx_snappy_decode_batch_fused(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                                const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len,
+                                                uint32_t* consumed, int32_t* status, const uint32_t* expected_masked_crc,
+                                                uint32_t* crc_out, uint32_t n, void* stream) {
+    return decode_batch(in, in_off, in_len, out, out_off, out_cap, out_len, consumed, status, expected_masked_crc, crc_out, n, stream,
+                        true);
+}
+
+// Replaces LZ4FastDecompressor.decompress as Lz4FrameDecoder.decode calls it for one
+// BLOCK_TYPE_COMPRESSED block (Lz4FrameDecoder.java:199-208): block i = in[in_off[i] .. +in_len[i])
+// must decode to exactly out_len[i] bytes at out + out_off[i].
+extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                       const uint64_t* out_off, const uint32_t* out_len, int32_t* status, uint32_t n,
+                                       void* stream) {
+    using namespace nx::dec;
+    if (n == 0) return NX_OK;
+    if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
+    if (nx::crc_tables_init() != NX_OK) return NX_ERR_HIP;
+    int dev = 0, cus = 256;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const size_t lds = kTabBytes + kWaves * sizeof(WaveLds);
+    NX_HIP_CHECK(wave_kernel_attrs(lds));
+    unsigned blocks_per_cu = (unsigned)(160 * 1024 / lds);
+    if (blocks_per_cu < 1) blocks_per_cu = 1;
+    const hipStream_t st = (hipStream_t)stream;
+    const uint64_t want = (uint64_t)cus * blocks_per_cu;
+    const uint32_t sb = n < kSubBatch ? n : kSubBatch;
+    std::lock_guard<std::mutex> lk(g_dws_mu);
+    DecWorkspace* W = nullptr;
+    NX_HIP_CHECK(dec_workspace(dev, st, sb, &W));
+    for (uint32_t base = 0; base < n; base += sb) {
+        const uint32_t m = n - base < sb ? n - base : sb;
+        const uint64_t need = (m + kWaves - 1) / kWaves;
+        hipLaunchKernelGGL(k_parse_lz4, dim3((m + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, st, in, in_off + base,
+                           in_len + base, out_len + base, W->rec, W->nrec, W->olen, status + base, m);
+        NX_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_expand, dim3((unsigned)(need < want ? need : want)), dim3(kWaves * 64), lds, st, in, in_off + base,
+                           in_len + base, out, out_off + base, W->rec, W->nrec, W->olen, status + base, nullptr, nullptr, m,
+                           nx::crc_tables_dev());
+        NX_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_lz4_serial, dim3((m + 255) / 256), dim3(256), 0, st, in, in_off + base, in_len + base, out_len + base,
+                           out, out_off + base, status + base, m);
+        NX_HIP_CHECK(hipGetLastError());
+    }
+    return NX_OK;
+}
