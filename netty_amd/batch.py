@@ -280,7 +280,7 @@ def pack(chunks: list[bytes], device, align: int = 16, pad: int = 0):
     buf = bytearray(cur + pad + 16)
     for o, c in zip(offs, chunks):
         buf[o:o + len(c)] = c
-    data = torch.frombuffer(bytes(buf), dtype=torch.uint8).to(device)
+    data = torch.frombuffer(buf, dtype=torch.uint8).to(device)  # buf is a fresh bytearray, copied by .to()
     off = torch.tensor(offs, dtype=torch.int64, device=device)
     ln = torch.tensor([len(c) for c in chunks], dtype=torch.int32, device=device)
     return data, off, ln

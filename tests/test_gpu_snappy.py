@@ -187,6 +187,31 @@ def test_crc32c_batch(dev, B, oracle):
     assert got == [oracle.snappy_checksum(c) for c in chunks]
 
 
+def test_crc32c_block_edges_every_alignment(dev, B, oracle):
+    """The CRC kernel reads a chunk as 8 KiB blocks of 128-byte lane slots aligned to the chunk END
+    (leading/trailing zero padding, init folded into bytes 0..3): lengths around the block and slot
+    edges (including chunk bytes 0..3 straddling blocks 0/1), at every start address mod 16."""
+    rng = random.Random(11)
+    lengths = [4, 5, 7, 8, 127, 128, 129, 8187, 8188, 8189, 8190, 8191, 8192, 8193, 8196, 16380, 16385, 16387, 16388,
+               24577, 65535, 65536, 65537, 100003]
+    buf, offs, lens, want = bytearray(), [], [], []
+    for n in lengths:
+        data = bytes(rng.getrandbits(8) for _ in range(n))
+        for s in range(16):
+            pos = (len(buf) + 15) // 16 * 16 + s
+            buf.extend(bytes(pos - len(buf)))
+            offs.append(pos)
+            buf.extend(data)
+            lens.append(n)
+        want += [oracle.snappy_checksum(data)] * 16
+    buf.extend(bytes(32))
+    inp = torch.frombuffer(buf, dtype=torch.uint8).to(dev)
+    off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    ln = torch.tensor(lens, dtype=torch.int32, device=dev)
+    got = [x & 0xFFFFFFFF for x in B.crc32c_masked(inp, off, ln).cpu().tolist()]
+    assert got == want
+
+
 def test_textgen_device_matches_host(dev, B, oracle):
     n, L = 37, 65536
     out = torch.empty(n * L, dtype=torch.uint8, device=dev)
