@@ -346,6 +346,34 @@ def roofline(algo_bytes, ms, n_chunks, kernels, traffic, copy_gbs):
 
 
 ENC_KERNELS = ["nx::enc::k_snappy_encode"]
+# Snappy.encode's memory requests per 64 KiB chunk of the bench corpus (CPU count of Netty's matcher,
+# profiles/r01/encoder_experiments.md): table probes (read + insert of a random slot) and candidate
+# compares (a random read of the chunk's input)
+ENC_PROBES_PER_CHUNK = 16546
+ENC_CANDIDATE_LOADS_PER_CHUNK = 9709
+
+
+def probe_ceiling(torch, dev, lanes=262144, steps=16384):
+    """The random-access ceiling of the encoder's request pattern on this GPU (netty_amd/tools/
+    probe_ceiling.hip: per lane a serial chain of table exchanges + 60 % dependent input loads over
+    its own 64 KiB regions, at the encoder's resident lane count).  Returns probes/s or None."""
+    import ctypes
+    path = os.path.join(ROOT, "netty_amd", "libnx_probe_ceiling.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.nx_probe_ceiling.restype = ctypes.c_int32
+    lib.nx_probe_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
+    tab = torch.empty(lanes * 16384, dtype=torch.int32, device=dev)
+    inp = torch.empty(lanes * 16384, dtype=torch.int32, device=dev)
+    sink = torch.empty(lanes, dtype=torch.int32, device=dev)
+    ms = ctypes.c_float(0.0)
+    rc = lib.nx_probe_ceiling(tab.data_ptr(), inp.data_ptr(), sink.data_ptr(), lanes, steps, ctypes.byref(ms),
+                              ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    del tab, inp, sink
+    torch.cuda.empty_cache()
+    return lanes * steps / (ms.value / 1e3) if rc == 0 and ms.value > 0 else None
 DEC_KERNELS = ["nx::dec::k_parse", "nx::dec::k_expand"]
 
 
@@ -407,6 +435,16 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
     traffic = load_traffic() if gpu else (None, "cpu test leg")
     r_dec = roofline(C_ + U, t_dec, n, DEC_KERNELS, traffic, copy_gbs)  # decode: C_in + U_out per chunk
     r_enc = roofline(U + C_, t_enc, n, ENC_KERNELS, traffic, copy_gbs)  # encode: U_in + C_out per chunk
+    if gpu and t_enc:
+        ceil = probe_ceiling(torch, dev)
+        got = ENC_PROBES_PER_CHUNK * n / (t_enc / 1e3)
+        r_enc["random_access"] = {
+            "note": "the encoder's bound: serial chains of random table exchanges + candidate loads per lane",
+            "probes_per_chunk": ENC_PROBES_PER_CHUNK, "candidate_loads_per_chunk": ENC_CANDIDATE_LOADS_PER_CHUNK,
+            "achieved_probes_per_s": round(got / 1e9, 3) * 1e9,
+            "ceiling_probes_per_s": round(ceil / 1e9, 3) * 1e9 if ceil else None,
+            "frac": round(got / ceil, 4) if ceil else None,
+            "ceiling_source": "netty_amd/tools/probe_ceiling.hip, same request mix without compute, 262144 lanes, timed live"}
     dominant = r_enc if t_enc >= t_dec else r_dec
     value = args.total_chunks * CHUNK / elapsed * args.steps / 2**30
     line = {

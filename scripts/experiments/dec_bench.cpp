@@ -12,7 +12,7 @@
 #include <string.h>
 #include <vector>
 int main(int argc, char** argv) {
-    using namespace nx::dec;
+    using namespace nx::decx;
     int N = argc > 1 ? atoi(argv[1]) : 65536, R = argc > 2 ? atoi(argv[2]) : 3, crc = argc > 3 ? atoi(argv[3]) : 1;
     const int L = 65536;
     static nx_textgen_tables tg;
@@ -81,5 +81,12 @@ int main(int argc, char** argv) {
     printf("N=%d lds=%zu grid=%u parse_ms=%.2f expand_ms=%.2f per262k=%.1f+%.1f decGiB/s=%.1f ratio=%.4f badstatus=%d mismatch=%d\n", N, lds,
            eg, bp, be, bp * 262144.0 / N, be * 262144.0 / N, (double)N * L / ((bp + be) / 1e3) / (1 << 30), (double)tot / N / L, badst,
            bad);
+#ifdef NX_EXP_COUNT
+    unsigned long long c[8];
+    hipMemcpyFromSymbol(c, HIP_SYMBOL(g_cnt), sizeof(c));
+    const double fr = (double)N * R;
+    printf("per frame: passes %.1f rounds %.1f pieces %.1f far %.1f overlap %.1f  rounds/pass %.2f\n", c[0] / fr, c[1] / fr, c[2] / fr,
+           c[3] / fr, c[4] / fr, (double)c[1] / c[0]);
+#endif
     return 0;
 }

@@ -46,7 +46,7 @@
 #include "nx_common.hpp"
 
 namespace nx {
-namespace dec {
+namespace decx {
 
 constexpr int kWaves = 12;        // waves per workgroup (2 workgroups per CU → 24 waves/CU)
 constexpr int kRing = 4096;       // decoded-output history per wave
@@ -98,6 +98,9 @@ __device__ __forceinline__ uint32_t raw8(const uint32_t* __restrict__ T, uint32_
     return c;
 }
 
+#ifdef NX_EXP_COUNT
+__device__ unsigned long long g_cnt[8];  // passes, rounds, pieces, far pieces, overlap pieces, batches
+#endif
 // Wave-uniform value → SGPR (values loaded by vector memory ops or shuffles are otherwise VGPRs and
 // every branch on them becomes exec-masked divergent code).
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -399,6 +402,23 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
         }
         uint64_t pending = __ballot(valid);
         uint64_t done = ~pending;
+#ifdef NX_EXP_COUNT
+        {
+            const uint64_t farm = __ballot(valid && gl && !lit), ovm = __ballot(valid && overlap);
+            int nr = 0;
+            for (uint64_t pd = pending, dn = done; pd; ++nr) {
+                const uint64_t rb = __ballot(((pd >> lane) & 1ull) != 0 && (need & ~dn) == 0ull);
+                pd &= ~rb; dn |= rb;
+            }
+            if (lane == 0) {
+                atomicAdd(&g_cnt[0], 1ull);
+                atomicAdd(&g_cnt[1], (unsigned long long)nr);
+                atomicAdd(&g_cnt[2], (unsigned long long)__popcll(pending));
+                atomicAdd(&g_cnt[3], (unsigned long long)__popcll(farm));
+                atomicAdd(&g_cnt[4], (unsigned long long)__popcll(ovm));
+            }
+        }
+#endif
         for (int round = 0; pending; ++round) {
             if (round > 64) return false;
             const bool ready = ((pending >> lane) & 1ull) != 0 && (need & ~done) == 0ull;
@@ -667,11 +687,17 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
 // waits once, then each lane parses tags until its window runs out.  One memory latency per ~20
 // tags instead of one per tag for whichever lane happens to cross a block.
 constexpr int kParseBlock = 256;
+#ifdef NX_EXP_WIN128
+constexpr int kWinDw = 33;
+constexpr uint32_t kWinB = 128;
+#else
 constexpr int kWinDw = 17;
+constexpr uint32_t kWinB = 64;
+#endif
 struct BurstWin {
     const uint8_t* origin;  // chunk start rounded down to 16 bytes
     uint32_t pad, end;      // chunk start - origin; chunk end, origin-relative
-    uint32_t base;          // window = origin-relative [base, base + 64)
+    uint32_t base;          // window = origin-relative [base, base + kWinB)
     uint32_t* w;            // this lane's LDS window
     __device__ __forceinline__ void init(const uint8_t* in, uint32_t length, uint32_t* lds) {
         origin = reinterpret_cast<const uint8_t*>((uintptr_t)in & ~(uintptr_t)15);
@@ -680,15 +706,23 @@ struct BurstWin {
         base = 0xFFFFFF00u;
         w = lds;
     }
-    // are the (up to) 5 header bytes at chunk position p in the window?
     __device__ __forceinline__ bool has(uint32_t p) const {
         const uint32_t q = p + pad;
-        return q >= base && (q + 5u <= base + 64u || base + 64u >= end);
+        return q >= base && (q + 5u <= base + kWinB || base + kWinB >= end);
     }
     __device__ __forceinline__ void load(uint32_t p) {
+#ifdef NX_EXP_WIN128
+        // whole lines: start at the line of q unless the header would cross the window end
+        const uint32_t q = p + pad;
+        const uint32_t origin_line = (uint32_t)((uintptr_t)origin & 127u);
+        uint32_t b = ((q + origin_line) & ~127u) - origin_line;  // origin-relative start of q's line
+        if ((int32_t)b < 0 || q + 5u > b + kWinB) b = q & ~15u;
+        base = b;
+#else
         base = (p + pad) & ~15u;
+#endif
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
+        for (uint32_t k = 0; k < kWinB / 16; ++k) {
             if (base + 16u * k < end) {
                 const uint4 x = *reinterpret_cast<const uint4*>(origin + base + 16u * k);
                 w[4 * k] = x.x;
@@ -698,7 +732,6 @@ struct BurstWin {
             }
         }
     }
-    // 8 bytes at chunk position p, has(p) (bytes at or past the chunk end are unspecified)
     __device__ __forceinline__ uint64_t get8(uint32_t p) const {
         const uint32_t off = p + pad - base;
         const uint32_t i = off >> 2, s = off & 3u;
@@ -707,6 +740,40 @@ struct BurstWin {
     }
 };
 
+#ifdef NX_EXP_REC64
+// Record writer: 16 records per 64-byte store
+struct RecWriter {
+    uint4* slot;
+    uint32_t n;
+    uint32_t q[16];
+    __device__ __forceinline__ bool put(uint32_t r) {
+        if (n >= kRecCap) return false;
+        const uint32_t k = n & 15u;
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) q[j] = k == j ? r : q[j];
+        if (k == 15) {
+            uint4* d = slot + (n >> 4) * 4;
+            d[0] = make_uint4(q[0], q[1], q[2], q[3]);
+            d[1] = make_uint4(q[4], q[5], q[6], q[7]);
+            d[2] = make_uint4(q[8], q[9], q[10], q[11]);
+            d[3] = make_uint4(q[12], q[13], q[14], q[15]);
+        }
+        ++n;
+        return true;
+    }
+    __device__ __forceinline__ void finish() {
+        const uint32_t k = n & 15u;
+        if (k) {
+            uint4* d = slot + (n >> 4) * 4;
+            d[0] = make_uint4(q[0], q[1], q[2], q[3]);
+            if (k > 4) d[1] = make_uint4(q[4], q[5], q[6], q[7]);
+            if (k > 8) d[2] = make_uint4(q[8], q[9], q[10], q[11]);
+            if (k > 12) d[3] = make_uint4(q[12], q[13], q[14], q[15]);
+        }
+    }
+};
+#define NX_RW_INIT(ptr) RecWriter rw{ptr, 0, {}}
+#else
 // Record writer: 4 records per 16-byte store into the frame's slot.
 struct RecWriter {
     uint4* slot;
@@ -727,6 +794,8 @@ struct RecWriter {
         if (n & 3u) slot[n >> 2] = make_uint4(q0, q1, q2, q3);
     }
 };
+#define NX_RW_INIT(ptr) RecWriter rw{ptr, 0, 0, 0, 0, 0}
+#endif
 
 __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ out_cap,
@@ -745,7 +814,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
     }
     BurstWin win;
     win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
-    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), 0, 0, 0, 0, 0};
+    NX_RW_INIT(reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap));
     uint32_t ip = 0, op = 0;
     int32_t st = NX_OK;
     bool run = false;
@@ -939,7 +1008,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lz4(const uint8_t* __rest
     }
     BurstWin win;
     win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
-    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), 0, 0, 0, 0, 0};
+    NX_RW_INIT(reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap));
     uint32_t ip = 0, op = 0;
     int32_t st = NX_OK;
     bool fit = true;
@@ -1091,7 +1160,7 @@ __global__ void __launch_bounds__(256) k_lz4_serial(const uint8_t* __restrict__ 
     status[c] = st;
 }
 
-}  // namespace dec
+}  // namespace decx
 }  // namespace nx
 
 namespace {
@@ -1112,7 +1181,7 @@ static hipError_t wave_kernel_attrs(size_t lds) {
     static std::once_flag once;
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [&] {
-        for (const void* k : {(const void*)nx::dec::k_decode_fused, (const void*)nx::dec::k_expand})
+        for (const void* k : {(const void*)nx::decx::k_decode_fused, (const void*)nx::decx::k_expand})
             if (attr_err == hipSuccess) attr_err = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     return attr_err;
@@ -1133,7 +1202,7 @@ static hipError_t dec_workspace(int dev, hipStream_t st, uint32_t sb, DecWorkspa
         W.rec = nullptr;
         W.nrec = nullptr;
         W.olen = nullptr;
-        NX_HIP_CHECK_E(hipMalloc(&W.rec, (size_t)sb * nx::dec::kRecCap * sizeof(uint32_t)));
+        NX_HIP_CHECK_E(hipMalloc(&W.rec, (size_t)sb * nx::decx::kRecCap * sizeof(uint32_t)));
         NX_HIP_CHECK_E(hipMalloc(&W.nrec, (size_t)sb * sizeof(uint32_t)));
         NX_HIP_CHECK_E(hipMalloc(&W.olen, (size_t)sb * sizeof(uint32_t)));
         W.frames = sb;
@@ -1146,7 +1215,7 @@ static hipError_t dec_workspace(int dev, hipStream_t st, uint32_t sb, DecWorkspa
 static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
                             const uint32_t* out_cap, uint32_t* out_len, uint32_t* consumed, int32_t* status,
                             const uint32_t* expected_masked_crc, uint32_t* crc_out, uint32_t n, void* stream, bool fused_only) {
-    using namespace nx::dec;
+    using namespace nx::decx;
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
     if (nx::crc_tables_init() != NX_OK) return NX_ERR_HIP;
@@ -1195,7 +1264,7 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
     return NX_OK;
 }
 
-extern "C" int32_t nx_snappy_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+extern "C" int32_t xexp_nx_snappy_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                           const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len,
                                           uint32_t* consumed, int32_t* status, const uint32_t* expected_masked_crc,
                                           uint32_t* crc_out, uint32_t n, void* stream) {
@@ -1203,7 +1272,7 @@ extern "C" int32_t nx_snappy_decode_batch(const uint8_t* in, const uint64_t* in_
                         false);
 }
 
-extern "C" int32_t nx_snappy_decode_batch_fused(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+extern "C" int32_t xexp_nx_snappy_decode_batch_fused(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                                 const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len,
                                                 uint32_t* consumed, int32_t* status, const uint32_t* expected_masked_crc,
                                                 uint32_t* crc_out, uint32_t n, void* stream) {
@@ -1214,10 +1283,10 @@ extern "C" int32_t nx_snappy_decode_batch_fused(const uint8_t* in, const uint64_
 // Replaces LZ4FastDecompressor.decompress as Lz4FrameDecoder.decode calls it for one
 // BLOCK_TYPE_COMPRESSED block (Lz4FrameDecoder.java:199-208): block i = in[in_off[i] .. +in_len[i])
 // must decode to exactly out_len[i] bytes at out + out_off[i].
-extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+extern "C" int32_t xexp_nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                        const uint64_t* out_off, const uint32_t* out_len, int32_t* status, uint32_t n,
                                        void* stream) {
-    using namespace nx::dec;
+    using namespace nx::decx;
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
     if (nx::crc_tables_init() != NX_OK) return NX_ERR_HIP;

@@ -1,0 +1,424 @@
+// snappy_encode.hip — Snappy block encoder, bit-exact with Netty's Snappy.encode (Snappy.java:82-313).
+//
+// Netty's greedy matcher is a serial state machine whose output depends on the exact probe order
+// (the `skip++ >> 5` heuristic, :107-115) and on an evolving 16384-entry hash table (:97-100,
+// 126-128, 148-152).  There is no safe intra-chunk speculation, so each chunk is one lane's serial
+// state machine and the parallelism is the thousands of independent chunks of a batch (16 waves
+// per CU → 262 144 chunks in flight on 256 CUs).  What the kernel optimises is the memory side of
+// each lane's dependency chain:
+//   * every 4-byte window is one unaligned dword load (Java's big-endian getInt = bswap), and the
+//     bytes at the probe position are reused from the hash computation that loaded them;
+//   * the next probe's table load is issued before the current candidate compare resolves
+//     (a same-hash collision is forwarded in registers), so a probe costs one memory round trip;
+//   * match extension compares 4 bytes per step and finds the first mismatch with ctz;
+//   * output bytes are packed into dwords and written with aligned 4-byte stores; literal runs
+//     are copied 4 bytes at a time with a funnel shift.
+// Hash table: Java allocates a zeroed short[min(nextPow2(len),16384)] per call (:97-99,191).
+// Each resident lane owns a 16384-entry uint32 slot in a device workspace; an entry is
+//   stamp[31:28] | check[27:16] | position[15:0]
+// A stamp mismatch reads as position 0 — exactly a freshly zeroed table, without a clear per
+// chunk.  `check` is 12 bits folded from the 4 bytes at `position`: when it differs from the
+// probe word's fold, getInt(ip) != getInt(candidate) is already decided and the random read of
+// the candidate bytes is skipped (most probes of a literal run end this way).  The candidate
+// position — and with it the emitted stream — is unchanged; only the memory traffic drops.
+#include <stdlib.h>
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include "nx_common.hpp"
+
+namespace nx {
+namespace encx {
+
+typedef uint32_t __attribute__((aligned(1))) u32u;
+
+typedef uint64_t __attribute__((aligned(1))) u64u;
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const u32u*>(p); }  // LE, unaligned
+__device__ __forceinline__ uint64_t ld64(const uint8_t* p) { return *reinterpret_cast<const u64u*>(p); }
+__device__ __forceinline__ uint32_t hash_of(uint32_t le, int shift) {
+    return (__builtin_bswap32(le) * 0x1e35a7bdu) >> shift;  // hash (:177-179) on the BIG-endian getInt
+}
+
+// Output writer: bytes are packed into `acc` and leave as aligned dword stores; with PAIR (8-byte
+// aligned destination) two dwords leave as one 8-byte store.
+template <bool PAIR>
+struct WriterT {
+    uint32_t* w;   // next aligned dword to store
+    uint32_t acc;  // pending bytes (little-endian order)
+    uint32_t na;   // number of pending bytes (0..3)
+    uint32_t nw;   // dwords stored
+    uint32_t s0;   // PAIR: the staged even dword
+    __device__ __forceinline__ void emit(uint32_t v) {
+        if (!PAIR) {
+            w[nw] = v;
+        } else if (nw & 1u) {
+            *reinterpret_cast<uint2*>(w + nw - 1u) = make_uint2(s0, v);
+        } else {
+            s0 = v;
+        }
+        ++nw;
+    }
+    __device__ __forceinline__ void put(uint32_t b) {
+        acc |= b << (8 * na);
+        if (++na == 4) {
+            emit(acc);
+            acc = 0;
+            na = 0;
+        }
+    }
+    // append `n` bytes starting at p (unaligned source)
+    __device__ __forceinline__ void copy(const uint8_t* p, int32_t n) {
+        while (n >= 4) {
+            const uint32_t v = ld32(p);
+            if (na == 0) {
+                emit(v);
+            } else {
+                emit(acc | (v << (8 * na)));
+                acc = v >> (32 - 8 * na);
+            }
+            p += 4;
+            n -= 4;
+        }
+        while (n-- > 0) put(*p++);
+    }
+    __device__ __forceinline__ uint32_t pos() const { return nw * 4 + na; }
+    __device__ __forceinline__ void finish() {
+        if (PAIR && (nw & 1u)) w[nw - 1u] = s0;
+        uint8_t* t = reinterpret_cast<uint8_t*>(w + nw);
+        for (uint32_t i = 0; i < na; ++i) t[i] = (uint8_t)(acc >> (8 * i));
+    }
+};
+
+// Byte-store writer for unaligned destinations (same interface).
+struct ByteWriter {
+    uint8_t* o;
+    uint32_t n;
+    __device__ __forceinline__ void put(uint32_t b) { o[n++] = (uint8_t)b; }
+    __device__ __forceinline__ void copy(const uint8_t* p, int32_t k) {
+        for (int32_t i = 0; i < k; ++i) o[n + i] = p[i];
+        n += (uint32_t)k;
+    }
+    __device__ __forceinline__ uint32_t pos() const { return n; }
+    __device__ __forceinline__ void finish() {}
+};
+
+template <class Wr>
+__device__ __forceinline__ void enc_literal(const uint8_t* in, Wr& w, int32_t length) {
+    // encodeLiteral (:268-281)
+    if (length < 61) {
+        w.put((uint32_t)((length - 1) << 2));
+    } else {
+        const int32_t v = length - 1;
+        const int bitLength = 31 - __clz((uint32_t)v);  // bitsToEncode (:249-257), v >= 60
+        const int bytesToEncode = 1 + bitLength / 8;
+        w.put((uint32_t)((59 + bytesToEncode) << 2));
+        for (int i = 0; i < bytesToEncode; i++) w.put((uint32_t)((v >> (i * 8)) & 0xff));
+    }
+    w.copy(in, length);
+}
+
+template <class Wr>
+__device__ __forceinline__ void enc_copy_off(Wr& w, int32_t offset, int32_t length) {
+    // encodeCopyWithOffset (:283-292)
+    if (length < 12 && offset < 2048) {
+        w.put((uint32_t)(1 | ((length - 4) << 2) | ((offset >> 8) << 5)));
+        w.put((uint32_t)(offset & 0xff));
+    } else {
+        w.put((uint32_t)(2 | ((length - 1) << 2)));
+        w.put((uint32_t)(offset & 0xff));
+        w.put((uint32_t)((offset >> 8) & 0xff));
+    }
+}
+
+template <class Wr>
+__device__ __forceinline__ void enc_copy(Wr& w, int32_t offset, int32_t length) {
+    // encodeCopy (:301-313)
+    while (length >= 68) {
+        enc_copy_off(w, offset, 64);
+        length -= 64;
+    }
+    if (length > 64) {
+        enc_copy_off(w, offset, 60);
+        length -= 60;
+    }
+    enc_copy_off(w, offset, length);
+}
+
+// Register window over the lane's own input stream: 32 bytes from a 16-byte-aligned address.
+// The scan front moves 1-2 bytes per probe, so one refill (two 16-byte loads) serves the next
+// 10-25 stream reads that would otherwise each be a separate memory request; with 262 144 lanes
+// streaming at once, L2 cannot keep a lane's current line between its probes.  Dword i of the
+// window is picked by a 3-level select tree (dynamic register indexing would spill to scratch).
+// A 16-byte block that holds at least one byte of the chunk never crosses a page, so the loads
+// stay inside mapped memory; a second block wholly past the end is not loaded.
+struct StreamWin {
+    const uint8_t* origin;  // chunk start rounded down to 16 bytes
+    uint32_t pad;           // chunk start - origin
+    uint32_t end;           // chunk end, origin-relative
+    uint32_t wb;            // window base, origin-relative, multiple of 16
+    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
+    __device__ __forceinline__ void init(const uint8_t* in, int32_t length) {
+        origin = reinterpret_cast<const uint8_t*>((uintptr_t)in & ~(uintptr_t)15);
+        pad = (uint32_t)((uintptr_t)in & 15u);
+        end = pad + (uint32_t)length;
+        wb = 0x80000000u;  // empty: q - wb > 27 for every position
+    }
+    __device__ __forceinline__ static uint32_t sel(uint32_t i, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4,
+                                                   uint32_t a5, uint32_t a6, uint32_t a7) {
+        const bool b0 = i & 1u, b1 = i & 2u, b2 = i & 4u;
+        const uint32_t c0 = b0 ? a1 : a0, c1 = b0 ? a3 : a2, c2 = b0 ? a5 : a4, c3 = b0 ? a7 : a6;
+        const uint32_t d0 = b1 ? c1 : c0, d1 = b1 ? c3 : c2;
+        return b2 ? d1 : d0;
+    }
+    // the 4 bytes at chunk position p (p + 4 <= length), little-endian
+    __device__ __forceinline__ uint32_t get(int32_t p) {
+        const uint32_t q = (uint32_t)p + pad;
+        uint32_t off = q - wb;
+        if (off > 27u) {
+            if (off < 44u) {
+                // forward by less than 16 bytes past the window: slide it one block, keeping the
+                // upper block, so each input block is loaded once on a forward scan
+                wb += 16u;
+                w0 = w4; w1 = w5; w2 = w6; w3 = w7;
+                if (wb + 16u < end) {
+                    const uint4 y = *reinterpret_cast<const uint4*>(origin + wb + 16u);
+                    w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
+                }
+            } else {
+                wb = q & ~15u;
+                const uint4 x = *reinterpret_cast<const uint4*>(origin + wb);
+                w0 = x.x; w1 = x.y; w2 = x.z; w3 = x.w;
+                if (wb + 16u < end) {
+                    const uint4 y = *reinterpret_cast<const uint4*>(origin + wb + 16u);
+                    w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
+                }
+            }
+            off = q - wb;
+        }
+        const uint32_t i = off >> 2;
+        const uint32_t lo = sel(i, w0, w1, w2, w3, w4, w5, w6, w7);
+        const uint32_t hi = sel(i + 1u, w0, w1, w2, w3, w4, w5, w6, w7);
+        return __builtin_amdgcn_alignbyte(hi, lo, off & 3u);
+    }
+};
+
+// The 8 bytes at chunk position c, or its 4 when fewer than 8 remain: the candidate compare and the
+// first step of the match extension share one memory request.
+__device__ __forceinline__ uint64_t ld_cand(const uint8_t* in, int32_t c, int32_t length) {
+    return c + 8 <= length ? ld64(in + c) : (uint64_t)ld32(in + c);
+}
+
+// 4 + findMatchingLength(in, candidate + 4, inIndex + 4, length)  (:224-239): the common-prefix
+// length bounded by the bytes left, computed 4 bytes per step (the inIndex side from the window).
+// `first` = the 4 bytes at a, already read with the candidate compare; b <= length - 4 implies
+// a + 4 <= length (a < b), which is when ld_cand read them.
+__device__ __forceinline__ int32_t match_len(const uint8_t* in, StreamWin& win, int32_t a, int32_t b, int32_t length,
+                                             uint32_t first) {
+    int32_t m = 0;
+    if (b <= length - 4) {
+        const uint32_t x0 = first ^ win.get(b);
+        if (x0) return (int32_t)(__builtin_ctz(x0) >> 3);
+        m = 4;
+        while (b + m <= length - 4) {
+            const uint32_t x = ld32(in + a + m) ^ win.get(b + m);
+            if (x) return m + (int32_t)(__builtin_ctz(x) >> 3);
+            m += 4;
+        }
+    }
+    while (b + m < length && in[a + m] == in[b + m]) ++m;
+    return m;
+}
+
+template <bool SWAP, class Wr>
+__device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length, Wr& w, uint32_t* __restrict__ table, uint32_t stamp) {
+    for (int i = 0;; i++) {  // preamble (:84-92)
+        const uint32_t b = (uint32_t)length >> (i * 7);
+        if ((b & 0xFFFFFF80u) != 0) {
+            w.put((b & 0x7f) | 0x80);
+        } else {
+            w.put(b);
+            break;
+        }
+    }
+    uint32_t hts = length <= 1 ? 1u : (1u << (32 - __clz((uint32_t)(length - 1))));
+    if (hts > 16384u) hts = 16384u;
+    const int shift = __clz(hts) + 1;
+    const uint32_t stag = stamp << 28;
+    const uint32_t word0 = length >= 4 ? ld32(in) : 0u;  // getInt(base + 0): an empty slot's candidate
+#define TST(ptr, v) (*(ptr) = (v))
+    // read-and-insert of one table slot: a single atomic swap (one memory request instead of a
+    // load and a store; same-address order keeps Java's read-then-write semantics)
+#define XCH(ptr, v) (SWAP ? __hip_atomic_exchange((ptr), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) \
+                          : ({ const uint32_t o_ = *(ptr); *(ptr) = (v); o_; }))
+#define CHK(wd) (((wd) ^ ((wd) >> 12) ^ ((wd) >> 24)) & 0xFFFu)
+#define MK(pos, wd) (stag | (CHK(wd) << 16) | (uint32_t)(pos))
+#define LIVE(e) (((e) & 0xF0000000u) == stag)
+#define TBL_DEC(e) (LIVE(e) ? (int32_t)((e) & 0xFFFFu) : 0)
+    // may getInt(ip) == getInt(candidate)?  false is exact, true needs the candidate bytes
+#define MAYBE(e, wd) (LIVE(e) ? ((((e) >> 16) & 0xFFFu) == CHK(wd)) : ((wd) == word0))
+    int32_t nextEmit = 0;
+    if (length >= 15) {  // MIN_COMPRESSIBLE_BYTES (:34,104)
+        StreamWin win;
+        win.init(in, length);
+        int32_t inIndex = 1;
+        uint32_t nextWord = win.get(1);
+        uint32_t nextHash = hash_of(nextWord, shift);
+        for (;;) {  // outer: (:106)
+            int32_t skip = 32;
+            int32_t nextIndex = inIndex;
+            int32_t candidate;
+            uint32_t curWord;
+            uint64_t cand8;  // the 8 bytes at candidate (4 near the chunk end), read once per compare
+            // ---- probe run (:107-130), in Java's order: each probe's swap waits for the previous
+            // compare (a speculative next swap, undone on a match, cost 7 % more time in requests);
+            // only the next position's bytes and hash are computed ahead
+            uint32_t entry;
+            do {
+                inIndex = nextIndex;
+                const uint32_t hash = nextHash;
+                curWord = nextWord;
+                nextIndex = inIndex + (skip++ >> 5);
+                if (nextIndex > length - 4) goto done;
+                nextWord = win.get(nextIndex);
+                nextHash = hash_of(nextWord, shift);
+                entry = XCH(table + hash, MK(inIndex, curWord));
+                candidate = TBL_DEC(entry);
+            } while (!(MAYBE(entry, curWord) && curWord == (uint32_t)(cand8 = ld_cand(in, candidate, length))));
+
+            enc_literal(in + nextEmit, w, inIndex - nextEmit);  // (:132)
+
+            int32_t insertTail;
+            for (;;) {  // (:135-154)
+                const int32_t base = inIndex;
+                const int32_t matched = 4 + match_len(in, win, candidate + 4, inIndex + 4, length, (uint32_t)(cand8 >> 32));
+                inIndex += matched;
+                enc_copy(w, base - candidate, matched);
+                insertTail = inIndex - 1;
+                nextEmit = inIndex;
+                if (inIndex >= length - 4) goto done;
+                const uint32_t wTail = win.get(insertTail);
+                const uint32_t wCur = win.get(inIndex);
+                const uint32_t prevHash = hash_of(wTail, shift);
+                TST(table + prevHash, MK(inIndex - 1, wTail));
+                const uint32_t currentHash = hash_of(wCur, shift);
+                const uint32_t e = XCH(table + currentHash, MK(inIndex, wCur));
+                candidate = TBL_DEC(e);
+                if (!MAYBE(e, wCur) || wCur != (uint32_t)(cand8 = ld_cand(in, candidate, length))) break;
+            }
+            nextWord = win.get(insertTail + 2);
+            nextHash = hash_of(nextWord, shift);  // (:156)
+            ++inIndex;
+        }
+    }
+done:
+#undef TBL_DEC
+#undef MAYBE
+#undef LIVE
+#undef MK
+#undef CHK
+#undef XCH
+#undef TST
+    if (nextEmit < length) enc_literal(in + nextEmit, w, length - nextEmit);  // (:162-164)
+    w.finish();
+    return w.pos();
+}
+
+template <bool SWAP>
+#ifndef NX_ENC_PAIR
+#define NX_ENC_PAIR 1
+#endif
+#ifndef NX_ENC_MINBLK
+#define NX_ENC_MINBLK 6
+#endif
+__global__ void __launch_bounds__(256, NX_ENC_MINBLK) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                       const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                       const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
+                                                       int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
+                                                       uint32_t stamp_base) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    uint32_t* table = workspace + (size_t)tid * 16384u;
+    uint32_t iter = 0;
+    for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
+        const uint32_t len = in_len[c];
+        if (len > 65536u) {
+            status[c] = NX_ERR_INVALID_ARG;
+            out_len[c] = 0;
+            continue;
+        }
+        const uint32_t stamp = stamp_base + iter + 1u;  // 1..15, host re-zeroes the workspace before wrap
+        uint8_t* o = out + out_off[c];
+        uint32_t olen;
+        const uint8_t* src = in + in_off[c];
+        if ((((uintptr_t)o) & 7u) == 0 && NX_ENC_PAIR) {
+            WriterT<true> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
+            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
+        } else if ((((uintptr_t)o) & 3u) == 0) {
+            WriterT<false> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
+            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
+        } else {
+            ByteWriter w{o, 0};
+            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
+        }
+        out_len[c] = olen;
+        status[c] = NX_OK;
+    }
+}
+
+}  // namespace encx
+}  // namespace nx
+
+namespace {
+// Encoder hash-table workspace, one per (device, stream): launches on one stream are ordered, so
+// they may share a workspace; launches on different streams may overlap and must not.
+struct Workspace {
+    uint32_t* ws = nullptr;
+    size_t threads = 0;
+    uint32_t stamp = 0;  // last stamp used; entries carry 4-bit stamps 1..15
+};
+std::mutex g_ws_mu;
+std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
+constexpr unsigned kEncBlock = 256;
+constexpr unsigned kEncWavesPerCU = 16;
+constexpr uint32_t kMaxStamp = 15;
+}  // namespace
+
+extern "C" int32_t xexp_nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                          const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream) {
+    if (n == 0) return NX_OK;
+    if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
+    int dev = 0, cus = 256;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    constexpr unsigned waves_per_cu = kEncWavesPerCU;
+    const hipStream_t st = (hipStream_t)stream;
+    const size_t want = (size_t)cus * waves_per_cu * 64;
+    const size_t threads = n < want ? ((n + kEncBlock - 1) / kEncBlock) * kEncBlock : want;
+    const size_t per = 16384u * sizeof(uint32_t);
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    Workspace& W = g_ws[{dev, st}];
+    if (W.ws == nullptr || W.threads < threads) {
+        if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
+        W.ws = nullptr;
+        NX_HIP_CHECK(hipMalloc(&W.ws, threads * per));
+        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, threads * per, st));
+        W.threads = threads;
+        W.stamp = 0;
+    }
+    // Each launch gives a resident lane at most kMaxStamp - 1 chunks (one stamp each).
+    const size_t per_launch = threads * (kMaxStamp - 1);
+    for (size_t base = 0; base < n; base += per_launch) {
+        const uint32_t m = (uint32_t)std::min<size_t>(per_launch, n - base);
+        const uint32_t iters = (uint32_t)((m + threads - 1) / threads);
+        if (W.stamp + iters >= kMaxStamp) {
+            NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.threads * per, st));
+            W.stamp = 0;
+        }
+        hipLaunchKernelGGL(nx::encx::k_snappy_encode<NX_EXP_SWAP>, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
+                           in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp);
+        NX_HIP_CHECK(hipGetLastError());
+        W.stamp += iters;
+    }
+    return NX_OK;
+}
