@@ -248,7 +248,8 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t length,
     const uint32_t word0 = length >= 4 ? ld32(in) : 0u;  // getInt(base + 0): an empty slot's candidate
 #define TST(ptr, v) (*(ptr) = (v))
     // read-and-insert of one table slot: a single atomic swap (one memory request instead of a
-    // load and a store; same-address order keeps Java's read-then-write semantics)
+    // load and a store; same-address order keeps Java's read-then-write semantics).  SWAP = false,
+    // load then store, is only instantiated by scripts/experiments/enc_var.cpp (8 % slower).
 #define XCH(ptr, v) (SWAP ? __hip_atomic_exchange((ptr), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) \
                           : ({ const uint32_t o_ = *(ptr); *(ptr) = (v); o_; }))
 #define CHK(wd) (((wd) ^ ((wd) >> 12) ^ ((wd) >> 24)) & 0xFFFu)
@@ -324,14 +325,10 @@ done:
     return w.pos();
 }
 
+// Launch bound 6 blocks of 256 per CU keeps the kernel under 80 VGPRs (no spills) at the 16 waves/CU
+// the host launches.
 template <bool SWAP>
-#ifndef NX_ENC_PAIR
-#define NX_ENC_PAIR 1
-#endif
-#ifndef NX_ENC_MINBLK
-#define NX_ENC_MINBLK 6
-#endif
-__global__ void __launch_bounds__(256, NX_ENC_MINBLK) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+__global__ void __launch_bounds__(256, 6) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                        const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
                                                        int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
@@ -351,7 +348,7 @@ __global__ void __launch_bounds__(256, NX_ENC_MINBLK) k_snappy_encode(const uint
         uint8_t* o = out + out_off[c];
         uint32_t olen;
         const uint8_t* src = in + in_off[c];
-        if ((((uintptr_t)o) & 7u) == 0 && NX_ENC_PAIR) {
+        if ((((uintptr_t)o) & 7u) == 0) {
             WriterT<true> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
             olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
         } else if ((((uintptr_t)o) & 3u) == 0) {

@@ -40,7 +40,12 @@ int main(int argc, char** argv) {
     hipDeviceSynchronize();
     if (nx::crc_tables_init() != NX_OK) return 2;
     const size_t lds = kTabBytes + kWaves * sizeof(WaveLds);
-    hipFuncSetAttribute((const void*)k_expand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+#ifdef NX_EXP_R8
+#define K_EXPAND k_expand8
+#else
+#define K_EXPAND k_expand
+#endif
+    hipFuncSetAttribute((const void*)K_EXPAND, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     int cus = 256;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const unsigned bpc = (unsigned)(160 * 1024 / lds);
@@ -55,7 +60,7 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(k_parse, dim3((N + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, 0, denc, ooff, olen, nullptr, rec,
                            nrec, dlen, nullptr, st, (uint32_t)N);
         hipEventRecord(e1);
-        hipLaunchKernelGGL(k_expand, dim3(eg), dim3(kWaves * 64), lds, 0, denc, ooff, olen, ddec, ioff, rec, nrec, dlen, st,
+        hipLaunchKernelGGL(K_EXPAND, dim3(eg), dim3(kWaves * 64), lds, 0, denc, ooff, olen, ddec, ioff, rec, nrec, dlen, st,
                            crc ? crcs : nullptr, nullptr, (uint32_t)N, nx::crc_tables_dev());
         hipEventRecord(e2);
         hipEventSynchronize(e2);

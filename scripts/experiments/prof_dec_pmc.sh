@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); EXP=$ROOT/scripts/experiments; OUT=$ROOT/gpurun_out/decprof; mkdir -p "$OUT"; export TMPDIR=/tmp
 N=${N:-65536}; BIN=${BIN:-dec_bench_base}
 cd /tmp
-timeout -k 10 120 "$EXP/dec_bench_count" "$N" 1 1 > "$OUT/count.log" 2>&1 || exit 1
+timeout -k 10 120 "$EXP/${CBIN:-dec_bench_count}" "$N" 1 1 > "$OUT/count.log" 2>&1 || exit 1
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- "$EXP/$BIN" "$N" 2 1 > "$OUT/kt.log" 2>&1 || exit 1
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \

@@ -885,6 +885,16 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
                 run = false;
                 continue;
             }
+#ifdef NX_EXP_R8
+            bool fit = true;
+            if (isl) {  // a zero-length literal (field 0xFFFFFFFF) emits nothing
+                for (uint32_t k = 0; k < lj && fit; k += 8u) fit = rw.put(((min(8u, lj - k) - 1u) << 25) | (dpos + k));
+            } else {
+                for (uint32_t k = 0; k < clen && fit; k += 8u)
+                    fit = rw.put(0x80000000u | ((min(8u, clen - k) - 1u) << 25) |
+                                 (coff < 8u ? 0x10000000u | (((k >> 3) & 7u) << 8) | coff : coff));
+            }
+#else
             const uint32_t m0 = lj < 64u ? lj : 64u;
             const uint32_t r = isl ? (((m0 - 1u) << 25) | dpos) : (0x80000000u | ((clen - 1u) << 25) | coff);
             bool fit = (isl && lj == 0u) || rw.put(r);  // a zero-length literal (field 0xFFFFFFFF) emits nothing
@@ -894,6 +904,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
                     fit = rw.put(((m - 1u) << 25) | (dpos + k));
                 }
             }
+#endif
             if (!fit) {
                 st = kNeedFused;
                 run = false;
@@ -975,6 +986,220 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
     }
 }
 
+
+#ifdef NX_EXP_R8
+// =====================================================================================
+// k_expand8: one wave per frame, one <= 8-byte record per lane per pass
+// =====================================================================================
+// Records (k_parse / k_parse_lz4 split every literal and copy at 8 bytes): bit 31 copy | bit 28
+// periodic | bits 27..25 length-1 | bits 24..0 literal input position or copy offset d; a copy with
+// d < 8 is "periodic" and carries in bits 10..8 its index k' within its 64-byte group, whose bytes repeat the d bytes before the group start
+// T' = start - 8k' (out[T'+j] = out[T'-d + (j mod d)]), so it depends on bytes before T' only.
+//
+// A pass = 64 consecutive records = output [O, E), E - O <= 512.  Each lane fetches its record's 8
+// source bytes (literal: the input stage or HBM; copy: the ring, or HBM when it reaches more than
+// 4 KiB back: flushed and drained) and writes its 1-8 bytes into the ring with up to three masked
+// dword ORs.  A copy whose source bytes are produced in the same pass waits for the lanes producing
+// them (a per-pass byte -> lane map gives the range); rounds repeat until every lane is done.
+__global__ void __launch_bounds__(kWaves * 64, 6)
+    k_expand8(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
+              uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ rec,
+              const uint32_t* __restrict__ nrec, uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
+              const uint32_t* __restrict__ expect, uint32_t* __restrict__ crc_out, uint32_t n, const CrcTables* __restrict__ tabs) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const bool do_crc = (expect != nullptr) || (crc_out != nullptr);
+    const WaveSetup s = wave_setup(smem, tabs, do_crc);
+    const int lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * kWaves;
+    WaveLds& L = *s.L;
+    const uint32_t* lds32 = L.ring;  // ring at dwords [0, 1024), stage at [1024, 1280)
+    const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);
+    // byte -> producing-lane map of the pass: 516 bytes over tagw + scratch
+    const uint32_t map_base = s.lds_base + (uint32_t)offsetof(WaveLds, tagw);
+    const uint8_t* map8 = reinterpret_cast<const uint8_t*>(L.tagw);
+    for (uint32_t c = blockIdx.x * kWaves + s.wave; c < n; c += nw) {
+        int32_t st = (int32_t)uni((uint32_t)status[c]);
+        if (st == kNeedFused) continue;
+        const uint32_t N = uni(nrec[c]);
+        Frame f{in + in_off[c], in_len[c], out + out_off[c], 0u};
+        FrameIO io(L, f, s.sT, s.sSH, do_crc, lane);
+        const uint32_t* __restrict__ R = rec + (size_t)c * kRecCap;
+        uint32_t O = 0;
+        bool primed = false;
+        uint32_t rnext = (uint32_t)lane < N ? R[lane] : 0u;
+        for (uint32_t b = 0; b < N; b += 64u) {
+            const uint32_t r = rnext;
+            rnext = b + 64u + (uint32_t)lane < N ? R[b + 64u + lane] : 0u;
+            const bool valid = b + (uint32_t)lane < N;
+            const bool isc = valid && (r >> 31) != 0u;
+            const uint32_t len = valid ? ((r >> 25) & 7u) + 1u : 0u;
+            const uint32_t x = r & 0x1FFFFFFu;
+            const uint32_t incl = incl_scan(len);
+            const uint32_t os = O + incl - len;
+            const uint32_t E = O + uni((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
+            const uint64_t litm = __ballot(valid && !isc);
+            if (litm) {
+                const uint32_t w = uni((uint32_t)__builtin_amdgcn_readlane((int)x, __ffsll((long long)litm) - 1));
+                if (!primed) {
+                    io.prime(w + io.a);
+                    primed = true;
+                } else {
+                    io.advance(w + io.a);
+                }
+            }
+            io.flush_to(O);  // ring slots of [O, E) alias [O - 4096, E - 4096): flushed
+            // ---- this lane's source
+            const bool ovl = isc && ((r >> 28) & 1u) != 0u;  // periodic copy (d < 8): source = the d bytes before T'
+            const uint32_t d = ovl ? x & 7u : x;              // copy offset
+            const uint32_t T = ovl ? os - 8u * ((x >> 8) & 7u) : os;
+            const uint32_t sp = isc ? T - d : x;              // copy: output position; literal: input position
+            const bool far = isc && !ovl && E > (uint32_t)kRing && sp < E - (uint32_t)kRing;
+            const bool lit = valid && !isc;
+            const uint32_t stp = x + io.a;                    // literal: stage coordinate
+            const bool lit_g = lit && (stp - io.sbase) > (uint32_t)(kStage - 12);
+            uint32_t v0 = 0, v1 = 0;                          // the 8 source bytes (fixed sources)
+            wave_sync();  // stage writes of prime/advance; the previous pass's map reads
+            if (lit && !lit_g) {
+                const uint32_t w = stp >> 2, sh = stp & 3u;
+                const uint32_t a0 = lds32[kRing / 4 + (w & (kStage / 4 - 1))];
+                const uint32_t a1 = lds32[kRing / 4 + ((w + 1u) & (kStage / 4 - 1))];
+                const uint32_t a2 = lds32[kRing / 4 + ((w + 2u) & (kStage / 4 - 1))];
+                v0 = __builtin_amdgcn_alignbyte(a1, a0, sh);
+                v1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
+            }
+            if (__ballot(lit_g || far)) {
+                if (lit_g) {
+                    if (x + 8u <= io.in_len) {
+                        v0 = g_ld32u(io.src + x);
+                        v1 = g_ld32u(io.src + x + 4u);
+                    } else {
+#pragma unroll
+                        for (uint32_t i = 0; i < 8; ++i)
+                            if (x + i < io.in_len) (i < 4 ? v0 : v1) |= g_ld8(io.src + x + i) << (8 * (i & 3u));
+                    }
+                } else if (far) {
+                    v0 = g_ld32u(io.dst + sp);  // flushed and drained output of this frame (sp + 8 <= os)
+                    v1 = g_ld32u(io.dst + sp + 4u);
+                }
+            }
+            // periodic copies: output byte i = period[(8k' + i) mod d], as v_perm selectors
+            uint32_t sel0 = 0x03020100u, sel1 = 0x07060504u;
+            const bool any_ovl = __ballot(ovl) != 0ull;
+            if (any_ovl && ovl) {
+                uint32_t m = (8u * ((x >> 8) & 7u)) % d;
+                uint32_t sl[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    sl[i] = m;
+                    m = m + 1u == d ? 0u : m + 1u;
+                }
+                sel0 = sl[0] | (sl[1] << 8) | (sl[2] << 16) | (sl[3] << 24);
+                sel1 = sl[4] | (sl[5] << 8) | (sl[6] << 16) | (sl[7] << 24);
+            }
+            // ---- destination: bytes [os, os + len) = ring dwords q, q+1, q+2 at byte offset o
+            const uint32_t o = os & 3u;
+            const uint32_t q = os >> 2;
+            uint32_t dm[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int lo = max((int)o - 4 * k, 0), hi = min((int)(o + len) - 4 * k, 4);
+                dm[k] = hi > lo ? ((0xFFFFFFFFu >> (32 - 8 * (hi - lo))) << (8 * lo)) : 0u;
+            }
+            // ---- producer map of [O, E) (by byte offset from O & ~3), then this lane's dependencies
+            const uint32_t Oal = O & ~3u;
+            {
+                const uint32_t mq = (os - Oal) >> 2;
+                const uint32_t lv = (uint32_t)lane * 0x01010101u;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const uint32_t mm = dm[k];
+                    const uint32_t ad = map_base + 4u * (mm ? mq + (uint32_t)k : 0u);
+                    asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(ad), "v"(mm), "v"(lv & mm) : "memory");
+                }
+            }
+#ifndef NX_EXP_NOSYNC2
+            wave_sync();
+#endif
+            uint64_t need = 0;
+            if (isc && !far) {
+                const uint32_t lo0 = ovl ? T - d : sp;
+                const uint32_t hi = ovl ? T : sp + len;
+                if (hi > O) {
+                    const uint32_t lo = lo0 > O ? lo0 : O;
+                    const uint32_t pa = map8[lo - Oal], pb = map8[hi - 1u - Oal];
+                    need = (pb >= 63u ? ~0ull : ((2ull << pb) - 1ull)) & ~((1ull << (pa & 63u)) - 1ull);
+                }
+            }
+            const uint32_t rw0 = s.lds_base + 4u * (q & (kRing / 4 - 1));
+            const uint32_t rw1 = s.lds_base + 4u * ((q + 1u) & (kRing / 4 - 1));
+            const uint32_t rw2 = s.lds_base + 4u * ((q + 2u) & (kRing / 4 - 1));
+            const bool near = isc && !far;
+            const uint32_t rsp = sp & (kRing - 1);
+            uint64_t pending = __ballot(valid);
+            uint64_t done = ~pending;
+            for (int round = 0; pending; ++round) {
+                if (round > 64) {
+                    st = kGuardTrip + 3;
+                    break;
+                }
+                const bool ready = ((pending >> lane) & 1ull) != 0 && (need & ~done) == 0ull;
+                uint32_t a = v0, bb = v1;
+                if (near) {  // ring bytes [sp, sp + 8)
+                    const uint32_t w = rsp >> 2, sh = rsp & 3u;
+                    const uint32_t a0 = lds32[w], a1 = lds32[(w + 1u) & (kRing / 4 - 1)], a2 = lds32[(w + 2u) & (kRing / 4 - 1)];
+                    a = __builtin_amdgcn_alignbyte(a1, a0, sh);
+                    bb = __builtin_amdgcn_alignbyte(a2, a1, sh);
+                }
+                if (any_ovl && ovl) {
+                    const uint32_t p0 = __builtin_amdgcn_perm(bb, a, sel0), p1 = __builtin_amdgcn_perm(bb, a, sel1);
+                    a = p0;
+                    bb = p1;
+                }
+                // the 8 bytes shifted to output byte offset o: dwords (a<<8o), (bb:a >> 8(4-o)), (bb >> 8(4-o))
+                const uint32_t w0 = a << (8u * o);
+                const uint32_t w1 = o ? __builtin_amdgcn_alignbyte(bb, a, 4u - o) : bb;
+                const uint32_t w2 = o ? bb >> (8u * (4u - o)) : 0u;
+                const uint32_t m0 = ready ? dm[0] : 0u, m1 = ready ? dm[1] : 0u, m2 = ready ? dm[2] : 0u;
+                asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(rw0), "v"(m0), "v"(w0 & m0) : "memory");
+                asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(rw1), "v"(m1), "v"(w1 & m1) : "memory");
+                asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(rw2), "v"(m2), "v"(w2 & m2) : "memory");
+                const uint64_t rb = __ballot(ready);
+                pending &= ~rb;
+                done |= rb;
+#ifndef NX_EXP_NOSYNC
+                if (pending) wave_sync();
+#endif
+            }
+#ifdef NX_EXP_COUNT
+            if (lane == 0) {
+                atomicAdd(&g_cnt[0], 1ull);
+                atomicAdd(&g_cnt[2], (unsigned long long)__popcll(__ballot(valid)));
+            }
+            {
+                int nr = 0;
+                for (uint64_t pd = __ballot(valid), dn = ~__ballot(valid); pd; ++nr) {
+                    const uint64_t rb = __ballot(((pd >> lane) & 1ull) != 0 && (need & ~dn) == 0ull);
+                    pd &= ~rb; dn |= rb;
+                }
+                const uint64_t farm = __ballot(far), ovm = __ballot(ovl);
+                if (lane == 0) {
+                    atomicAdd(&g_cnt[1], (unsigned long long)nr);
+                    atomicAdd(&g_cnt[3], (unsigned long long)__popcll(farm));
+                    atomicAdd(&g_cnt[4], (unsigned long long)__popcll(ovm));
+                }
+            }
+#endif
+            if (st == kGuardTrip + 3) break;
+            O = E;
+        }
+        const uint32_t Ofin = uni(out_len[c]);
+        if (st == kGuardTrip + 3) O = Ofin;  // unreachable on a consistent record stream
+        const uint32_t crc = io.finish(O, &tabs->NS[0][0][0]);
+        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],
+                     crc_out ? &crc_out[c] : nullptr);
+    }
+}
+#endif
 // =====================================================================================
 // LZ4 blocks through the same record expander
 // =====================================================================================
@@ -1034,10 +1259,14 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lz4(const uint8_t* __rest
             st = NX_ERR_LZ4_MALFORMED;
             break;
         }
+#ifdef NX_EXP_R8
+        for (uint32_t k = 0; k < lit && fit; k += 8u) fit = rw.put(((min(8u, lit - k) - 1u) << 25) | (ip + k));
+#else
         for (uint32_t k = 0; k < lit && fit; k += 64u) {
             const uint32_t m = lit - k < 64u ? lit - k : 64u;
             fit = rw.put(((m - 1u) << 25) | (ip + k));
         }
+#endif
         if (!fit) break;
         ip += lit;
         op += lit;
@@ -1069,10 +1298,15 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lz4(const uint8_t* __rest
             st = NX_ERR_LZ4_MALFORMED;
             break;
         }
+#ifdef NX_EXP_R8
+        for (uint32_t k = 0; k < ml && fit; k += 8u)
+            fit = rw.put(0x80000000u | ((min(8u, ml - k) - 1u) << 25) | (off < 8u ? 0x10000000u | (((k >> 3) & 7u) << 8) | off : off));
+#else
         for (uint32_t k = 0; k < ml && fit; k += 64u) {
             const uint32_t m = ml - k < 64u ? ml - k : 64u;
             fit = rw.put(0x80000000u | ((m - 1u) << 25) | off);
         }
+#endif
         if (!fit) break;
         op += ml;
     }
