@@ -13,6 +13,9 @@
 //   * match extension compares 4 bytes per step and finds the first mismatch with ctz;
 //   * output bytes are packed into dwords and written with aligned 4-byte stores; literal runs
 //     are copied 4 bytes at a time with a funnel shift.
+// Small batches take two latency forms of the same matcher (nx_snappy_encode_batch picks by batch
+// size): up to one chunk per CU, a workgroup per chunk with the table and the chunk in LDS; up to
+// kSpreadMaxChunks, one chunk per wave (lane 0), so no wave serialises 64 divergent matchers.
 // Hash table: Java allocates a zeroed short[min(nextPow2(len),16384)] per call (:97-99,191).
 // Each resident lane owns a 16384-entry uint32 slot in a device workspace; an entry is
 //   stamp[31:28] | check[27:16] | position[15:0]
@@ -327,14 +330,21 @@ done:
 
 // Launch bound 6 blocks of 256 per CU keeps the kernel under 80 VGPRs (no spills) at the 16 waves/CU
 // the host launches.
-template <bool SWAP>
+//
+// SPREAD = false: lane t encodes chunks t, t + lanes, ... (throughput form, every lane of a wave busy).
+// SPREAD = true: one chunk per WAVE, lane 0 only (small batches: lanes of different chunks never share
+// a wave's divergent control flow, which otherwise serialises a wave's 64 matchers: 64 chunks in one
+// wave take 6x as long as one).  Lane/wave w owns table slot w of the workspace in either form.
+template <bool SWAP, bool SPREAD>
 __global__ void __launch_bounds__(256, 6) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                        const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
                                                        int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
                                                        uint32_t stamp_base) {
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t nthreads = gridDim.x * blockDim.x;
+    const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (SPREAD && (gtid & 63u) != 0u) return;
+    const uint32_t tid = SPREAD ? gtid >> 6 : gtid;
+    const uint32_t nthreads = SPREAD ? (gridDim.x * blockDim.x) >> 6 : gridDim.x * blockDim.x;
     uint32_t* table = workspace + (size_t)tid * 16384u;
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
@@ -363,6 +373,61 @@ __global__ void __launch_bounds__(256, 6) k_snappy_encode(const uint8_t* __restr
     }
 }
 
+// Latency form for batches of at most one chunk per CU: one workgroup per chunk clears a table in
+// LDS and stages the chunk there, then one lane runs the matcher against LDS only (no stamps: the
+// table is zeroed, an entry's stamp is 1).  128 KiB of LDS, one chunk per CU; 1.6x faster than the
+// SPREAD form for a lone chunk (profiles/r02/notes/small_batches.md).
+constexpr uint32_t kLdsTableBytes = 16384u * 4u;
+constexpr uint32_t kLdsBytes = kLdsTableBytes + 65536u + 16u;
+__global__ void __launch_bounds__(64) k_snappy_encode_lds(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                         const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                         const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
+                                                         int32_t* __restrict__ status, uint32_t n) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* table = reinterpret_cast<uint32_t*>(smem);
+    uint8_t* buf = smem + kLdsTableBytes;
+    const uint32_t t = threadIdx.x;
+    for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
+        const uint32_t len = in_len[c];
+        if (len > 65536u) {
+            if (t == 0) {
+                status[c] = NX_ERR_INVALID_ARG;
+                out_len[c] = 0;
+            }
+            continue;
+        }
+        const uint8_t* src = in + in_off[c];
+        for (uint32_t i = t; i < 16384u / 4u; i += 64u) reinterpret_cast<uint4*>(table)[i] = make_uint4(0, 0, 0, 0);
+        for (uint32_t i = 4u * t; i < len; i += 256u) {
+            uint32_t v = 0;
+            if (i + 4u <= len) {
+                v = ld32(src + i);
+            } else {
+                for (uint32_t k = 0; i + k < len; ++k) v |= (uint32_t)src[i + k] << (8 * k);
+            }
+            *reinterpret_cast<uint32_t*>(buf + i) = v;
+        }
+        __syncthreads();
+        if (t == 0) {
+            uint8_t* o = out + out_off[c];
+            uint32_t olen;
+            if ((((uintptr_t)o) & 7u) == 0) {
+                WriterT<true> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
+                olen = encode_chunk<false>(buf, (int32_t)len, w, table, 1u);
+            } else if ((((uintptr_t)o) & 3u) == 0) {
+                WriterT<false> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
+                olen = encode_chunk<false>(buf, (int32_t)len, w, table, 1u);
+            } else {
+                ByteWriter w{o, 0};
+                olen = encode_chunk<false>(buf, (int32_t)len, w, table, 1u);
+            }
+            out_len[c] = olen;
+            status[c] = NX_OK;
+        }
+        __syncthreads();  // the next chunk's staging overwrites the table and buffer
+    }
+}
+
 }  // namespace enc
 }  // namespace nx
 
@@ -371,7 +436,7 @@ namespace {
 // they may share a workspace; launches on different streams may overlap and must not.
 struct Workspace {
     uint32_t* ws = nullptr;
-    size_t threads = 0;
+    size_t threads = 0;  // table slots (lanes of the dense form, waves of the spread form)
     uint32_t stamp = 0;  // last stamp used; entries carry 4-bit stamps 1..15
 };
 std::mutex g_ws_mu;
@@ -379,6 +444,7 @@ std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
 constexpr unsigned kEncBlock = 256;
 constexpr unsigned kEncWavesPerCU = 16;
 constexpr uint32_t kMaxStamp = 15;
+constexpr uint32_t kSpreadMaxChunks = 16384;  // above this the dense form is faster
 }  // namespace
 
 extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
@@ -388,32 +454,53 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
     int dev = 0, cus = 256;
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    constexpr unsigned waves_per_cu = kEncWavesPerCU;
     const hipStream_t st = (hipStream_t)stream;
-    const size_t want = (size_t)cus * waves_per_cu * 64;
-    const size_t threads = n < want ? ((n + kEncBlock - 1) / kEncBlock) * kEncBlock : want;
+    // Batch-size policy (profiles/r02/notes/small_batches.md): a chunk per CU with LDS tables, then a
+    // chunk per wave, then the dense lane-per-chunk form once the batch fills the chip.
+    if (n <= (uint32_t)cus) {
+        static std::once_flag once;
+        static hipError_t attr = hipSuccess;
+        std::call_once(once, [] {
+            attr = hipFuncSetAttribute((const void*)nx::enc::k_snappy_encode_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)nx::enc::kLdsBytes);
+        });
+        NX_HIP_CHECK(attr);
+        hipLaunchKernelGGL(nx::enc::k_snappy_encode_lds, dim3(n), dim3(64), nx::enc::kLdsBytes, st, in, in_off, in_len, out, out_off,
+                           out_len, status, n);
+        NX_HIP_CHECK(hipGetLastError());
+        return NX_OK;
+    }
+    const bool spread = n <= kSpreadMaxChunks;
+    const size_t want = (size_t)cus * kEncWavesPerCU * (spread ? 1 : 64);  // table slots: waves or lanes
+    const size_t slots = n < want ? (spread ? n : ((n + kEncBlock - 1) / kEncBlock) * kEncBlock) : want;
     const size_t per = 16384u * sizeof(uint32_t);
     std::lock_guard<std::mutex> lk(g_ws_mu);
     Workspace& W = g_ws[{dev, st}];
-    if (W.ws == nullptr || W.threads < threads) {
+    if (W.ws == nullptr || W.threads < slots) {
         if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
         W.ws = nullptr;
-        NX_HIP_CHECK(hipMalloc(&W.ws, threads * per));
-        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, threads * per, st));
-        W.threads = threads;
+        NX_HIP_CHECK(hipMalloc(&W.ws, slots * per));
+        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, slots * per, st));
+        W.threads = slots;
         W.stamp = 0;
     }
-    // Each launch gives a resident lane at most kMaxStamp - 1 chunks (one stamp each).
-    const size_t per_launch = threads * (kMaxStamp - 1);
+    // Each launch gives a table slot at most kMaxStamp - 1 chunks (one stamp each).
+    const size_t per_launch = slots * (kMaxStamp - 1);
     for (size_t base = 0; base < n; base += per_launch) {
         const uint32_t m = (uint32_t)std::min<size_t>(per_launch, n - base);
-        const uint32_t iters = (uint32_t)((m + threads - 1) / threads);
+        const uint32_t iters = (uint32_t)((m + slots - 1) / slots);
         if (W.stamp + iters >= kMaxStamp) {
             NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.threads * per, st));
             W.stamp = 0;
         }
-        hipLaunchKernelGGL(nx::enc::k_snappy_encode<true>, dim3((unsigned)(threads / kEncBlock)), dim3(kEncBlock), 0, st, in,
-                           in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp);
+        if (spread) {
+            const size_t waves = std::min<size_t>(slots, m);
+            hipLaunchKernelGGL((nx::enc::k_snappy_encode<true, true>), dim3((unsigned)waves), dim3(64), 0, st, in, in_off + base,
+                               in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp);
+        } else {
+            hipLaunchKernelGGL((nx::enc::k_snappy_encode<true, false>), dim3((unsigned)(slots / kEncBlock)), dim3(kEncBlock), 0, st, in,
+                               in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp);
+        }
         NX_HIP_CHECK(hipGetLastError());
         W.stamp += iters;
     }

@@ -43,7 +43,13 @@ int main(int argc, char** argv) {
         (void)hipEventRecord(b); (void)hipEventSynchronize(b); (void)hipEventElapsedTime(&ms, a, b);
         best_ref = std::min(best_ref, ms);
         (void)hipEventRecord(a);
+#if defined(NX_EXP_LDS)
+        if (xexp_lds_encode_batch(din, ioff, ilen, d2, ooff, l2, s2, N, 0) != 0) return 2;
+#elif defined(NX_EXP_SPREAD)
+        if (xexp_spread_encode_batch(din, ioff, ilen, d2, ooff, l2, s2, N, 0) != 0) return 2;
+#else
         if (xexp_nx_snappy_encode_batch(din, ioff, ilen, d2, ooff, l2, s2, N, 0) != 0) return 2;
+#endif
         (void)hipEventRecord(b); (void)hipEventSynchronize(b); (void)hipEventElapsedTime(&ms, a, b);
         best = std::min(best, ms);
     }

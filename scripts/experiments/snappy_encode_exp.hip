@@ -366,6 +366,99 @@ __global__ void __launch_bounds__(256, NX_ENC_MINBLK) k_snappy_encode(const uint
     }
 }
 
+
+// Low-latency form for small batches: one workgroup per chunk keeps the chunk's table (16 384 u32)
+// and its input (<= 64 KiB) in LDS; the workgroup clears the table and stages the input, then one
+// lane runs the serial matcher against LDS only.  One chunk per CU (128 KiB of LDS).
+constexpr uint32_t kLdsTable = 16384u * 4u;
+__global__ void __launch_bounds__(64) k_snappy_encode_lds(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                         const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                         const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
+                                                         int32_t* __restrict__ status, uint32_t n) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* table = reinterpret_cast<uint32_t*>(smem);
+    uint8_t* buf = smem + kLdsTable;
+    const uint32_t t = threadIdx.x;
+    for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
+        const uint32_t len = in_len[c];
+        if (len > 65536u) {
+            if (t == 0) {
+                status[c] = NX_ERR_INVALID_ARG;
+                out_len[c] = 0;
+            }
+            continue;
+        }
+        const uint8_t* src = in + in_off[c];
+        for (uint32_t i = t; i < 16384u / 4u; i += 64u) reinterpret_cast<uint4*>(table)[i] = make_uint4(0, 0, 0, 0);
+        for (uint32_t i = 4u * t; i < len; i += 256u) {
+            uint32_t v;
+            if (i + 4u <= len) {
+                v = ld32(src + i);
+            } else {
+                v = 0;
+                for (uint32_t k = 0; i + k < len; ++k) v |= (uint32_t)src[i + k] << (8 * k);
+            }
+            *reinterpret_cast<uint32_t*>(buf + i) = v;
+        }
+        __syncthreads();
+        if (t == 0) {
+            uint8_t* o = out + out_off[c];
+            uint32_t olen;
+            if ((((uintptr_t)o) & 7u) == 0) {
+                WriterT<true> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
+                olen = encode_chunk<false>(buf, (int32_t)len, w, table, 1u);
+            } else if ((((uintptr_t)o) & 3u) == 0) {
+                WriterT<false> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
+                olen = encode_chunk<false>(buf, (int32_t)len, w, table, 1u);
+            } else {
+                ByteWriter w{o, 0};
+                olen = encode_chunk<false>(buf, (int32_t)len, w, table, 1u);
+            }
+            out_len[c] = olen;
+            status[c] = NX_OK;
+        }
+        __syncthreads();
+    }
+}
+
+// Spread form for small batches: one chunk per WAVE (lane 0 works, the other lanes exit), so lanes of
+// different chunks never share a wave's divergent control flow.
+__global__ void __launch_bounds__(256) k_snappy_encode_spread(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                            const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                            const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
+                                                            int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
+                                                            uint32_t stamp_base) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid & 63u) return;
+    const uint32_t wid = tid >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    uint32_t* table = workspace + (size_t)wid * 16384u;
+    uint32_t iter = 0;
+    for (uint32_t c = wid; c < n; c += nwaves, ++iter) {
+        const uint32_t len = in_len[c];
+        if (len > 65536u) {
+            status[c] = NX_ERR_INVALID_ARG;
+            out_len[c] = 0;
+            continue;
+        }
+        const uint32_t stamp = stamp_base + iter + 1u;
+        uint8_t* o = out + out_off[c];
+        uint32_t olen;
+        const uint8_t* src = in + in_off[c];
+        if ((((uintptr_t)o) & 7u) == 0) {
+            WriterT<true> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
+            olen = encode_chunk<true>(src, (int32_t)len, w, table, stamp);
+        } else if ((((uintptr_t)o) & 3u) == 0) {
+            WriterT<false> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
+            olen = encode_chunk<true>(src, (int32_t)len, w, table, stamp);
+        } else {
+            ByteWriter w{o, 0};
+            olen = encode_chunk<true>(src, (int32_t)len, w, table, stamp);
+        }
+        out_len[c] = olen;
+        status[c] = NX_OK;
+    }
+}
 }  // namespace encx
 }  // namespace nx
 
@@ -421,4 +514,43 @@ extern "C" int32_t xexp_nx_snappy_encode_batch(const uint8_t* in, const uint64_t
         W.stamp += iters;
     }
     return NX_OK;
+}
+
+extern "C" int32_t xexp_lds_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                          const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream) {
+    const size_t lds = nx::encx::kLdsTable + 65536 + 16;
+    static bool once = false;
+    if (!once) {
+        if (hipFuncSetAttribute((const void*)nx::encx::k_snappy_encode_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return NX_ERR_HIP;
+        once = true;
+    }
+    hipLaunchKernelGGL(nx::encx::k_snappy_encode_lds, dim3(n), dim3(64), lds, (hipStream_t)stream, in, in_off, in_len, out, out_off,
+                       out_len, status, n);
+    return hipGetLastError() == hipSuccess ? NX_OK : NX_ERR_HIP;
+}
+
+extern "C" int32_t xexp_spread_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                             const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream) {
+    static uint32_t* ws = nullptr;
+    const uint32_t waves = n < 4096u ? n : 4096u;
+    if (!ws) {
+        if (hipMalloc(&ws, (size_t)4096 * 16384 * 4) != hipSuccess) return NX_ERR_HIP;
+        if (hipMemset(ws, 0, (size_t)4096 * 16384 * 4) != hipSuccess) return NX_ERR_HIP;
+    }
+    // (experiment: 14 chunks per wave at most before the stamps wrap; n <= 4096 * 14 here)
+    static uint32_t stamp = 0;
+    const uint32_t iters = (n + waves - 1) / waves;
+    if (stamp + iters >= 15u) {
+        if (hipMemsetAsync(ws, 0, (size_t)4096 * 16384 * 4, (hipStream_t)stream) != hipSuccess) return NX_ERR_HIP;
+        stamp = 0;
+    }
+    const uint32_t threads = waves * 64u;
+#ifndef NX_EXP_SPREAD_BLK
+#define NX_EXP_SPREAD_BLK 256u
+#endif
+    hipLaunchKernelGGL(nx::encx::k_snappy_encode_spread, dim3((threads + NX_EXP_SPREAD_BLK - 1) / NX_EXP_SPREAD_BLK), dim3(NX_EXP_SPREAD_BLK), 0, (hipStream_t)stream, in, in_off, in_len,
+                       out, out_off, out_len, status, n, ws, stamp);
+    stamp += iters;
+    return hipGetLastError() == hipSuccess ? NX_OK : NX_ERR_HIP;
 }

@@ -269,6 +269,30 @@ def test_pack_batch_gathers_slots():
         assert torch.equal(got, want)
 
 
+@pytest.mark.parametrize("n", [1, 7, 256, 257, 4097, 16384, 16385])
+def test_snappy_encode_batch_size_forms(dev, B, oracle, n):
+    """nx_snappy_encode_batch picks the LDS form (n <= CUs), the wave-per-chunk form (n <= 16 384) or
+    the dense lane-per-chunk form by batch size: each is bit-exact with the oracle, on mixed sizes
+    (1 B .. 64 KiB, text and random) and unaligned starts/outputs."""
+    rng = random.Random(n)
+    idx = sorted({0, n - 1} | {rng.randrange(n) for _ in range(min(n, 40))})
+    sizes = [rng.choice([1, 14, 15, 16, 100, 4096, 32767, 65535, 65536]) if i in idx else 64 for i in range(n)]
+    chunks = [(oracle.textgen_chunk(i, s) if i % 2 else bytes(rng.getrandbits(8) for _ in range(s))) if i in idx
+              else bytes(s) for i, s in enumerate(sizes)]
+    inp, off, ln = B.pack(chunks, dev, align=1)
+    cap = [B.snappy_max_compressed_length(len(c)) + 1 for c in chunks]
+    out, ooff = B.out_slots(cap, dev, align=1)
+    olen, st = B.snappy_encode(inp, off, ln, out, ooff)
+    assert int((st != 0).sum()) == 0
+    ol, oo = olen.cpu().tolist(), ooff.cpu().tolist()
+    for i in idx:
+        assert out[oo[i]:oo[i] + ol[i]].cpu().numpy().tobytes() == oracle.snappy_encode(chunks[i]), i
+    zero = oracle.snappy_encode(bytes(64))
+    for i in range(0, n, max(1, n // 50)):
+        if i not in idx:
+            assert out[oo[i]:oo[i] + ol[i]].cpu().numpy().tobytes() == zero, i
+
+
 def test_snappy_encode_stamp_wrap_many_chunks_per_lane(dev, B, oracle):
     """one encoder lane encodes more than 14 chunks, so the host splits the batch
     into launches and re-zeroes the 4-bit-stamped table workspace before the stamps wrap
