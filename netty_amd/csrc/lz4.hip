@@ -151,13 +151,14 @@ last_literals:
     return op + lit;
 }
 
+template <bool SPREAD>
 __global__ void __launch_bounds__(256) k_lz4_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                     const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
                                                     int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
                                                     uint32_t stamp_base) {
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t nthreads = gridDim.x * blockDim.x;
+    uint32_t tid, nthreads;
+    if (!chunk_slot<SPREAD>(tid, nthreads)) return;
     uint32_t* table = workspace + (size_t)tid * kTableSlots;
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
@@ -199,8 +200,8 @@ extern "C" int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const hipStream_t st = (hipStream_t)stream;
-    const size_t want = (size_t)cus * 16 * 64;  // 16 waves per CU, as the Snappy encoder
-    const size_t threads = n < want ? ((n + 255) / 256) * 256 : want;
+    const nx::LaneGrid g = nx::lane_grid(n, cus, 16);  // 16 waves per CU, as the Snappy encoder
+    const size_t threads = g.slots;
     const size_t per = nx::lz4::kTableSlots * sizeof(uint32_t);
     std::lock_guard<std::mutex> lk(g_lz4_mu);
     Lz4Workspace& W = g_lz4_ws[{dev, st}];
@@ -217,8 +218,12 @@ extern "C" int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off
         NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.threads * per, st));
         W.stamp = 0;
     }
-    hipLaunchKernelGGL(nx::lz4::k_lz4_encode, dim3((unsigned)(threads / 256)), dim3(256), 0, st, in, in_off, in_len, out, out_off,
-                       out_len, status, n, W.ws, W.stamp);
+    if (g.spread)
+        hipLaunchKernelGGL(nx::lz4::k_lz4_encode<true>, dim3(g.grid), dim3(g.block), 0, st, in, in_off, in_len, out, out_off, out_len,
+                           status, n, W.ws, W.stamp);
+    else
+        hipLaunchKernelGGL(nx::lz4::k_lz4_encode<false>, dim3(g.grid), dim3(g.block), 0, st, in, in_off, in_len, out, out_off, out_len,
+                           status, n, W.ws, W.stamp);
     NX_HIP_CHECK(hipGetLastError());
     W.stamp += iters;
     return NX_OK;

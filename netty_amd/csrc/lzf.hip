@@ -135,12 +135,13 @@ __device__ int32_t decode_chunk(const uint8_t* __restrict__ in, int32_t in_len, 
     return op == out_len ? NX_OK : NX_ERR_LZF_CORRUPT;
 }
 
+template <bool SPREAD>
 __global__ void __launch_bounds__(256) k_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                 const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                 const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
                                                 int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ ws, uint32_t stamp_base) {
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t nthreads = gridDim.x * blockDim.x;
+    uint32_t tid, nthreads;
+    if (!chunk_slot<SPREAD>(tid, nthreads)) return;
     uint32_t* htab = ws + (size_t)tid * HSIZE;
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
@@ -169,13 +170,18 @@ __global__ void __launch_bounds__(256) k_decode(const uint8_t* __restrict__ in, 
 }  // namespace lzf
 }  // namespace nx
 
+#include <map>
 #include <mutex>
 namespace {
+// Hash-table workspace, one per (device, stream): launches on one stream are ordered and may share
+// it; launches on different streams (or devices) may overlap and must not.
+struct LzfWorkspace {
+    uint32_t* ws = nullptr;
+    size_t slots = 0;
+    uint32_t stamp = 0;
+};
 std::mutex g_mu;
-uint32_t* g_ws = nullptr;
-size_t g_ws_threads = 0;
-uint32_t g_stamp = 0;
-int g_dev = -1;
+std::map<std::pair<int, hipStream_t>, LzfWorkspace> g_lzf_ws;
 }  // namespace
 
 extern "C" int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
@@ -185,29 +191,32 @@ extern "C" int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off
     int dev = 0, cus = 256;
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const size_t want = (size_t)cus * 8 * 64;
-    const size_t threads = n < want ? ((n + 255) / 256) * 256 : want;
+    const nx::LaneGrid g = nx::lane_grid(n, cus, 8);
+    const hipStream_t st = (hipStream_t)stream;
     const size_t per = (size_t)nx::lzf::HSIZE * sizeof(uint32_t);
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_ws || g_ws_threads < threads || g_dev != dev) {
-        if (g_ws) (void)hipFree(g_ws);
-        g_ws = nullptr;
-        const size_t cap = threads > want ? threads : want;
-        NX_HIP_CHECK(hipMalloc(&g_ws, cap * per));
-        NX_HIP_CHECK(hipMemsetAsync(g_ws, 0, cap * per, (hipStream_t)stream));
-        g_ws_threads = cap;
-        g_dev = dev;
-        g_stamp = 0;
+    LzfWorkspace& W = g_lzf_ws[{dev, st}];
+    if (W.ws == nullptr || W.slots < g.slots) {
+        if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
+        W.ws = nullptr;
+        NX_HIP_CHECK(hipMalloc(&W.ws, g.slots * per));
+        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, g.slots * per, st));
+        W.slots = g.slots;
+        W.stamp = 0;
     }
-    const uint32_t iters = (uint32_t)((n + threads - 1) / threads);
-    if ((uint64_t)g_stamp + iters >= 65535u) {
-        NX_HIP_CHECK(hipMemsetAsync(g_ws, 0, g_ws_threads * per, (hipStream_t)stream));
-        g_stamp = 0;
+    const uint32_t iters = (uint32_t)((n + g.slots - 1) / g.slots);
+    if ((uint64_t)W.stamp + iters >= 65535u) {
+        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.slots * per, st));
+        W.stamp = 0;
     }
-    hipLaunchKernelGGL(nx::lzf::k_encode, dim3((unsigned)(threads / 256)), dim3(256), 0, (hipStream_t)stream, in, in_off, in_len, out,
-                       out_off, out_len, status, n, g_ws, g_stamp);
+    if (g.spread)
+        hipLaunchKernelGGL(nx::lzf::k_encode<true>, dim3(g.grid), dim3(g.block), 0, st, in, in_off, in_len, out, out_off, out_len, status,
+                           n, W.ws, W.stamp);
+    else
+        hipLaunchKernelGGL(nx::lzf::k_encode<false>, dim3(g.grid), dim3(g.block), 0, st, in, in_off, in_len, out, out_off, out_len,
+                           status, n, W.ws, W.stamp);
     NX_HIP_CHECK(hipGetLastError());
-    g_stamp += iters;
+    W.stamp += iters;
     return NX_OK;
 }
 

@@ -62,6 +62,33 @@ __host__ __device__ inline uint32_t gf_x8n(uint64_t n) {
     return result;
 }
 
+// Lane-per-chunk encoders (LZ4, FastLZ, LZF; Snappy has its own three forms): the dense form gives
+// every lane a chunk; for batches up to kSpreadMaxChunks the SPREAD form gives each wave one chunk
+// on lane 0, so the serial matchers of different chunks never share a wave's divergent control
+// flow (64 divergent matchers in one wave run ~6x longer than one).  Table slot = lane or wave.
+constexpr uint32_t kSpreadMaxChunks = 16384;
+template <bool SPREAD>
+__device__ __forceinline__ bool chunk_slot(uint32_t& slot, uint32_t& slots) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, t = gridDim.x * blockDim.x;
+    slot = SPREAD ? g >> 6 : g;
+    slots = SPREAD ? t >> 6 : t;
+    return !SPREAD || (g & 63u) == 0u;
+}
+struct LaneGrid {
+    bool spread;
+    size_t slots;  // table slots the launch uses (lanes or waves)
+    unsigned grid, block;
+};
+inline LaneGrid lane_grid(uint32_t n, int cus, unsigned waves_per_cu) {
+    LaneGrid g;
+    g.spread = n <= kSpreadMaxChunks;
+    const size_t want = (size_t)cus * waves_per_cu * (g.spread ? 1u : 64u);
+    g.slots = n < want ? (g.spread ? (size_t)n : ((size_t)n + 255) / 256 * 256) : want;
+    g.block = g.spread ? 64u : 256u;
+    g.grid = (unsigned)(g.spread ? g.slots : g.slots / 256);
+    return g;
+}
+
 // Kernel launch helper: grid-stride sizes.
 inline unsigned grid_for(uint64_t threads, unsigned block) {
     uint64_t g = (threads + block - 1) / block;
