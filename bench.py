@@ -59,6 +59,7 @@ def parse(argv=None):
     ap.add_argument("--e2e-chunks", type=int, default=131072, help="chunks through the torch host pipeline (8 GiB)")
     ap.add_argument("--e2e-sub", type=int, default=65536, help="chunks per pipelined sub-batch")
     ap.add_argument("--no-alt", action="store_true", help="skip the FastLZ/LZF/LZ4 (configs[3]) measurement")
+    ap.add_argument("--no-probe-ceiling", action="store_true", help="skip the live random-access ceiling of the encoder")
     ap.add_argument("--alt-chunks", type=int, default=262144)
     ap.add_argument("--no-frame-scan", action="store_true", help="skip the framed-stream (§8f row 1) measurement")
     ap.add_argument("--scan-chunks", type=int, default=131072, help="chunks laid out as framed streams")
@@ -435,7 +436,7 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
     traffic = load_traffic() if gpu else (None, "cpu test leg")
     r_dec = roofline(C_ + U, t_dec, n, DEC_KERNELS, traffic, copy_gbs)  # decode: C_in + U_out per chunk
     r_enc = roofline(U + C_, t_enc, n, ENC_KERNELS, traffic, copy_gbs)  # encode: U_in + C_out per chunk
-    if gpu and t_enc:
+    if gpu and t_enc and not args.no_probe_ceiling:
         ceil = probe_ceiling(torch, dev)
         got = ENC_PROBES_PER_CHUNK * n / (t_enc / 1e3)
         r_enc["random_access"] = {
@@ -471,6 +472,8 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
     }
     ok = S.all_true(ok, device=dev)
     line["verified"] = ok
+    if gpu and rank == 0:
+        line["device"] = device_info(torch, dev)
     if gpu and args.weak_chunks > 0:
         del leg
         torch.cuda.empty_cache()
@@ -518,6 +521,24 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
 
 
 # ---------------------------------------------------------------------------------------- extra legs
+def device_info(torch, dev):
+    """What the box is: device properties and the power cap (the encoder's speed differs by ~15 %
+    between boxes of this pool; recorded so runs can be compared)."""
+    import subprocess
+    p = torch.cuda.get_device_properties(dev)
+    info = {"name": p.name, "arch": p.gcnArchName, "cus": p.multi_processor_count, "hbm_gib": round(p.total_memory / 2**30, 1),
+            "pci_bus_id": getattr(p, "pci_bus_id", None)}
+    try:
+        r = subprocess.run(["rocm-smi", "--showmaxpower", "--showmemorypartition", "--showcomputepartition"], capture_output=True,
+                           text=True, timeout=30)
+        keep = [ln.split(":", 1)[1].strip() if ":" in ln else ln for ln in r.stdout.splitlines()
+                if "GPU[" in ln and ("Power" in ln or "Partition" in ln)]
+        info["rocm_smi"] = keep
+    except (OSError, subprocess.SubprocessError):
+        info["rocm_smi"] = None
+    return info
+
+
 def e2e_capi(channels: int, messages: int, timeout: float = 240.0):
     """Host-to-host Snappy frame round trip through the asynchronous batcher C-ABI
     (netty_amd/tools/e2e_capi.cpp): `channels` SnappyFrameEncoder/Decoder pairs, `messages` 65535-byte
