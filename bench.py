@@ -557,7 +557,9 @@ def e2e_capi(channels: int, messages: int, timeout: float = 240.0):
     except (ValueError, IndexError):
         return {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
     d["path"] = ("pooled-direct-ByteBuf stand-in (registered host memory) -> nx_snappy_frame_encoder_submit x N -> one flush "
-                 "-> framed bytes in mapped pinned memory -> nx_snappy_frame_decoder_submit x N -> one flush -> messages")
+                 "-> framed bytes in mapped pinned memory -> (network: copied, untimed, into a registered receive buffer) -> "
+                 "nx_snappy_frame_decoder_submit_registered x N -> one flush -> messages; decode_copied_*: the same through "
+                 "nx_snappy_frame_decoder_submit (payloads copied at submit)")
     return d
 
 

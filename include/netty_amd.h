@@ -331,6 +331,11 @@ int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx_batcher* b
  * (status < 0) the first failure's message; a failed job marks the decoder corrupted (:227-230). */
 int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
                                        size_t* consumed);
+/* The same for a cumulation in registered memory (a pooled direct buffer the socket read into): the
+ * consumed bytes in[0..*consumed) are not copied; they stay valid until the job completes (a Java
+ * caller keeps a retained slice) and the chunk payloads are gathered from the mapped pages at flush. */
+int64_t nx_snappy_frame_decoder_submit_registered(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
+                                                  size_t* consumed);
 int32_t nx_batcher_flush(nx_batcher* b);
 int32_t nx_batcher_poll(nx_batcher* b, int64_t ticket);  /* 1 done, 0 pending, < 0 error; never blocks */
 int32_t nx_batcher_wait(nx_batcher* b, int64_t ticket);  /* blocks (flushes first if needed): NX_OK */

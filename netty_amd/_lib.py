@@ -64,6 +64,7 @@ _SIGS = {
     "nx_host_unregister": (i32, [vp]),
     "nx_snappy_frame_encoder_submit": (i64, [vp, vp, vp, sz, i32]),
     "nx_snappy_frame_decoder_submit": (i64, [vp, vp, vp, sz, C.POINTER(sz)]),
+    "nx_snappy_frame_decoder_submit_registered": (i64, [vp, vp, vp, sz, C.POINTER(sz)]),
     "nx_batcher_flush": (i32, [vp]),
     "nx_batcher_poll": (i32, [vp, i64]),
     "nx_batcher_wait": (i32, [vp, i64]),

@@ -239,19 +239,22 @@ struct Batch {
         size_t len;
         uint64_t din_off;
     };
-    std::vector<Direct> direct;  // registered encoder inputs, DMA'd at flush (din_off in the direct region)
+    std::vector<Direct> direct;  // registered inputs / cumulations, gathered at flush (din_off in the direct region)
     uint64_t direct_used = 0;
     std::vector<EncSlice> esl;
     std::vector<uint8_t> esl_direct;  // slice input lies in the direct region
     std::vector<EncJob> ejob;
     uint64_t eslots = 0;
     std::vector<DecAct> dact;
+    std::vector<uint8_t> dact_direct;  // payload lies in the direct region (registered cumulation)
     std::vector<DecJob> djob;
     std::vector<uint64_t> dc_off;  // compressed chunks: payload offsets / lengths / expected CRC
     std::vector<uint32_t> dc_len, dc_crc;
     bool dc_validate = false;
+    std::vector<uint8_t> dc_direct;
     std::vector<uint64_t> du_off;  // uncompressed chunks (CRC32C)
     std::vector<uint32_t> du_len;
+    std::vector<uint8_t> du_direct;
     Pinned out;  // mapped result arena: job outputs, then the result records
     uint64_t out_used = 0, res_enc = 0, res_dec = 0;
     std::vector<Job*> jobs;
@@ -268,13 +271,16 @@ struct Batch {
         ejob.clear();
         eslots = 0;
         dact.clear();
+        dact_direct.clear();
         djob.clear();
         dc_off.clear();
         dc_len.clear();
         dc_crc.clear();
+        dc_direct.clear();
         dc_validate = false;
         du_off.clear();
         du_len.clear();
+        du_direct.clear();
         out_used = res_enc = res_dec = 0;
         for (Job* j : jobs) delete j;
         jobs.clear();
@@ -380,6 +386,12 @@ int32_t launch(nx_batcher* b, Batch* bt) {
     const uint64_t d0 = (bt->st_used + 15) & ~15ull;
     for (uint32_t i = 0; i < nes; ++i)
         if (bt->esl_direct[i]) bt->esl[i].in_off += d0;
+    for (uint32_t i = 0; i < nda; ++i)
+        if (bt->dact_direct[i]) bt->dact[i].in_off += d0;
+    for (uint32_t i = 0; i < ndc; ++i)
+        if (bt->dc_direct[i]) bt->dc_off[i] += d0;
+    for (uint32_t i = 0; i < ndu; ++i)
+        if (bt->du_direct[i]) bt->du_off[i] += d0;
     std::vector<uint64_t> ein(nes), eslot(nes), dslot(ndc);
     std::vector<uint32_t> elen(nes);
     for (uint32_t i = 0; i < nes; ++i) {
@@ -654,8 +666,8 @@ extern "C" int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx
     return (int64_t)j->ticket;
 }
 
-extern "C" int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
-                                                  size_t* consumed) {
+namespace {
+int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n, size_t* consumed, bool registered) {
     if (!d || !b || (!in && n) || !consumed) return NX_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(b->mu);
     Batch* bt = collecting(b);
@@ -684,6 +696,34 @@ extern "C" int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx
         if (j->has_parse_err) d->corrupted = true;  // later submits skip their input (:227-230)
     }
     *consumed = p;
+    // on a failure below the batch's arrays go back to their sizes at entry (other jobs stay valid)
+    const size_t n_act = bt->dact.size(), n_dc = bt->dc_off.size(), n_du = bt->du_off.size(), n_dir = bt->direct.size();
+    const uint64_t dir_used = bt->direct_used;
+    auto fail = [&](int32_t code) -> int64_t {
+        bt->dact.resize(n_act);
+        bt->dact_direct.resize(n_act);
+        bt->dc_off.resize(n_dc);
+        bt->dc_len.resize(n_dc);
+        bt->dc_crc.resize(n_dc);
+        bt->dc_direct.resize(n_dc);
+        bt->du_off.resize(n_du);
+        bt->du_len.resize(n_du);
+        bt->du_direct.resize(n_du);
+        bt->direct.resize(n_dir);
+        bt->direct_used = dir_used;
+        delete j;
+        return code;
+    };
+    // registered cumulation: the consumed bytes are gathered from the mapped pages at flush (the
+    // caller keeps them valid until the job completes); else every payload is copied now
+    uint64_t rbase = 0;
+    if (registered && p) {
+        const uint8_t* dsrc = registered_device_ptr(in, p);
+        if (!dsrc) return fail(NX_ERR_INVALID_ARG);  // not inside an nx_host_register'd range
+        rbase = (bt->direct_used + 15) & ~15ull;
+        bt->direct.push_back({in, dsrc, p, rbase});
+        bt->direct_used = rbase + p;
+    }
     DecJob J{};
     J.a0 = (uint32_t)bt->dact.size();
     J.validate = d->validate ? 1u : 0u;
@@ -691,12 +731,15 @@ extern "C" int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx
     for (const SnappyAction& a : j->acts) {
         if (a.kind != SAct::Uncomp && a.kind != SAct::Comp) continue;
         uint64_t off = 0;
-        uint8_t* st = bt->stage(a.dlen, &off);
-        if (!st) {
-            delete j;
-            return NX_ERR_HIP;
+        if (registered) {
+            off = rbase + a.data;
+        } else {
+            uint8_t* st = bt->stage(a.dlen, &off);
+            if (!st) return fail(NX_ERR_HIP);
+            memcpy(st, in + a.data, a.dlen);
         }
-        memcpy(st, in + a.data, a.dlen);
+        const uint8_t dir = registered ? 1 : 0;
+        bt->dact_direct.push_back(dir);
         DecAct A{off, a.dlen, 0, 0, a.crc};
         if (a.kind == SAct::Comp) {
             A.kind = 2;
@@ -704,6 +747,7 @@ extern "C" int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx
             bt->dc_off.push_back(off);
             bt->dc_len.push_back(a.dlen);
             bt->dc_crc.push_back(a.crc);
+            bt->dc_direct.push_back(dir);
             if (d->validate) bt->dc_validate = true;
             out_need += 65536;
         } else {
@@ -711,21 +755,30 @@ extern "C" int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx
             A.chunk = (uint32_t)bt->du_off.size();
             bt->du_off.push_back(off);
             bt->du_len.push_back(a.dlen);
+            bt->du_direct.push_back(dir);
             out_need += a.dlen;
         }
         bt->dact.push_back(A);
     }
     J.na = (uint32_t)bt->dact.size() - J.a0;
-    if (!bt->reserve_out(out_need + 16, &J.out_off)) {
-        delete j;
-        return NX_ERR_HIP;
-    }
+    if (!bt->reserve_out(out_need + 16, &J.out_off)) return fail(NX_ERR_HIP);
     j->index = (uint32_t)bt->djob.size();
     bt->djob.push_back(J);
     bt->jobs.push_back(j);
     bt->live += 1;
     b->tickets[j->ticket] = {bt, j};
     return (int64_t)j->ticket;
+}
+}  // namespace
+
+extern "C" int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
+                                                  size_t* consumed) {
+    return decoder_submit(d, b, in, n, consumed, false);
+}
+
+extern "C" int64_t nx_snappy_frame_decoder_submit_registered(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
+                                                             size_t* consumed) {
+    return decoder_submit(d, b, in, n, consumed, true);
 }
 
 extern "C" int32_t nx_batcher_flush(nx_batcher* b) {

@@ -347,6 +347,16 @@ class Batcher:
         del decoder._cum[:consumed.value]
         return t
 
+    def submit_decode_registered(self, decoder: "SnappyFrameDecoder", ptr: int, n: int) -> tuple[int, int]:
+        """SnappyFrameDecoder.decode over a cumulation the caller holds in registered memory
+        (register()): nothing is copied; bytes [ptr, ptr + consumed) must stay valid until the job
+        completes.  Returns (ticket, consumed); the caller discards the consumed bytes afterwards."""
+        consumed = C.c_size_t(0)
+        t = _lib.load().nx_snappy_frame_decoder_submit_registered(decoder._h, self._h, C.c_void_p(ptr), n, C.byref(consumed))
+        if t < 0:
+            raise RuntimeError(f"nx_snappy_frame_decoder_submit_registered: {_lib.status_string(t)}")
+        return t, consumed.value
+
     def flush(self):
         r = _lib.load().nx_batcher_flush(self._h)
         if r != 0:

@@ -116,3 +116,54 @@ def test_batcher_registered_input(nx, oracle):
         assert b.result(t) == [oracle.snappy_frame_encode(data)[0]]
     finally:
         nx.Batcher.unregister(addr)
+
+
+def test_batcher_registered_cumulations(nx, oracle):
+    """Decoder cumulations in registered memory (nx_snappy_frame_decoder_submit_registered: the socket
+    read into a pooled direct buffer) are gathered at flush without the staging copy; mixed in one
+    batch with copied cumulations and a registered encoder input, every channel's messages are the
+    oracle's (compressed and uncompressed chunks, validating and not)."""
+    msgs = _messages(oracle, 48)
+    streams = []
+    for m in msgs:
+        f, _ = oracle.snappy_frame_encode(m)
+        streams.append(f if m else oracle.snappy_frame_encode(b"y")[0])
+    want = [m if m else b"y" for m in msgs]
+    blob = b"".join(streams)
+    buf = (C.c_uint8 * (len(blob) + 64)).from_buffer_copy(blob + bytes(64))
+    addr = C.addressof(buf)
+    enc_in = oracle.textgen_chunk(5, 200000)
+    ebuf = (C.c_uint8 * len(enc_in)).from_buffer_copy(enc_in)
+    eaddr = C.addressof(ebuf)
+    nx.Batcher.register(addr, len(blob) + 64)
+    nx.Batcher.register(eaddr, len(enc_in))
+    try:
+        b = nx.Batcher()
+        decs = [nx.SnappyFrameDecoder(i % 3 == 0) for i in range(len(msgs))]
+        te = b.submit_encode(nx.SnappyFrameEncoder(), memoryview(ebuf), registered_ptr=eaddr)
+        tickets, pos = [], 0
+        for i, (d, s) in enumerate(zip(decs, streams)):
+            if i % 4 == 3:  # a copied cumulation between registered ones
+                tickets.append(b.submit_decode(d, s))
+            else:
+                t, consumed = b.submit_decode_registered(d, addr + pos, len(s))
+                assert consumed == len(s)
+                tickets.append(t)
+            pos += len(s)
+        b.flush()
+        b.wait(tickets[-1])
+        b.wait(te)
+        for i, t in enumerate(tickets):
+            assert b"".join(b.result(t)) == want[i], i
+        assert b.result(te) == [oracle.snappy_frame_encode(enc_in)[0]]
+    finally:
+        nx.Batcher.unregister(addr)
+        nx.Batcher.unregister(eaddr)
+
+
+def test_batcher_registered_cumulation_outside_registration(nx, oracle):
+    f, _ = oracle.snappy_frame_encode(b"hello, world" * 10)
+    buf = (C.c_uint8 * len(f)).from_buffer_copy(f)
+    b = nx.Batcher()
+    with pytest.raises(RuntimeError, match="submit_registered"):
+        b.submit_decode_registered(nx.SnappyFrameDecoder(), C.addressof(buf), len(f))
