@@ -136,8 +136,9 @@ int32_t nx_fastlz_decompress_batch(const uint8_t* in, const uint64_t* in_off, co
 int32_t nx_adler32_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len,
                          uint32_t* out, uint32_t n, void* stream);
 
-/* Replaces LZFEncoder.appendEncoded(...) for one chunk (LzfEncoder.java:218-221): writes a complete
- * "ZV" block (compressed if it saves bytes, else non-compressed).  in_len[i] <= 65535.
+/* Replaces ChunkEncoder.appendEncodedChunk(...) as LZFEncoder.appendEncoded calls it per 65535-byte
+ * chunk (LzfEncoder.java:218-221; compress-lzf 1.0.3 ChunkEncoder.tryCompress, fresh table): writes
+ * a complete "ZV" block (compressed if it saves bytes, else non-compressed).  in_len[i] <= 65535.
  * PARITY UNPINNED vs com.ning:compress-lzf (third-party, not in the reference). */
 int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                             uint8_t* out, const uint64_t* out_off, uint32_t* out_len,

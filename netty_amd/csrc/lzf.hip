@@ -1,72 +1,87 @@
 // lzf.hip — LZF chunk encoder/decoder, batched (LzfEncoder.java:218-221 / LzfDecoder.java:205).
 //
-// The LZF block arithmetic lives in the third-party com.ning:compress-lzf:1.0.3, which is not in
-// /root/reference.  The decoder is format-exact (liblzf format: ctrl < 32 → literal run of
-// ctrl+1; else back-reference of (ctrl>>5)+2 [+ext] bytes at distance ((ctrl&31)<<8)+byte+1,
-// looping until outPos == outEnd as ChunkDecoder.decodeChunk does).  The encoder is the build's
-// own greedy hash encoder producing a valid "ZV" block (PARITY UNPINNED: no reference bytes
-// exist offline); it equals oracle/netty_oracle.c orc_lzf_encode_chunk byte for byte.
+// The LZF block arithmetic lives in the third-party com.ning:compress-lzf:1.0.3 (pom.xml:941-945),
+// which is not in /root/reference.  The decoder is format-exact (liblzf format: ctrl < 32 → literal
+// run of ctrl+1; else back-reference of (ctrl>>5)+2 [+ext] bytes at distance ((ctrl&31)<<8)+byte+1,
+// looping until outPos == outEnd as ChunkDecoder.decodeChunk does).  The encoder is ChunkEncoder.
+// tryCompress (what LzfEncoder.java:161-163,219 runs) as oracle/netty_oracle.c
+// orc_lzf_compress_body_ex restates it — hash ((seen * 57321) >> 9) & 16383 of the big-endian int
+// of bytes [p-1, p+2], 3-byte candidate check, MAX_OFF 8192, MAX_REF 264, matchEnd-2/-1 inserts —
+// byte for byte (PARITY UNPINNED vs the library itself: no reference bytes exist offline).
 #include "nx_common.hpp"
 
 namespace nx {
 namespace lzf {
 
-constexpr int HLOG = 14;
-constexpr int HSIZE = 1 << HLOG;
+constexpr int HSIZE = 16384;
 constexpr int32_t MAX_OFF = 8192;
 constexpr int32_t MAX_REF = 264;
 constexpr int32_t MAX_LIT = 32;
 
-__device__ __forceinline__ uint32_t hash3(uint32_t v) { return ((v * 2654435761u) >> (32 - HLOG)) & (HSIZE - 1); }
+// ChunkEncoder.hash: Java int multiply (wraps), arithmetic shift
+__device__ __forceinline__ uint32_t jhash(int32_t h) { return (uint32_t)(((int32_t)((uint32_t)h * 57321u) >> 9) & (HSIZE - 1)); }
+__device__ __forceinline__ int32_t first2(const uint8_t* in, int32_t p) {  // ChunkEncoder.first: (in[p] << 8) + (in[p+1] & 0xFF), in[p] signed
+    return (int32_t)((uint32_t)(int32_t)(int8_t)in[p] << 8) + in[p + 1];
+}
 
-// returns body length; htab entries: (stamp << 16) | (pos + 1), 0 = empty (-1 in the oracle)
+// Returns body length.  htab entries: (stamp << 16) | (position + 1); a stamp mismatch is the Java
+// zero (position 0).  Whether the chunk starts the Java array or continues a message does not change
+// the bytes: a never-written slot or an earlier chunk's entry can never pass the 3-byte check
+// (oracle/netty_oracle.c orc_lzf_compress_body).
 __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, uint8_t* __restrict__ out, uint32_t* __restrict__ htab,
                                  uint32_t stamp) {
     const uint32_t stag = stamp << 16;
-    int32_t ip = 0, op = 0, lit = 0;
-    op++;
-    while (ip + 2 < n) {
-        const uint32_t seq = ((uint32_t)in[ip] << 16) | ((uint32_t)in[ip + 1] << 8) | in[ip + 2];
-        const uint32_t h = hash3(seq);
+    const int32_t inEnd = n - 4;
+    int32_t ip = 0, op = 1, lit = 0;
+    int32_t seen = first2(in, 0);
+    while (ip < inEnd) {
+        const uint8_t p2 = in[ip + 2];
+        seen = (int32_t)(((uint32_t)seen << 8) + p2);
+        const uint32_t h = jhash(seen);
         const uint32_t e = htab[h];
-        const int32_t ref = ((e & 0xFFFF0000u) == stag) ? (int32_t)(e & 0xFFFFu) - 1 : -1;
+        const int32_t ref = ((e & 0xFFFF0000u) == stag) ? (int32_t)(e & 0xFFFFu) - 1 : 0;
         htab[h] = stag | (uint32_t)(ip + 1);
-        const int32_t off = ip - ref - 1;
-        if (ref >= 0 && off < MAX_OFF && in[ref] == in[ip] && in[ref + 1] == in[ip + 1] && in[ref + 2] == in[ip + 2]) {
-            int32_t maxlen = n - ip;
-            if (maxlen > MAX_REF) maxlen = MAX_REF;
-            int32_t len = 3;
-            while (len < maxlen && in[ref + len] == in[ip + len]) len++;
-            if (lit) {
-                out[op - lit - 1] = (uint8_t)(lit - 1);
-            } else {
-                op--;
-            }
-            lit = 0;
-            const int32_t l2 = len - 2;
-            if (l2 < 7) {
-                out[op++] = (uint8_t)((off >> 8) + (l2 << 5));
-            } else {
-                out[op++] = (uint8_t)((off >> 8) + (7 << 5));
-                out[op++] = (uint8_t)(l2 - 7);
-            }
-            out[op++] = (uint8_t)off;
-            op++;
-            ip += len;
-            if (ip + 2 < n) {
-                const uint32_t s1 = ((uint32_t)in[ip - 1] << 16) | ((uint32_t)in[ip] << 8) | in[ip + 1];
-                htab[hash3(s1)] = stag | (uint32_t)(ip - 1 + 1);
+        int32_t off = ip - ref;
+        if (ref < 0 || ref >= ip || off > MAX_OFF || in[ref + 2] != p2 || in[ref + 1] != (uint8_t)(seen >> 8) ||
+            in[ref] != (uint8_t)(seen >> 16)) {
+            out[op++] = in[ip++];
+            if (++lit == MAX_LIT) {
+                out[op - 33] = 31;
+                lit = 0;
+                op++;
             }
             continue;
         }
-        out[op++] = in[ip++];
-        if (++lit == MAX_LIT) {
+        int32_t maxLen = inEnd - ip + 2;
+        if (maxLen > MAX_REF) maxLen = MAX_REF;
+        if (lit == 0) {
+            op--;
+        } else {
             out[op - lit - 1] = (uint8_t)(lit - 1);
             lit = 0;
-            op++;
         }
+        int32_t len = 3;
+        while (len < maxLen && in[ref + len] == in[ip + len]) len++;
+        len -= 2;
+        --off;
+        if (len < 7) {
+            out[op++] = (uint8_t)((off >> 8) + (len << 5));
+        } else {
+            out[op++] = (uint8_t)((off >> 8) + (7 << 5));
+            out[op++] = (uint8_t)(len - 7);
+        }
+        out[op++] = (uint8_t)off;
+        op++;
+        ip += len;  // matchEnd - 2 (<= n - 4)
+        seen = first2(in, ip);
+        seen = (int32_t)(((uint32_t)seen << 8) + in[ip + 2]);
+        htab[jhash(seen)] = stag | (uint32_t)(ip + 1);
+        ++ip;
+        seen = (int32_t)(((uint32_t)seen << 8) + in[ip + 2]);
+        htab[jhash(seen)] = stag | (uint32_t)(ip + 1);
+        ++ip;
     }
-    while (ip < n) {
+    while (ip < n) {  // handleTail
         out[op++] = in[ip++];
         if (++lit == MAX_LIT) {
             out[op - lit - 1] = (uint8_t)(lit - 1);

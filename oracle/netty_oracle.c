@@ -714,7 +714,7 @@ size_t orc_fastlz_frame_encode(const uint8_t* buf, size_t r0, size_t n, int leve
  * LZF — format restated from liblzf / com.ning:compress-lzf 1.0.3 (third party, not in
  * /root/reference).  Decoder: ChunkDecoder.decodeChunk semantics as called from
  * LzfDecoder.java:205 (loop until outPos == outEnd; overrun/underrun/bad ref → error).
- * Encoder: the build's own greedy hash encoder (PARITY UNPINNED — no reference bytes).
+ * Encoder: ChunkEncoder.tryCompress restated below (PARITY UNPINNED — no reference bytes).
  * ===================================================================================== */
 int32_t orc_lzf_decode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out, int32_t out_len) {
     int32_t ip = 0, op = 0;
@@ -745,59 +745,84 @@ int32_t orc_lzf_decode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out, in
     return op == out_len ? NX_OK : NX_ERR_LZF_CORRUPT;
 }
 
-#define LZF_HLOG 14
+/* compress-lzf 1.0.3 ChunkEncoder.tryCompress (com.ning:compress-lzf, pom.xml:941-945; not vendored).
+ * Netty's LzfEncoder takes ChunkEncoderFactory.optimalNonAllocatingInstance (LzfEncoder.java:161-163)
+ * → UnsafeChunkEncoderLE on x86, whose output equals the safe ChunkEncoder's restated here:
+ *   - int[16384] table (calcHashLen(max(65535, ...)) for the default totalLength = MAX_CHUNK_LEN),
+ *     zero-initialised, entries = absolute input positions; hash(h) = ((h * 57321) >> 9) & 16383 on
+ *     Java int (wrapping multiply, arithmetic shift) of `seen` = the big-endian int of the bytes
+ *     [p-1, p, p+1, p+2] (at the first probe and after a match its top byte is the sign of in[p]);
+ *   - a candidate ref is taken iff firstPos <= ref < p, p - ref <= MAX_OFF (8192) and the 3 bytes at
+ *     ref equal those at p.  The hash depends only on the low 23 bits of `seen` (bytes p+1, p+2 and
+ *     7 bits of p), and the first probe (p = firstPos) writes its slot, so a never-written slot (a
+ *     Java zero, array position 0) or an entry of an earlier chunk (< firstPos) can never pass the
+ *     3-byte check: every chunk encodes as with a fresh table, whatever its position in the message;
+ *   - matches extend to min(MAX_REF = 264, inEnd - p + 2) bytes (inEnd = end - TAIL_LENGTH 4), are
+ *     emitted as (len-2, off-1), and insert positions matchEnd-2 and matchEnd-1;
+ *   - literal runs of at most 32 bytes, the header byte reserved ahead (handleTail for the last 4).
+ * PARITY UNPINNED: no reference bytes exist offline (LzfEncoderTest.java:31-38 only round-trips).
+ * A long-lived Java encoder keeps its table across messages, so a later message may take an older
+ * (still valid) match than a fresh table would; this restates a fresh encoder's output. */
+#define LZF_HSIZE 16384
 #define LZF_MAX_OFF 8192
 #define LZF_MAX_REF 264
 #define LZF_MAX_LIT 32
 
-static inline uint32_t lzf_hash(uint32_t v) { return ((v * 2654435761u) >> (32 - LZF_HLOG)) & ((1u << LZF_HLOG) - 1); }
+static inline int32_t lzf_jhash(int32_t h) { return ((int32_t)((uint32_t)h * 57321u) >> 9) & (LZF_HSIZE - 1); }
 
 int32_t orc_lzf_compress_body(const uint8_t* in, int32_t n, uint8_t* out) {
-    int32_t* htab = (int32_t*)malloc(sizeof(int32_t) << LZF_HLOG);
-    for (int i = 0; i < (1 << LZF_HLOG); ++i) htab[i] = -1;
-    int32_t ip = 0, op = 0, lit = 0;
-    op++; /* literal-length placeholder */
-    while (ip + 2 < n) {
-        uint32_t seq = ((uint32_t)in[ip] << 16) | ((uint32_t)in[ip + 1] << 8) | in[ip + 2];
-        uint32_t h = lzf_hash(seq);
-        int32_t ref = htab[h];
-        htab[h] = ip;
-        int32_t off = ip - ref - 1;
-        if (ref >= 0 && off < LZF_MAX_OFF && in[ref] == in[ip] && in[ref + 1] == in[ip + 1] &&
-            in[ref + 2] == in[ip + 2]) {
-            int32_t maxlen = n - ip;
-            if (maxlen > LZF_MAX_REF) maxlen = LZF_MAX_REF;
-            int32_t len = 3;
-            while (len < maxlen && in[ref + len] == in[ip + len]) len++;
-            if (lit) {
-                out[op - lit - 1] = (uint8_t)(lit - 1);
-            } else {
-                op--;
-            }
-            lit = 0;
-            int32_t l2 = len - 2;
-            if (l2 < 7) {
-                out[op++] = (uint8_t)((off >> 8) + (l2 << 5));
-            } else {
-                out[op++] = (uint8_t)((off >> 8) + (7 << 5));
-                out[op++] = (uint8_t)(l2 - 7);
-            }
-            out[op++] = (uint8_t)off;
-            op++; /* next literal placeholder */
-            ip += len;
-            if (ip + 2 < n) {
-                uint32_t s1 = ((uint32_t)in[ip - 1] << 16) | ((uint32_t)in[ip] << 8) | in[ip + 1];
-                htab[lzf_hash(s1)] = ip - 1;
+    int32_t* ht = (int32_t*)calloc(LZF_HSIZE, sizeof(int32_t)); /* position + 1; 0 = the Java zero */
+    int32_t ip = 0, op = 1, lit = 0; /* ++outPos: literal-length byte reserved */
+    const int32_t inEnd = n - 4;
+    int32_t seen = (int32_t)((uint32_t)(int32_t)(int8_t)in[0] << 8) + in[1]; /* first(in, inPos) */
+    while (ip < inEnd) {
+        const uint8_t p2 = in[ip + 2];
+        seen = (int32_t)(((uint32_t)seen << 8) + p2);
+        const int32_t h = lzf_jhash(seen);
+        const int32_t e = ht[h];
+        const int32_t ref = e ? e - 1 : 0;
+        ht[h] = ip + 1;
+        int32_t off = ip - ref;
+        if (ref < 0 || ref >= ip || off > LZF_MAX_OFF || in[ref + 2] != p2 || in[ref + 1] != (uint8_t)(seen >> 8) ||
+            in[ref] != (uint8_t)(seen >> 16)) {
+            out[op++] = in[ip++];
+            if (++lit == LZF_MAX_LIT) {
+                out[op - 33] = 31;
+                lit = 0;
+                op++;
             }
             continue;
         }
-        out[op++] = in[ip++];
-        if (++lit == LZF_MAX_LIT) {
+        int32_t maxLen = inEnd - ip + 2;
+        if (maxLen > LZF_MAX_REF) maxLen = LZF_MAX_REF;
+        if (lit == 0) {
+            op--; /* unreserve */
+        } else {
             out[op - lit - 1] = (uint8_t)(lit - 1);
             lit = 0;
-            op++;
         }
+        int32_t len = 3;
+        while (len < maxLen && in[ref + len] == in[ip + len]) len++;
+        len -= 2;
+        --off;
+        if (len < 7) {
+            out[op++] = (uint8_t)((off >> 8) + (len << 5));
+        } else {
+            out[op++] = (uint8_t)((off >> 8) + (7 << 5));
+            out[op++] = (uint8_t)(len - 7);
+        }
+        out[op++] = (uint8_t)off;
+        op++;
+        ip += len; /* matchEnd - 2 (<= n - 4) */
+        seen = (int32_t)((uint32_t)(int32_t)(int8_t)in[ip] << 8) + in[ip + 1];
+        seen = (int32_t)(((uint32_t)seen << 8) + in[ip + 2]);
+        ht[lzf_jhash(seen)] = ip + 1;
+        ++ip;
+        seen = (int32_t)(((uint32_t)seen << 8) + in[ip + 2]);
+        ht[lzf_jhash(seen)] = ip + 1;
+        ++ip;
     }
+    /* handleTail */
     while (ip < n) {
         out[op++] = in[ip++];
         if (++lit == LZF_MAX_LIT) {
@@ -811,11 +836,12 @@ int32_t orc_lzf_compress_body(const uint8_t* in, int32_t n, uint8_t* out) {
     } else {
         op--;
     }
-    free(htab);
+    free(ht);
     return op;
 }
 
-/* One LZFChunk: compressed "ZV 01 clen ulen body" if it beats "ZV 00 len data", else the latter. */
+/* One LZFChunk (ChunkEncoder.appendEncodedChunk): compressed "ZV 01 clen ulen body" if it beats
+ * "ZV 00 len data", else the latter. */
 size_t orc_lzf_encode_chunk(const uint8_t* in, int32_t n, uint8_t* out) {
     if (n >= 16) {
         int32_t clen = orc_lzf_compress_body(in, n, out + 7);

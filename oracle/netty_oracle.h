@@ -68,7 +68,8 @@ size_t orc_lzf_encode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out);
 /* LZF compressed-chunk body decoder (ChunkDecoder.decodeChunk semantics). Returns NX_OK or
  * NX_ERR_LZF_CORRUPT; writes exactly out_len bytes on success. */
 int32_t orc_lzf_decode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out, int32_t out_len);
-/* Raw LZF body compressor used by orc_lzf_encode_chunk; returns body length (may exceed in_len). */
+/* Raw LZF body compressor (compress-lzf 1.0.3 ChunkEncoder.tryCompress) used by orc_lzf_encode_chunk;
+ * returns body length (may exceed in_len). */
 int32_t orc_lzf_compress_body(const uint8_t* in, int32_t in_len, uint8_t* out);
 size_t orc_lzf_frame_encode(const uint8_t* in, size_t n, int32_t compress_threshold, uint8_t* out);
 size_t orc_lzf_frame_max_encoded(size_t n);

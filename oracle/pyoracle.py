@@ -175,6 +175,7 @@ def fastlz_frame_encode(data: bytes, level: int = 0, checksum: bool = False, r0:
 
 # ---------------------------------------------------------------- LZF
 def lzf_encode_chunk(data: bytes) -> bytes:
+    """One LZFChunk as ChunkEncoder.appendEncodedChunk writes it (compress-lzf 1.0.3, fresh table)."""
     out = _buf(len(data) + len(data) // 32 + 64)
     n = lib().orc_lzf_encode_chunk(bytes(data), len(data), out)
     return bytes(out[:n])

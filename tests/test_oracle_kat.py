@@ -182,6 +182,89 @@ def test_lzf_roundtrip(oracle):
     assert oracle.lzf_decode_chunk(bytes([0x20, 0x05]), 3)[0] == -30
 
 
+def _lzf_try_compress_py(inp: bytes) -> bytes:
+    """Second, independent restatement of compress-lzf 1.0.3 ChunkEncoder.tryCompress (Java int
+    arithmetic spelled out) to cross-check the C oracle's transcription (parity unpinned vs the
+    library itself, which is not available offline)."""
+    def i32(x):
+        x &= 0xFFFFFFFF
+        return x - (1 << 32) if x >= 1 << 31 else x
+
+    def jhash(h):  # ((h * 57321) >> 9) & _hashModulo, _hashModulo = 16383
+        return (i32(h * 57321) >> 9) & 16383
+
+    def first(p):  # (in[p] << 8) + (in[p + 1] & 0xFF), in[] signed
+        b = inp[p] - 256 if inp[p] >= 128 else inp[p]
+        return i32((b << 8) + inp[p + 1])
+
+    n = len(inp)
+    ht = [0] * 16384
+    out = bytearray(2 * n + 64)
+    ip, op, lit, in_end = 0, 1, 0, n - 4
+    seen = first(0)
+    while ip < in_end:
+        p2 = inp[ip + 2]
+        seen = i32((seen << 8) + p2)
+        h = jhash(seen)
+        ref = ht[h]
+        ht[h] = ip
+        off = ip - ref
+        if (ref >= ip or off > 8192 or inp[ref + 2] != p2 or inp[ref + 1] != (seen >> 8) & 255
+                or inp[ref] != (seen >> 16) & 255):
+            out[op] = inp[ip]
+            op, ip, lit = op + 1, ip + 1, lit + 1
+            if lit == 32:
+                out[op - 33] = 31
+                lit, op = 0, op + 1
+            continue
+        max_len = min(264, in_end - ip + 2)
+        if lit == 0:
+            op -= 1
+        else:
+            out[op - lit - 1] = lit - 1
+            lit = 0
+        ln = 3
+        while ln < max_len and inp[ref + ln] == inp[ip + ln]:
+            ln += 1
+        ln, off = ln - 2, off - 1
+        if ln < 7:
+            out[op] = ((off >> 8) + (ln << 5)) & 255
+            op += 1
+        else:
+            out[op], out[op + 1] = ((off >> 8) + (7 << 5)) & 255, ln - 7
+            op += 2
+        out[op] = off & 255
+        op += 2
+        ip += ln
+        seen = i32((first(ip) << 8) + inp[ip + 2])
+        ht[jhash(seen)] = ip
+        ip += 1
+        seen = i32((seen << 8) + inp[ip + 2])
+        ht[jhash(seen)] = ip
+        ip += 1
+    while ip < n:  # handleTail
+        out[op] = inp[ip]
+        op, ip, lit = op + 1, ip + 1, lit + 1
+        if lit == 32:
+            out[op - lit - 1] = lit - 1
+            lit, op = 0, op + 1
+    if lit:
+        out[op - lit - 1] = lit - 1
+    else:
+        op -= 1
+    return bytes(out[:op])
+
+
+def test_lzf_encoder_restatements_agree(oracle):
+    import random
+    r = random.Random(7)
+    cases = [oracle.textgen_chunk(3, 6000), bytes(3000), bytes(r.randrange(4) for _ in range(4000)),
+             bytes(r.randrange(256) for _ in range(999)), b"ab" * 700 + bytes(range(256)) * 3,
+             bytes(r.randrange(3) | 0x80 for _ in range(2000)), bytes(16), b"abc" + b"xyz" * 30 + b"abcd" * 40]
+    for c in cases:
+        assert oracle.lzf_compress_body(c) == _lzf_try_compress_py(c)
+
+
 def test_textgen_deterministic(oracle):
     a = oracle.textgen_chunk(0, 65536)
     assert a == oracle.textgen_chunk(0, 65536) and a != oracle.textgen_chunk(1, 65536)
