@@ -343,6 +343,12 @@ int32_t nx_batcher_wait(nx_batcher* b, int64_t ticket);  /* blocks (flushes firs
 int32_t nx_batcher_result(nx_batcher* b, int64_t ticket, const nx_msg** msgs, size_t* n_msgs, const char** err_msg);
 int32_t nx_batcher_release(nx_batcher* b, int64_t ticket);
 int32_t nx_batcher_stats(nx_batcher* b, uint64_t* flushes, uint64_t* launches, uint64_t* chunks);
+/* Auto-flush: once the collecting batch holds `bytes` of input (copied payloads + registered ranges),
+ * the submit that crossed the threshold launches it (0 = off, the default: only flush() launches).
+ * Flushes rotate over four HIP streams, so a launched batch's PCIe traffic (gather from registered
+ * pages, results into mapped memory) overlaps the next batch's kernels; results are applied in flush
+ * order, so per-decoder semantics are those of one serial execution. */
+int32_t nx_batcher_set_flush_bytes(nx_batcher* b, size_t bytes);
 
 #ifdef __cplusplus
 }

@@ -71,6 +71,7 @@ _SIGS = {
     "nx_batcher_result": (i32, [vp, i64, C.POINTER(C.POINTER(NxMsg)), C.POINTER(sz), C.POINTER(C.c_char_p)]),
     "nx_batcher_release": (i32, [vp, i64]),
     "nx_batcher_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]),
+    "nx_batcher_set_flush_bytes": (i32, [vp, sz]),
     # host handler layer
     "nx_snappy_frame_encoder_new": (vp, [i32]),
     "nx_snappy_frame_encoder_free": (None, [vp]),

@@ -17,6 +17,11 @@
 //           job's result — framed encoder output, or the decoder's messages — straight into mapped
 //           pinned host memory (only the result bytes cross PCIe; no D2H of capacity-sized slots).
 //   poll    hipEventQuery: 1 when the job's batch is done (never blocks); wait() blocks (tests).
+//   streams flushes go round-robin to kStreams HIP streams, so one batch's host gather / result
+//           writes (PCIe) overlap the next batch's kernels; results are still APPLIED in flush order
+//           (a later batch waits for the earlier ones), which keeps each decoder's corrupted state
+//           exactly as a serial execution would leave it.  An optional auto-flush threshold
+//           (nx_batcher_set_flush_bytes) launches the collecting batch once its input reaches it.
 //   result  zero-copy views of the job's output in the pinned arena, valid until release().
 //
 // Results are applied in submission order per decoder: a failing chunk marks the decoder corrupted
@@ -260,6 +265,7 @@ struct Batch {
     std::vector<Job*> jobs;
     nx::h::DevBuf din, slots, gops;
     hipEvent_t ev = nullptr;
+    uint64_t seq = 0;  // flush order
     bool inflight = false, done = false;
     size_t live = 0;  // jobs not yet released
     void reset() {
@@ -324,21 +330,26 @@ const uint8_t* registered_device_ptr(const uint8_t* p, size_t n) {
 }
 }  // namespace
 
+constexpr int kStreams = 4;
 struct nx_batcher {
     std::mutex mu;
-    hipStream_t s = nullptr;
+    hipStream_t s[kStreams] = {};
     std::deque<Batch*> all;  // every batch object (collecting, in flight, or done)
     Batch* cur = nullptr;    // the collecting batch
     std::unordered_map<uint64_t, std::pair<Batch*, Job*>> tickets;
     uint64_t next_ticket = 1;
     uint64_t launches = 0, chunks = 0, flushes = 0;
+    uint64_t applied = 0;     // batches applied, in flush order (Batch::seq < applied)
+    size_t flush_bytes = 0;   // auto-flush threshold on a batch's input bytes (0 = only explicit flushes)
 };
 
 namespace {
 
+bool advance(nx_batcher* b, uint64_t upto, bool block);
+
 Batch* fresh_batch(nx_batcher* b) {
+    advance(b, ~0ull, false);  // apply every completed batch (in flush order), even if its jobs were released unpolled
     for (Batch* x : b->all) {
-        if (x->inflight && x->live == 0 && hipEventQuery(x->ev) == hipSuccess) x->inflight = false;  // released unpolled
         if (!x->inflight && x->live == 0 && x != b->cur) {
             x->reset();
             return x;
@@ -360,7 +371,7 @@ Batch* collecting(nx_batcher* b) {
 
 // Launch everything `bt` collected (batcher lock held).
 int32_t launch(nx_batcher* b, Batch* bt) {
-    const hipStream_t s = b->s;
+    const hipStream_t s = b->s[b->flushes % kStreams];
     const uint32_t nes = (uint32_t)bt->esl.size(), nej = (uint32_t)bt->ejob.size(), nda = (uint32_t)bt->dact.size();
     const uint32_t ndj = (uint32_t)bt->djob.size(), ndc = (uint32_t)bt->dc_off.size(), ndu = (uint32_t)bt->du_off.size();
     struct Lay {
@@ -475,6 +486,7 @@ int32_t launch(nx_batcher* b, Batch* bt) {
     }
     if (hipEventRecord(bt->ev, s) != hipSuccess) return NX_ERR_HIP;
     bt->inflight = true;
+    bt->seq = b->flushes;
     b->flushes += 1;
     return NX_OK;
 }
@@ -534,15 +546,34 @@ void apply(Batch* bt) {
     bt->done = true;
 }
 
-bool poll_batch(Batch* bt, bool block) {
+// Apply completed batches in flush order up to (and including) sequence number `upto`; false if one
+// of them is not complete (non-blocking) or failed.
+bool advance(nx_batcher* b, uint64_t upto, bool block) {
+    while (b->applied <= upto && b->applied < b->flushes) {
+        Batch* bt = nullptr;
+        for (Batch* x : b->all)
+            if (x->inflight && x->seq == b->applied) bt = x;
+        if (!bt) return false;  // unreachable: every launched batch stays in flight until applied
+        const hipError_t e = block ? hipEventSynchronize(bt->ev) : hipEventQuery(bt->ev);
+        if (e != hipSuccess) return false;
+        apply(bt);
+        bt->inflight = false;
+        b->applied += 1;
+    }
+    return true;
+}
+
+bool poll_batch(nx_batcher* b, Batch* bt, bool block) {
     if (bt->done) return true;
     if (!bt->inflight) return false;
-    const hipError_t e = block ? hipEventSynchronize(bt->ev) : hipEventQuery(bt->ev);
-    if (e == hipErrorNotReady) return false;
-    if (e != hipSuccess) return false;
-    apply(bt);
-    bt->inflight = false;
-    return true;
+    return advance(b, bt->seq, block) && bt->done;
+}
+
+// Auto-flush: launch the collecting batch once its input reaches the threshold (batcher lock held).
+int32_t maybe_autoflush(nx_batcher* b, Batch* bt) {
+    if (!b->flush_bytes || bt != b->cur || bt->st_used + bt->direct_used < b->flush_bytes) return NX_OK;
+    b->cur = nullptr;
+    return launch(b, bt);
 }
 
 }  // namespace
@@ -553,18 +584,21 @@ extern "C" nx_batcher* nx_batcher_new(void) {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return nullptr;
     if (nx::crc_tables_init() != NX_OK) return nullptr;
     auto* b = new nx_batcher();
-    if (hipStreamCreateWithFlags(&b->s, hipStreamNonBlocking) != hipSuccess) {
-        delete b;
-        return nullptr;
+    for (int i = 0; i < kStreams; ++i) {
+        if (hipStreamCreateWithFlags(&b->s[i], hipStreamNonBlocking) != hipSuccess) {
+            for (int k = 0; k < i; ++k) (void)hipStreamDestroy(b->s[k]);
+            delete b;
+            return nullptr;
+        }
     }
     return b;
 }
 
 extern "C" void nx_batcher_free(nx_batcher* b) {
     if (!b) return;
-    (void)hipStreamSynchronize(b->s);
+    for (int i = 0; i < kStreams; ++i) (void)hipStreamSynchronize(b->s[i]);
     for (Batch* x : b->all) delete x;
-    (void)hipStreamDestroy(b->s);
+    for (int i = 0; i < kStreams; ++i) (void)hipStreamDestroy(b->s[i]);
     delete b;
 }
 
@@ -663,7 +697,8 @@ extern "C" int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx
     bt->jobs.push_back(j);
     bt->live += 1;
     b->tickets[j->ticket] = {bt, j};
-    return (int64_t)j->ticket;
+    const int32_t r = maybe_autoflush(b, bt);
+    return r == NX_OK ? (int64_t)j->ticket : (int64_t)r;
 }
 
 namespace {
@@ -767,7 +802,8 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
     bt->jobs.push_back(j);
     bt->live += 1;
     b->tickets[j->ticket] = {bt, j};
-    return (int64_t)j->ticket;
+    const int32_t r = maybe_autoflush(b, bt);
+    return r == NX_OK ? (int64_t)j->ticket : (int64_t)r;
 }
 }  // namespace
 
@@ -795,7 +831,7 @@ extern "C" int32_t nx_batcher_poll(nx_batcher* b, int64_t ticket) {
     std::lock_guard<std::mutex> lk(b->mu);
     auto it = b->tickets.find((uint64_t)ticket);
     if (it == b->tickets.end()) return NX_ERR_INVALID_ARG;
-    return poll_batch(it->second.first, false) ? 1 : 0;
+    return poll_batch(b, it->second.first, false) ? 1 : 0;
 }
 
 extern "C" int32_t nx_batcher_wait(nx_batcher* b, int64_t ticket) {
@@ -814,7 +850,7 @@ extern "C" int32_t nx_batcher_wait(nx_batcher* b, int64_t ticket) {
     }
     if (hipEventSynchronize(bt->ev) != hipSuccess) return NX_ERR_HIP;
     std::lock_guard<std::mutex> lk(b->mu);
-    return poll_batch(bt, true) ? NX_OK : NX_ERR_HIP;
+    return poll_batch(b, bt, true) ? NX_OK : NX_ERR_HIP;
 }
 
 extern "C" int32_t nx_batcher_result(nx_batcher* b, int64_t ticket, const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {
@@ -838,6 +874,13 @@ extern "C" int32_t nx_batcher_release(nx_batcher* b, int64_t ticket) {
     Batch* bt = it->second.first;
     b->tickets.erase(it);
     if (bt->live) bt->live -= 1;
+    return NX_OK;
+}
+
+extern "C" int32_t nx_batcher_set_flush_bytes(nx_batcher* b, size_t bytes) {
+    if (!b) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    b->flush_bytes = bytes;
     return NX_OK;
 }
 

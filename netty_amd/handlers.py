@@ -311,8 +311,14 @@ class Batcher:
     encode()/decode() calls of many SnappyFrameEncoder / SnappyFrameDecoder instances become jobs of
     one GPU launch per flush().  submit_* never touches the GPU; poll() never blocks."""
 
-    def __init__(self):
+    def __init__(self, flush_bytes: int = 0):
         self._h = _new(_lib.load().nx_batcher_new(), "Batcher")
+        if flush_bytes:
+            self.set_flush_bytes(flush_bytes)
+
+    def set_flush_bytes(self, n: int):
+        """Auto-flush once the collecting batch holds n input bytes (0 = only flush())."""
+        _lib.load().nx_batcher_set_flush_bytes(self._h, n)
 
     def close(self):
         if self._h:

@@ -8,7 +8,10 @@
 // timed twice per round, through nx_snappy_frame_decoder_submit_registered (payloads gathered from
 // the mapped pages at flush) and through nx_snappy_frame_decoder_submit (payloads copied at
 // submit), each by its own set of decoders.  Prints one JSON object.
-// Usage: e2e_capi [C] [M] [S] [rounds]
+// flush_mib > 0 sets the batcher's auto-flush threshold (nx_batcher_set_flush_bytes): batches of that
+// many MiB launch while later messages are still being submitted, rotating over the batcher's
+// streams, so PCIe traffic and kernels of consecutive batches overlap.
+// Usage: e2e_capi [C] [M] [S] [rounds] [flush_mib]
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -22,6 +25,7 @@ static double now() { return std::chrono::duration<double>(std::chrono::steady_c
 int main(int argc, char** argv) {
     const int C = argc > 1 ? atoi(argv[1]) : 256, M = argc > 2 ? atoi(argv[2]) : 256, S = argc > 3 ? atoi(argv[3]) : 65535;
     const int R = argc > 4 ? atoi(argv[4]) : 3;
+    const size_t flush_mib = argc > 5 ? (size_t)atol(argv[5]) : 0;
     const size_t N = (size_t)C * M, U = N * (size_t)S;
     uint8_t* in = (uint8_t*)aligned_alloc(4096, (U + 4095) / 4096 * 4096);
     static nx_textgen_tables tg;
@@ -34,6 +38,7 @@ int main(int argc, char** argv) {
         return 1;
     }
     nx_batcher* b = nx_batcher_new();
+    if (b && flush_mib) nx_batcher_set_flush_bytes(b, flush_mib << 20);
     std::vector<nx_snappy_frame_encoder*> enc(C);
     std::vector<nx_snappy_frame_decoder*> dec(C), dec2(C);
     for (int c = 0; c < C; ++c) {
@@ -157,9 +162,9 @@ int main(int argc, char** argv) {
            "\"decode_copied_gib_s\": %.3f, \"encode_s\": %.4f, \"decode_s\": %.4f, \"decode_copied_s\": %.4f, "
            "\"phases_s\": {\"encode_submit\": %.4f, \"encode_flush_wait\": %.4f, \"decode_submit\": %.4f, "
            "\"decode_flush_wait\": %.4f, \"decode_copied_submit\": %.4f, \"decode_copied_flush_wait\": %.4f}, "
-           "\"flushes\": %llu, \"launches\": %llu, \"verified\": %s}\n",
+           "\"flush_mib\": %zu, \"flushes\": %llu, \"launches\": %llu, \"verified\": %s}\n",
            C, M, S, U, comp_total, g / best_e, g / best_d, g / (best_e + best_d), g / best_dc, best_e, best_d, best_dc, ph[0], ph[1],
-           ph[2], ph[3], ph[4], ph[5], (unsigned long long)fl, (unsigned long long)la, ok ? "true" : "false");
+           ph[2], ph[3], ph[4], ph[5], flush_mib, (unsigned long long)fl, (unsigned long long)la, ok ? "true" : "false");
     for (int c = 0; c < C; ++c) {
         nx_snappy_frame_encoder_free(enc[c]);
         nx_snappy_frame_decoder_free(dec[c]);

@@ -167,3 +167,37 @@ def test_batcher_registered_cumulation_outside_registration(nx, oracle):
     b = nx.Batcher()
     with pytest.raises(RuntimeError, match="submit_registered"):
         b.submit_decode_registered(nx.SnappyFrameDecoder(), C.addressof(buf), len(f))
+
+
+def test_batcher_autoflush_ordered_across_streams(nx, oracle):
+    """Auto-flush (nx_batcher_set_flush_bytes): batches launch while later calls are submitted and
+    rotate over the batcher's streams, yet results are applied in flush order: a decoder that fails in
+    an early batch delivers nothing from its later jobs in later batches (SnappyFrameDecoder.java:86-89,
+    227-230), and every other channel's bytes equal the oracle's."""
+    msgs = _messages(oracle, 40)
+    b = nx.Batcher(flush_bytes=256 * 1024)
+    encs = [nx.SnappyFrameEncoder() for _ in msgs]
+    et = [b.submit_encode(e, m) for e, m in zip(encs, msgs)]
+    assert b.stats()["flushes"] >= 4  # several batches launched during the submits
+    data = oracle.textgen_chunk(21, 300000)
+    f, _ = oracle.snappy_frame_encode(data)
+    bad = bytearray(f)
+    bad[10 + 4] ^= 0xFF
+    d_bad, d_ok = nx.SnappyFrameDecoder(True), nx.SnappyFrameDecoder(True)
+    t_bad = b.submit_decode(d_bad, bytes(bad))
+    t_ok = [b.submit_decode(d_ok, f[k:k + 50000]) for k in range(0, len(f), 50000)]
+    fill = [b.submit_encode(nx.SnappyFrameEncoder(), oracle.textgen_chunk(30 + i, 200000)) for i in range(4)]
+    t_after = b.submit_decode(d_bad, f[10:])  # a later batch, same failed decoder
+    b.flush()
+    assert b.stats()["flushes"] >= 7
+    b.wait(t_after)
+    for t in fill:
+        b.wait(t)
+    for i, (t, m) in enumerate(zip(et, msgs)):
+        b.wait(t)
+        want, _ = oracle.snappy_frame_encode(m, started=not m)
+        assert b.result(t) == ([b""] if not m else [want]), i
+    with pytest.raises(nx.DecompressionException, match="mismatching checksum"):
+        b.result(t_bad)
+    assert b"".join(b"".join(b.result(t)) for t in t_ok) == data
+    assert b.result(t_after) == []
