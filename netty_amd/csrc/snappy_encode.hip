@@ -148,7 +148,8 @@ __device__ __forceinline__ void enc_copy(Wr& w, int32_t offset, int32_t length) 
     enc_copy_off(w, offset, length);
 }
 
-// Register window over the lane's own input stream: 32 bytes from a 16-byte-aligned address.
+// Register window over the lane's own input stream: 32 bytes from a 16-byte-aligned address, plus
+// the following 16-byte block prefetched one slide ahead.
 // The scan front moves 1-2 bytes per probe, so one refill (two 16-byte loads) serves the next
 // 10-25 stream reads that would otherwise each be a separate memory request; with 262 144 lanes
 // streaming at once, L2 cannot keep a lane's current line between its probes.  Dword i of the
@@ -161,6 +162,7 @@ struct StreamWin {
     uint32_t end;           // chunk end, origin-relative
     uint32_t wb;            // window base, origin-relative, multiple of 16
     uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
+    uint32_t f0, f1, f2, f3;  // the block after the window (wb + 32), loaded one slide ahead
     __device__ __forceinline__ void init(const uint8_t* in, int32_t length) {
         origin = reinterpret_cast<const uint8_t*>((uintptr_t)in & ~(uintptr_t)15);
         pad = (uint32_t)((uintptr_t)in & 15u);
@@ -181,12 +183,15 @@ struct StreamWin {
         if (off > 27u) {
             if (off < 44u) {
                 // forward by less than 16 bytes past the window: slide it one block, keeping the
-                // upper block, so each input block is loaded once on a forward scan
+                // upper block, so each input block is loaded once on a forward scan; the new upper
+                // block was prefetched at the previous slide (its load is off the dependent chain),
+                // and the block after it is prefetched now
                 wb += 16u;
                 w0 = w4; w1 = w5; w2 = w6; w3 = w7;
-                if (wb + 16u < end) {
-                    const uint4 y = *reinterpret_cast<const uint4*>(origin + wb + 16u);
-                    w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
+                w4 = f0; w5 = f1; w6 = f2; w7 = f3;
+                if (wb + 32u < end) {
+                    const uint4 z = *reinterpret_cast<const uint4*>(origin + wb + 32u);
+                    f0 = z.x; f1 = z.y; f2 = z.z; f3 = z.w;
                 }
             } else {
                 wb = q & ~15u;
@@ -195,6 +200,10 @@ struct StreamWin {
                 if (wb + 16u < end) {
                     const uint4 y = *reinterpret_cast<const uint4*>(origin + wb + 16u);
                     w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
+                }
+                if (wb + 32u < end) {
+                    const uint4 z = *reinterpret_cast<const uint4*>(origin + wb + 32u);
+                    f0 = z.x; f1 = z.y; f2 = z.z; f3 = z.w;
                 }
             }
             off = q - wb;
