@@ -17,13 +17,16 @@
 // size): up to one chunk per CU, a workgroup per chunk with the table and the chunk in LDS; up to
 // kSpreadMaxChunks, one chunk per wave (lane 0), so no wave serialises 64 divergent matchers.
 // Hash table: Java allocates a zeroed short[min(nextPow2(len),16384)] per call (:97-99,191).
-// Each resident lane owns a 16384-entry uint32 slot in a device workspace; an entry is
-//   stamp[31:28] | check[27:16] | position[15:0]
-// A stamp mismatch reads as position 0 — exactly a freshly zeroed table, without a clear per
-// chunk.  `check` is 12 bits folded from the 4 bytes at `position`: when it differs from the
-// probe word's fold, getInt(ip) != getInt(candidate) is already decided and the random read of
-// the candidate bytes is skipped (most probes of a literal run end this way).  The candidate
-// position — and with it the emitted stream — is unchanged; only the memory traffic drops.
+// HBM forms (encode_chunk_w): each resident lane owns a 16384-entry uint64 slot in a device
+// workspace; an entry is
+//   stamp[63:58] | next3[57:34] | resid << pbits | position
+// where resid (the low `shift` bits of the hash product) fixes the 4-byte word at `position` with
+// the slot, and next3 holds the 3 bytes after it: the candidate compare and matches of 4-6 bytes
+// need no read of the candidate's input bytes.  A stamp mismatch reads as position 0 — exactly a
+// freshly zeroed table, without a clear per chunk.  The LDS form (encode_chunk) keeps 32-bit
+// entries stamp[31:28] | check[27:16] | position[15:0] (its table must fit LDS with the chunk).
+// The candidate position — and with it the emitted stream — is Java's in every form; only the
+// memory traffic differs.
 #include <stdlib.h>
 #include <algorithm>
 #include <map>
@@ -337,6 +340,137 @@ done:
     return w.pos();
 }
 
+// ---------------------------------------------------------------------------------------------
+// Wide-entry form (the HBM-table kernels): each table entry carries enough of its position's bytes
+// that most probes and most short matches need no read of the candidate's input bytes.
+//   entry (64 bits) = stamp[63:58] | next3[57:34] | resid << pbits | position      (resid+position <= 34 bits)
+//     resid  = the low `shift` bits of bswap(word) * 0x1e35a7bd: with the slot (= the high bits,
+//              Snappy's hash) it determines the 4-byte word exactly, so getInt(ip) == getInt(candidate)
+//              is decided from the entry alone (no 12-bit check, no false-positive loads);
+//     next3  = the 3 bytes after the word (position + 4 .. + 6): a match of 4-6 bytes (45 % of this
+//              corpus's matches) is measured without reading the candidate at all, longer ones read
+//              from candidate + 7 on;
+//     stamp  = 6 bits, as the narrow form's 4 (a mismatch reads as Java's zero: position 0, whose
+//              word and next3 are held in registers).
+// The emitted stream is unchanged: the same probes in the same order, the same table semantics.
+__device__ __forceinline__ uint32_t bytes_at(const uint8_t* in, int32_t p, int32_t length) {  // up to 4 bytes at p (< length), LE, zero-padded
+    if (p + 4 <= length) return ld32(in + p);
+    uint32_t v = 0;
+    for (int32_t i = 0; p + i < length && i < 4; ++i) v |= (uint32_t)in[p + i] << (8 * i);
+    return v;
+}
+
+// 4 + findMatchingLength (:224-239) given the candidate's bytes 4..6 (cn3): bytes b.. against a..
+// (a = candidate + 4 < b = ip + 4), bounded by length.
+__device__ __forceinline__ int32_t match_len_w(const uint8_t* in, StreamWin& win, int32_t a, int32_t b, int32_t length, uint32_t cn3) {
+    int32_t m = 0;
+    if (b <= length - 4) {
+        const uint32_t x0 = (cn3 ^ win.get(b)) & 0xFFFFFFu;
+        if (x0) return (int32_t)(__builtin_ctz(x0) >> 3);
+        m = 3;
+        while (b + m <= length - 4) {
+            const uint32_t x = ld32(in + a + m) ^ win.get(b + m);
+            if (x) return m + (int32_t)(__builtin_ctz(x) >> 3);
+            m += 4;
+        }
+    }
+    while (b + m < length && in[a + m] == in[b + m]) ++m;
+    return m;
+}
+
+template <class Wr>
+__device__ uint32_t encode_chunk_w(const uint8_t* __restrict__ in, int32_t length, Wr& w, uint64_t* __restrict__ table, uint32_t stamp) {
+    for (int i = 0;; i++) {  // preamble (:84-92)
+        const uint32_t b = (uint32_t)length >> (i * 7);
+        if ((b & 0xFFFFFF80u) != 0) {
+            w.put((b & 0x7f) | 0x80);
+        } else {
+            w.put(b);
+            break;
+        }
+    }
+    uint32_t hts = length <= 1 ? 1u : (1u << (32 - __clz((uint32_t)(length - 1))));
+    if (hts > 16384u) hts = 16384u;
+    const int shift = __clz(hts) + 1;
+    int32_t nextEmit = 0;
+    if (length >= 15) {  // MIN_COMPRESSIBLE_BYTES (:34,104); hts >= 16, shift <= 28
+        const uint32_t pbits = hts == 16384u ? 16u : (uint32_t)(32 - shift);  // positions < 2^pbits
+        const uint32_t pmask = (1u << pbits) - 1u, rmask = (1u << shift) - 1u;
+        const uint64_t stag = (uint64_t)stamp << 58;
+        const uint32_t word0 = ld32(in);                            // getInt(base + 0): an empty slot's candidate
+        const uint32_t n3_0 = bytes_at(in, 4, length) & 0xFFFFFFu;  // and the 3 bytes after it
+#define RES(wd) ((__builtin_bswap32(wd) * 0x1e35a7bdu) & rmask)
+#define MKW(pos, wd, n3) (stag | ((uint64_t)(n3) << 34) | ((uint64_t)RES(wd) << pbits) | (uint64_t)(uint32_t)(pos))
+#define WLIVE(e) ((uint32_t)((e) >> 58) == stamp)
+#define WMATCH(e, wd) (WLIVE(e) ? (((uint32_t)((e) >> pbits) & rmask) == RES(wd)) : ((wd) == word0))
+#define WPOS(e) (WLIVE(e) ? (int32_t)((uint32_t)(e) & pmask) : 0)
+#define WN3(e) (WLIVE(e) ? ((uint32_t)((e) >> 34) & 0xFFFFFFu) : n3_0)
+#define XCH64(ptr, v) __hip_atomic_exchange((ptr), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+        StreamWin win;
+        win.init(in, length);
+        int32_t inIndex = 1;
+        uint32_t nextWord = win.get(1);
+        uint32_t nextHash = hash_of(nextWord, shift);
+        for (;;) {  // outer: (:106)
+            int32_t skip = 32;
+            int32_t nextIndex = inIndex;
+            uint64_t entry;
+            uint32_t curWord;
+            do {  // probe run (:107-130), in Java's order
+                inIndex = nextIndex;
+                const uint32_t hash = nextHash;
+                curWord = nextWord;
+                nextIndex = inIndex + (skip++ >> 5);
+                if (nextIndex > length - 4) goto done;
+                nextWord = win.get(nextIndex);
+                nextHash = hash_of(nextWord, shift);
+                const uint32_t n3 = win.get(inIndex + 4) & 0xFFFFFFu;  // inIndex + 4 < length; bytes past it are never compared
+                entry = XCH64(table + hash, MKW(inIndex, curWord, n3));
+            } while (!WMATCH(entry, curWord));
+            int32_t candidate = WPOS(entry);
+            uint32_t cn3 = WN3(entry);
+
+            enc_literal(in + nextEmit, w, inIndex - nextEmit);  // (:132)
+
+            int32_t insertTail;
+            for (;;) {  // (:135-154)
+                const int32_t base = inIndex;
+                const int32_t matched = 4 + match_len_w(in, win, candidate + 4, inIndex + 4, length, cn3);
+                inIndex += matched;
+                enc_copy(w, base - candidate, matched);
+                insertTail = inIndex - 1;
+                nextEmit = inIndex;
+                if (inIndex >= length - 4) goto done;
+                const uint32_t wTail = win.get(insertTail);
+                const uint32_t wCur = win.get(inIndex);
+                const uint32_t n3c = win.get(inIndex + 4) & 0xFFFFFFu;
+                const uint32_t n3t = ((wCur >> 24) | (n3c << 8)) & 0xFFFFFFu;  // bytes inIndex+3 .. +5
+                const uint32_t prevHash = hash_of(wTail, shift);
+                __hip_atomic_store(table + prevHash, MKW(inIndex - 1, wTail, n3t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t currentHash = hash_of(wCur, shift);
+                const uint64_t e = XCH64(table + currentHash, MKW(inIndex, wCur, n3c));
+                if (!WMATCH(e, wCur)) break;
+                candidate = WPOS(e);
+                cn3 = WN3(e);
+            }
+            nextWord = win.get(insertTail + 2);
+            nextHash = hash_of(nextWord, shift);  // (:156)
+            ++inIndex;
+        }
+#undef XCH64
+#undef WN3
+#undef WPOS
+#undef WMATCH
+#undef WLIVE
+#undef MKW
+#undef RES
+    }
+done:
+    if (nextEmit < length) enc_literal(in + nextEmit, w, length - nextEmit);  // (:162-164)
+    w.finish();
+    return w.pos();
+}
+
 // Launch bound 6 blocks of 256 per CU keeps the kernel under 80 VGPRs (no spills) at the 16 waves/CU
 // the host launches.
 //
@@ -345,16 +479,16 @@ done:
 // a wave's divergent control flow, which otherwise serialises a wave's 64 matchers: 64 chunks in one
 // wave take 6x as long as one).  Lane/wave w owns table slot w of the workspace in either form.
 template <bool SWAP, bool SPREAD>
-__global__ void __launch_bounds__(256, 6) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+__global__ void __launch_bounds__(256, 4) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                        const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
-                                                       int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
+                                                       int32_t* __restrict__ status, uint32_t n, uint64_t* __restrict__ workspace,
                                                        uint32_t stamp_base) {
     const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
     if (SPREAD && (gtid & 63u) != 0u) return;
     const uint32_t tid = SPREAD ? gtid >> 6 : gtid;
     const uint32_t nthreads = SPREAD ? (gridDim.x * blockDim.x) >> 6 : gridDim.x * blockDim.x;
-    uint32_t* table = workspace + (size_t)tid * 16384u;
+    uint64_t* table = workspace + (size_t)tid * 16384u;
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
         const uint32_t len = in_len[c];
@@ -363,19 +497,19 @@ __global__ void __launch_bounds__(256, 6) k_snappy_encode(const uint8_t* __restr
             out_len[c] = 0;
             continue;
         }
-        const uint32_t stamp = stamp_base + iter + 1u;  // 1..15, host re-zeroes the workspace before wrap
+        const uint32_t stamp = stamp_base + iter + 1u;  // 1..63, host re-zeroes the workspace before wrap
         uint8_t* o = out + out_off[c];
         uint32_t olen;
         const uint8_t* src = in + in_off[c];
         if ((((uintptr_t)o) & 7u) == 0) {
             WriterT<true> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
-            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
+            olen = encode_chunk_w(src, (int32_t)len, w, table, stamp);
         } else if ((((uintptr_t)o) & 3u) == 0) {
             WriterT<false> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
-            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
+            olen = encode_chunk_w(src, (int32_t)len, w, table, stamp);
         } else {
             ByteWriter w{o, 0};
-            olen = encode_chunk<SWAP>(src, (int32_t)len, w, table, stamp);
+            olen = encode_chunk_w(src, (int32_t)len, w, table, stamp);
         }
         out_len[c] = olen;
         status[c] = NX_OK;
@@ -444,15 +578,15 @@ namespace {
 // Encoder hash-table workspace, one per (device, stream): launches on one stream are ordered, so
 // they may share a workspace; launches on different streams may overlap and must not.
 struct Workspace {
-    uint32_t* ws = nullptr;
+    uint64_t* ws = nullptr;
     size_t threads = 0;  // table slots (lanes of the dense form, waves of the spread form)
-    uint32_t stamp = 0;  // last stamp used; entries carry 4-bit stamps 1..15
+    uint32_t stamp = 0;  // last stamp used; entries carry 6-bit stamps 1..63
 };
 std::mutex g_ws_mu;
 std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
 constexpr unsigned kEncBlock = 256;
 constexpr unsigned kEncWavesPerCU = 16;
-constexpr uint32_t kMaxStamp = 15;
+constexpr uint32_t kMaxStamp = 63;  // 6-bit stamps 1..63
 constexpr uint32_t kSpreadMaxChunks = 16384;  // above this the dense form is faster
 }  // namespace
 
@@ -482,7 +616,7 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
     const bool spread = n <= kSpreadMaxChunks;
     const size_t want = (size_t)cus * kEncWavesPerCU * (spread ? 1 : 64);  // table slots: waves or lanes
     const size_t slots = n < want ? (spread ? n : ((n + kEncBlock - 1) / kEncBlock) * kEncBlock) : want;
-    const size_t per = 16384u * sizeof(uint32_t);
+    const size_t per = 16384u * sizeof(uint64_t);
     std::lock_guard<std::mutex> lk(g_ws_mu);
     Workspace& W = g_ws[{dev, st}];
     if (W.ws == nullptr || W.threads < slots) {
