@@ -422,9 +422,11 @@ __device__ uint32_t encode_chunk_w(const uint8_t* __restrict__ in, int32_t lengt
                 curWord = nextWord;
                 nextIndex = inIndex + (skip++ >> 5);
                 if (nextIndex > length - 4) goto done;
+                // the bytes after inIndex first (inIndex + 4 < length; bytes past the end are never
+                // compared), then the next probe's word: the window only moves forward
+                const uint32_t n3 = win.get(inIndex + 4) & 0xFFFFFFu;
                 nextWord = win.get(nextIndex);
                 nextHash = hash_of(nextWord, shift);
-                const uint32_t n3 = win.get(inIndex + 4) & 0xFFFFFFu;  // inIndex + 4 < length; bytes past it are never compared
                 entry = XCH64(table + hash, MKW(inIndex, curWord, n3));
             } while (!WMATCH(entry, curWord));
             int32_t candidate = WPOS(entry);
