@@ -347,17 +347,20 @@ def roofline(algo_bytes, ms, n_chunks, kernels, traffic, copy_gbs):
 
 
 ENC_KERNELS = ["nx::enc::k_snappy_encode"]
-# Snappy.encode's memory requests per 64 KiB chunk of the bench corpus (CPU count of Netty's matcher,
-# profiles/r01/encoder_experiments.md): table probes (read + insert of a random slot) and candidate
-# compares (a random read of the chunk's input)
+# Snappy.encode's dependent memory requests per 64 KiB chunk of the bench corpus: table probes (one
+# exchange of a random 64-bit slot each; profiles/r01/encoder_experiments.md) and first reads of a
+# candidate's input — with the wide table entries (exact word + 3 following bytes) only matches of
+# 7+ bytes read the candidate (scripts/experiments/sim_window.py's match-length census: 4 275 of
+# 7 723 matches per chunk; 9 709 with the round-1 32-bit entries)
 ENC_PROBES_PER_CHUNK = 16546
-ENC_CANDIDATE_LOADS_PER_CHUNK = 9709
+ENC_CANDIDATE_LOADS_PER_CHUNK = 4275
 
 
 def probe_ceiling(torch, dev, lanes=262144, steps=16384):
     """The random-access ceiling of the encoder's request pattern on this GPU (netty_amd/tools/
-    probe_ceiling.hip: per lane a serial chain of table exchanges + 60 % dependent input loads over
-    its own 64 KiB regions, at the encoder's resident lane count).  Returns probes/s or None."""
+    probe_ceiling.hip: per lane a serial chain of 64-bit table exchanges + the encoder's share of
+    dependent input loads over its own regions, at the encoder's resident lane count).  Returns
+    probes/s or None."""
     import ctypes
     path = os.path.join(ROOT, "netty_amd", "libnx_probe_ceiling.so")
     if not os.path.exists(path):
@@ -365,12 +368,13 @@ def probe_ceiling(torch, dev, lanes=262144, steps=16384):
     lib = ctypes.CDLL(path)
     lib.nx_probe_ceiling.restype = ctypes.c_int32
     lib.nx_probe_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
-                                     ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
-    tab = torch.empty(lanes * 16384, dtype=torch.int32, device=dev)
+                                     ctypes.c_uint32, ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
+    tab = torch.empty(lanes * 16384, dtype=torch.int64, device=dev)
     inp = torch.empty(lanes * 16384, dtype=torch.int32, device=dev)
     sink = torch.empty(lanes, dtype=torch.int32, device=dev)
     ms = ctypes.c_float(0.0)
-    rc = lib.nx_probe_ceiling(tab.data_ptr(), inp.data_ptr(), sink.data_ptr(), lanes, steps, ctypes.byref(ms),
+    permille = round(1000 * ENC_CANDIDATE_LOADS_PER_CHUNK / ENC_PROBES_PER_CHUNK)
+    rc = lib.nx_probe_ceiling(tab.data_ptr(), inp.data_ptr(), sink.data_ptr(), lanes, steps, permille, ctypes.byref(ms),
                               ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
     del tab, inp, sink
     torch.cuda.empty_cache()
