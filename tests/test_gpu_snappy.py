@@ -293,13 +293,31 @@ def test_snappy_encode_batch_size_forms(dev, B, oracle, n):
             assert out[oo[i]:oo[i] + ol[i]].cpu().numpy().tobytes() == zero, i
 
 
+@pytest.mark.parametrize("fill", [300, 16400])
+def test_snappy_encode_parity_hbm_forms(dev, B, oracle, kat, fill):
+    """The whole parity corpus (short, random, zero, periodic, KAT inputs) through the HBM-table forms
+    (wave per chunk above CUs chunks, lane per chunk above 16 384) whose 64-bit entries decide the
+    candidate compare and short matches from the table alone: every chunk equals the oracle's bytes."""
+    corpus = _corpus(oracle, kat)
+    chunks = corpus + [oracle.textgen_chunk(5000 + i, 200) for i in range(fill - len(corpus))]
+    inp, off, ln = B.pack(chunks, dev, align=1)
+    cap = [B.snappy_max_compressed_length(len(c)) for c in chunks]
+    out, ooff = B.out_slots(cap, dev)
+    olen, st = B.snappy_encode(inp, off, ln, out, ooff)
+    assert int((st != 0).sum()) == 0
+    ol, oo, h = olen.cpu().tolist(), ooff.cpu().tolist(), out.cpu().numpy().tobytes()
+    for i in list(range(len(corpus))) + [len(chunks) - 1]:
+        assert h[oo[i]:oo[i] + ol[i]] == oracle.snappy_encode(chunks[i]), (i, len(chunks[i]))
+
+
 def test_snappy_encode_stamp_wrap_many_chunks_per_lane(dev, B, oracle):
-    """one encoder lane encodes more than 14 chunks, so the host splits the batch
-    into launches and re-zeroes the 4-bit-stamped table workspace before the stamps wrap
-    (snappy_encode.hip nx_snappy_encode_batch).  Lane t encodes chunks t, t + lanes, ...; the chunks of
-    the first and last lane in every launch, and a random sample, must equal the oracle's bytes."""
+    """one encoder lane encodes more chunks than there are table stamps (63), so
+    the host splits the batch into launches and re-zeroes the stamped table workspace before the
+    stamps wrap (snappy_encode.hip nx_snappy_encode_batch).  Lane t encodes chunks t, t + lanes, ...;
+    the chunks of the first and last lane in every launch, and a random sample, must equal the
+    oracle's bytes."""
     lanes = torch.cuda.get_device_properties(dev).multi_processor_count * 16 * 64
-    n, L = lanes * 15 + 7, 160
+    n, L = lanes * 63 + 7, 160
     src = torch.empty(n * L, dtype=torch.uint8, device=dev)
     B.textgen(src, 0, n, L)
     off = torch.arange(n, dtype=torch.int64, device=dev) * L
@@ -311,7 +329,7 @@ def test_snappy_encode_stamp_wrap_many_chunks_per_lane(dev, B, oracle):
     torch.cuda.synchronize()
     assert int((st != 0).sum()) == 0
     rng = random.Random(5)
-    pick = sorted({k * lanes + t for k in range(16) for t in (0, lanes - 1)} | {rng.randrange(n) for _ in range(300)})
+    pick = sorted({k * lanes + t for k in range(64) for t in (0, lanes - 1)} | {rng.randrange(n) for _ in range(300)})
     pick = [i for i in pick if i < n]
     ol = olen[pick].cpu().tolist()
     for i, m in zip(pick, ol):
