@@ -96,6 +96,73 @@ struct WriterT {
     }
 };
 
+// LDS-staged writer (dense form): a lane's output dwords gather in its own LDS stage of SD dwords
+// (SD*4-byte aligned units of the destination) and leave as whole units of 16-byte stores, so the L2
+// receives full-line writes it needs no read-for-merge nor repeated partial write-backs for; the
+// first unit (the destination need not be unit-aligned) and the tail are stored dword by dword.
+template <int SD>
+struct WriterL {
+    uint32_t* st;   // this lane's LDS stage
+    uint32_t* dst;  // output dword 0 (4-byte aligned)
+    uint32_t acc;   // pending bytes (little-endian order)
+    uint32_t na;    // number of pending bytes (0..3)
+    uint32_t nw;    // dwords emitted
+    uint32_t s;     // stage slot of the next dword = (dword address) mod SD
+    uint32_t lo;    // first valid slot of the current unit (nonzero only for the first unit)
+    __device__ __forceinline__ WriterL(uint32_t* stage, uint8_t* o)
+        : st(stage), dst(reinterpret_cast<uint32_t*>(o)), acc(0), na(0), nw(0) {
+        s = (uint32_t)(((uintptr_t)o >> 2) & (SD - 1));
+        lo = s;
+    }
+    __device__ __forceinline__ void emit(uint32_t v) {
+        st[s] = v;
+        ++nw;
+        if (s == SD - 1) {
+            uint32_t* g = dst + nw - SD;  // the unit's slot 0
+            if (lo == 0) {
+#pragma unroll
+                for (int q = 0; q < SD / 4; ++q)
+                    reinterpret_cast<uint4*>(g)[q] = make_uint4(st[4 * q], st[4 * q + 1], st[4 * q + 2], st[4 * q + 3]);
+            } else {
+                for (uint32_t j = lo; j < SD; ++j) g[j] = st[j];
+                lo = 0;
+            }
+            s = 0;
+        } else {
+            ++s;
+        }
+    }
+    __device__ __forceinline__ void put(uint32_t b) {
+        acc |= b << (8 * na);
+        if (++na == 4) {
+            emit(acc);
+            acc = 0;
+            na = 0;
+        }
+    }
+    __device__ __forceinline__ void copy(const uint8_t* p, int32_t n) {
+        while (n >= 4) {
+            const uint32_t v = ld32(p);
+            if (na == 0) {
+                emit(v);
+            } else {
+                emit(acc | (v << (8 * na)));
+                acc = v >> (32 - 8 * na);
+            }
+            p += 4;
+            n -= 4;
+        }
+        while (n-- > 0) put(*p++);
+    }
+    __device__ __forceinline__ uint32_t pos() const { return nw * 4 + na; }
+    __device__ __forceinline__ void finish() {
+        uint32_t* g = dst + nw - s;  // slot 0 of the open unit
+        for (uint32_t j = lo; j < s; ++j) g[j] = st[j];
+        uint8_t* t = reinterpret_cast<uint8_t*>(dst + nw);
+        for (uint32_t i = 0; i < na; ++i) t[i] = (uint8_t)(acc >> (8 * i));
+    }
+};
+
 // Byte-store writer for unaligned destinations (same interface).
 struct ByteWriter {
     uint8_t* o;
@@ -480,6 +547,7 @@ done:
 // SPREAD = true: one chunk per WAVE, lane 0 only (small batches: lanes of different chunks never share
 // a wave's divergent control flow, which otherwise serialises a wave's 64 matchers: 64 chunks in one
 // wave take 6x as long as one).  Lane/wave w owns table slot w of the workspace in either form.
+constexpr int kStageDw = 32;  // dense form: 128-byte output units staged in LDS (33 KiB per 256 lanes)
 template <bool SWAP, bool SPREAD>
 __global__ void __launch_bounds__(256, 4) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -491,6 +559,11 @@ __global__ void __launch_bounds__(256, 4) k_snappy_encode(const uint8_t* __restr
     const uint32_t tid = SPREAD ? gtid >> 6 : gtid;
     const uint32_t nthreads = SPREAD ? (gridDim.x * blockDim.x) >> 6 : gridDim.x * blockDim.x;
     uint64_t* table = workspace + (size_t)tid * 16384u;
+    uint32_t* stage = nullptr;
+    if constexpr (!SPREAD) {
+        __shared__ uint32_t stages[256 * (kStageDw + 1)];  // odd stride: lanes' slots on distinct banks
+        stage = &stages[threadIdx.x * (kStageDw + 1)];
+    }
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
         const uint32_t len = in_len[c];
@@ -503,7 +576,10 @@ __global__ void __launch_bounds__(256, 4) k_snappy_encode(const uint8_t* __restr
         uint8_t* o = out + out_off[c];
         uint32_t olen;
         const uint8_t* src = in + in_off[c];
-        if ((((uintptr_t)o) & 7u) == 0) {
+        if (!SPREAD && (((uintptr_t)o) & 3u) == 0) {
+            WriterL<kStageDw> w(stage, o);
+            olen = encode_chunk_w(src, (int32_t)len, w, table, stamp);
+        } else if ((((uintptr_t)o) & 7u) == 0) {
             WriterT<true> w{reinterpret_cast<uint32_t*>(o), 0, 0, 0, 0};
             olen = encode_chunk_w(src, (int32_t)len, w, table, stamp);
         } else if ((((uintptr_t)o) & 3u) == 0) {
