@@ -39,17 +39,17 @@ __device__ __forceinline__ uint32_t hash_at(const uint8_t* p) {
     return (uint32_t)(((ld64(p) << 24) * 889523592379ull) >> (64 - 12));           // LZ4_hash5, byU32
 }
 
-__device__ __forceinline__ uint32_t put_len(uint8_t* out, uint32_t op, uint32_t v) {  // 255-run of a length >= 15
-    for (; v >= 255u; v -= 255u) out[op++] = 255u;
-    out[op++] = (uint8_t)v;
+template <class O>
+__device__ __forceinline__ uint32_t put_len(O& out, uint32_t op, uint32_t v) {  // 255-run of a length >= 15
+    for (; v >= 255u; v -= 255u) out.set(op++, 255u);
+    out.set(op++, v);
     return op;
 }
 
 // Large == false: blocks < 65547 bytes, entries stamp << 16 | index.  Large == true: blocks of up
 // to 32 MiB, raw indices in a table the lane zeroes before and after the block.
-template <bool Large>
-__device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint8_t* __restrict__ out,
-                                 uint32_t* __restrict__ table, uint32_t stamp) {
+template <bool Large, class O>
+__device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, O& out, uint32_t* __restrict__ table, uint32_t stamp) {
     const uint32_t stag = stamp << 16;
 #define XCH(h, v) __hip_atomic_exchange(table + (h), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #define PUT(h, v) __hip_atomic_store(table + (h), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -89,18 +89,18 @@ __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint
             {
                 const uint32_t lit = (uint32_t)(ip - anchor);
                 if (lit >= 15u) {
-                    out[token] = 15u << 4;
+                    out.set(token, 15u << 4);
                     op = put_len(out, op, lit - 15u);
                 } else {
-                    out[token] = (uint8_t)(lit << 4);
+                    out.set(token, lit << 4);
                 }
-                for (uint32_t k = 0; k < lit; ++k) out[op + k] = in[anchor + k];
+                for (uint32_t k = 0; k < lit; ++k) out.set(op + k, in[anchor + k]);
                 op += lit;
             }
             for (;;) {  // _next_match
                 const uint32_t off = (uint32_t)(ip - match);
-                out[op++] = (uint8_t)off;
-                out[op++] = (uint8_t)(off >> 8);
+                out.set(op++, off & 0xFFu);
+                out.set(op++, (off >> 8) & 0xFFu);
                 int32_t mc = 0;
                 while (ip + kMinMatch + mc + 4 <= matchlimit) {
                     const uint32_t x = ld32(in + ip + kMinMatch + mc) ^ ld32(in + match + kMinMatch + mc);
@@ -114,10 +114,10 @@ __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint
             counted:
                 ip += mc + kMinMatch;
                 if (mc >= 15) {
-                    out[token] += 15u;
+                    out.set(token, out.get(token) + 15u);
                     op = put_len(out, op, (uint32_t)(mc - 15));
                 } else {
-                    out[token] += (uint8_t)mc;
+                    out.set(token, out.get(token) + (uint32_t)mc);
                 }
                 anchor = ip;
                 if (ip >= mflimit_plus_one) goto last_literals;
@@ -126,7 +126,7 @@ __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, uint
                 if ((!Large || mi + 65535 >= ip) && ld32(in + mi) == ld32(in + ip)) {
                     match = mi;
                     token = op++;
-                    out[token] = 0;
+                    out.set(token, 0u);
                     continue;
                 }
                 break;
@@ -142,12 +142,13 @@ last_literals:
         for (uint32_t k = 0; k < 4096u; ++k) __hip_atomic_store(table + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t lit = (uint32_t)(n - anchor);  // last literals
     if (lit >= 15u) {
-        out[op++] = 15u << 4;
+        out.set(op++, 15u << 4);
         op = put_len(out, op, lit - 15u);
     } else {
-        out[op++] = (uint8_t)(lit << 4);
+        out.set(op++, lit << 4);
     }
-    for (uint32_t k = 0; k < lit; ++k) out[op + k] = in[anchor + k];
+    for (uint32_t k = 0; k < lit; ++k) out.set(op + k, in[anchor + k]);
+    out.finish((int32_t)(op + lit));
     return op + lit;
 }
 
@@ -160,6 +161,11 @@ __global__ void __launch_bounds__(256) k_lz4_encode(const uint8_t* __restrict__ 
     uint32_t tid, nthreads;
     if (!chunk_slot<SPREAD>(tid, nthreads)) return;
     uint32_t* table = workspace + (size_t)tid * kTableSlots;
+    uint8_t* slot = nullptr;
+    if constexpr (!SPREAD) {
+        __shared__ __attribute__((aligned(16))) uint8_t stages[256 * kStageStride];
+        slot = &stages[threadIdx.x * kStageStride];
+    }
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
         const uint32_t len = in_len[c];
@@ -168,8 +174,16 @@ __global__ void __launch_bounds__(256) k_lz4_encode(const uint8_t* __restrict__ 
             status[c] = NX_ERR_INVALID_ARG;
             continue;
         }
-        out_len[c] = (int32_t)len >= k64KLimit ? encode_block<true>(in + in_off[c], (int32_t)len, out + out_off[c], table, 0u)
-                                  : encode_block<false>(in + in_off[c], (int32_t)len, out + out_off[c], table, stamp_base + iter + 1u);
+        if ((int32_t)len >= k64KLimit) {
+            GOut o{out + out_off[c]};
+            out_len[c] = encode_block<true>(in + in_off[c], (int32_t)len, o, table, 0u);
+        } else if (SPREAD) {
+            GOut o{out + out_off[c]};
+            out_len[c] = encode_block<false>(in + in_off[c], (int32_t)len, o, table, stamp_base + iter + 1u);
+        } else {
+            ByteStage o(slot, out + out_off[c]);  // dense form: whole 128-byte units (nx_common.hpp)
+            out_len[c] = encode_block<false>(in + in_off[c], (int32_t)len, o, table, stamp_base + iter + 1u);
+        }
         status[c] = NX_OK;
     }
 }

@@ -89,6 +89,59 @@ inline LaneGrid lane_grid(uint32_t n, int cus, unsigned waves_per_cu) {
     return g;
 }
 
+// Output of the byte-writing lane-per-chunk encoders (LZ4, FastLZ, LZF).  A lane's scattered byte
+// stores are partial-line writes the L2 has usually evicted before the lane's next byte comes, so
+// every one costs a line merge / write-back; the dense forms therefore stage the 128-byte-aligned
+// unit of the destination being written in the lane's own LDS slot and store it as eight 16-byte
+// writes when the lane moves past it (Snappy's WriterL does the same with dwords).  Positions are
+// relative to the chunk's output start; writes are sequential except for back-patches (token,
+// literal-run count), which land in LDS while their unit is staged and in global memory after.
+// GOut is the plain global form (small-batch forms, large LZ4 blocks).
+constexpr uint32_t kStageUnit = 128;
+constexpr uint32_t kStageStride = 132;  // bytes per lane slot: 33 dwords, lanes' dwords on distinct banks
+struct GOut {
+    uint8_t* p;
+    __device__ __forceinline__ void set(int32_t pos, uint32_t v) { p[pos] = (uint8_t)v; }
+    __device__ __forceinline__ uint32_t get(int32_t pos) const { return p[pos]; }
+    __device__ __forceinline__ void finish(int32_t) {}
+};
+struct ByteStage {
+    uint8_t* st;   // the lane's LDS slot
+    uint8_t* dst;  // output byte 0
+    int32_t u0;    // position of the staged unit's byte 0 (negative for the first, partial unit)
+    __device__ __forceinline__ ByteStage(uint8_t* slot, uint8_t* out)
+        : st(slot), dst(out), u0(-(int32_t)((uintptr_t)out & (kStageUnit - 1))) {}
+    __device__ __forceinline__ void flush_unit() {
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(st);
+        if (u0 >= 0) {
+            uint4* g = reinterpret_cast<uint4*>(dst + u0);
+#pragma unroll
+            for (int q = 0; q < (int)kStageUnit / 16; ++q) g[q] = make_uint4(s32[4 * q], s32[4 * q + 1], s32[4 * q + 2], s32[4 * q + 3]);
+        } else {
+            for (int32_t j = -u0; j < (int32_t)kStageUnit; ++j) dst[u0 + j] = st[j];
+        }
+        u0 += (int32_t)kStageUnit;
+    }
+    __device__ __forceinline__ void set(int32_t pos, uint32_t v) {
+        while (pos >= u0 + (int32_t)kStageUnit) flush_unit();
+        if (pos >= u0)
+            st[pos - u0] = (uint8_t)v;
+        else
+            dst[pos] = (uint8_t)v;
+    }
+    __device__ __forceinline__ uint32_t get(int32_t pos) const { return pos >= u0 ? st[pos - u0] : dst[pos]; }
+    // store the staged bytes [u0, end)
+    __device__ __forceinline__ void finish(int32_t end) {
+        int32_t j = u0 < 0 ? -u0 : 0;
+        if (u0 >= 0) {
+            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(st);
+            for (; j + 16 <= end - u0; j += 16)
+                *reinterpret_cast<uint4*>(dst + u0 + j) = make_uint4(s32[j / 4], s32[j / 4 + 1], s32[j / 4 + 2], s32[j / 4 + 3]);
+        }
+        for (; j < end - u0; ++j) dst[u0 + j] = st[j];
+    }
+};
+
 // Kernel launch helper: grid-stride sizes.
 inline unsigned grid_for(uint64_t threads, unsigned block) {
     uint64_t g = (threads + block - 1) / block;

@@ -3,6 +3,9 @@
 // repeated), encoded R times with nx_snappy_encode_batch; prints the best kernel ms and an output
 // checksum (equal checksums = identical bytes).
 #include ENC_SRC
+#ifndef ENC_FN
+#define ENC_FN nx_snappy_encode_batch
+#endif
 #include "../../include/netty_amd_textgen.h"
 #include <stdio.h>
 #include <string.h>
@@ -32,7 +35,7 @@ int main(int argc, char** argv) {
     float best = 1e30f;
     for (int r = 0; r < R; ++r) {
         hipEventRecord(a);
-        if (nx_snappy_encode_batch(din, ioff, ilen, dout, ooff, olen, st, N, 0) != 0) return 2;
+        if (ENC_FN(din, ioff, ilen, dout, ooff, olen, st, N, 0) != 0) return 2;
         hipEventRecord(b);
         hipEventSynchronize(b);
         float ms;
