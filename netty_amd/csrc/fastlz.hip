@@ -32,7 +32,8 @@ __device__ __forceinline__ int32_t hashf(const uint8_t* in, int32_t o, int32_t l
     return v & HASH_MASK;
 }
 
-__device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, uint8_t* __restrict__ out, int32_t proposedLevel,
+template <class O>
+__device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O& out, int32_t proposedLevel,
                             int32_t lim, uint32_t* __restrict__ htab, uint32_t stamp) {
     const int32_t level = proposedLevel == 0 ? (inLength < 65536 ? 1 : 2) : proposedLevel;
     int32_t ip = 0;
@@ -45,17 +46,18 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, ui
 #define HSET(h, v) (htab[(h)] = stag | (uint32_t)(v))
     if (inLength < 4) {
         if (inLength != 0) {
-            out[op++] = (uint8_t)(inLength - 1);
+            out.set(op++, (uint8_t)(inLength - 1));
             ipBound++;
-            while (ip <= ipBound) out[op++] = in[ip++];
+            while (ip <= ipBound) out.set(op++, in[ip++]);
+            out.finish(op);
             return inLength + 1;
         }
         return 0;
     }
     copy = 2;
-    out[op++] = MAX_COPY - 1;
-    out[op++] = in[ip++];
-    out[op++] = in[ip++];
+    out.set(op++, MAX_COPY - 1);
+    out.set(op++, in[ip++]);
+    out.set(op++, in[ip++]);
     while (ip < ipLimit) {
         int32_t ref = 0;
         int64_t distance = 0;
@@ -95,12 +97,12 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, ui
                 }
             }
             if (lit) {
-                out[op++] = in[anchor++];
+                out.set(op++, in[anchor++]);
                 ip = anchor;
                 copy++;
                 if (copy == MAX_COPY) {
                     copy = 0;
-                    out[op++] = MAX_COPY - 1;
+                    out.set(op++, MAX_COPY - 1);
                 }
                 continue;
             }
@@ -128,7 +130,7 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, ui
             }
         }
         if (copy != 0) {
-            out[op - copy - 1] = (uint8_t)(copy - 1);
+            out.set(op - copy - 1, (uint32_t)(copy - 1));
         } else {
             op--;
         }
@@ -138,46 +140,46 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, ui
         if (level == 2) {
             if (distance < MAX_DISTANCE) {
                 if (len < 7) {
-                    out[op++] = (uint8_t)((len << 5) + (int32_t)(distance >> 8));
-                    out[op++] = (uint8_t)(distance & 255);
+                    out.set(op++, (uint8_t)((len << 5) + (int32_t)(distance >> 8)));
+                    out.set(op++, (uint8_t)(distance & 255));
                 } else {
-                    out[op++] = (uint8_t)((7 << 5) + (int32_t)(distance >> 8));
-                    for (len -= 7; len >= 255; len -= 255) out[op++] = 255;
-                    out[op++] = (uint8_t)len;
-                    out[op++] = (uint8_t)(distance & 255);
+                    out.set(op++, (uint8_t)((7 << 5) + (int32_t)(distance >> 8)));
+                    for (len -= 7; len >= 255; len -= 255) out.set(op++, 255);
+                    out.set(op++, (uint8_t)len);
+                    out.set(op++, (uint8_t)(distance & 255));
                 }
             } else {
                 distance -= MAX_DISTANCE;
                 if (len < 7) {
-                    out[op++] = (uint8_t)((len << 5) + 31);
-                    out[op++] = 255;
-                    out[op++] = (uint8_t)(distance >> 8);
-                    out[op++] = (uint8_t)(distance & 255);
+                    out.set(op++, (uint8_t)((len << 5) + 31));
+                    out.set(op++, 255);
+                    out.set(op++, (uint8_t)(distance >> 8));
+                    out.set(op++, (uint8_t)(distance & 255));
                 } else {
-                    out[op++] = (uint8_t)((7 << 5) + 31);
-                    for (len -= 7; len >= 255; len -= 255) out[op++] = 255;
-                    out[op++] = (uint8_t)len;
-                    out[op++] = 255;
-                    out[op++] = (uint8_t)(distance >> 8);
-                    out[op++] = (uint8_t)(distance & 255);
+                    out.set(op++, (uint8_t)((7 << 5) + 31));
+                    for (len -= 7; len >= 255; len -= 255) out.set(op++, 255);
+                    out.set(op++, (uint8_t)len);
+                    out.set(op++, 255);
+                    out.set(op++, (uint8_t)(distance >> 8));
+                    out.set(op++, (uint8_t)(distance & 255));
                 }
             }
         } else {
             if (len > MAX_LEN - 2) {
                 while (len > MAX_LEN - 2) {
-                    out[op++] = (uint8_t)((7 << 5) + (int32_t)(distance >> 8));
-                    out[op++] = (uint8_t)(MAX_LEN - 2 - 7 - 2);
-                    out[op++] = (uint8_t)(distance & 255);
+                    out.set(op++, (uint8_t)((7 << 5) + (int32_t)(distance >> 8)));
+                    out.set(op++, (uint8_t)(MAX_LEN - 2 - 7 - 2));
+                    out.set(op++, (uint8_t)(distance & 255));
                     len -= MAX_LEN - 2;
                 }
             }
             if (len < 7) {
-                out[op++] = (uint8_t)((len << 5) + (int32_t)(distance >> 8));
-                out[op++] = (uint8_t)(distance & 255);
+                out.set(op++, (uint8_t)((len << 5) + (int32_t)(distance >> 8)));
+                out.set(op++, (uint8_t)(distance & 255));
             } else {
-                out[op++] = (uint8_t)((7 << 5) + (int32_t)(distance >> 8));
-                out[op++] = (uint8_t)(len - 7);
-                out[op++] = (uint8_t)(distance & 255);
+                out.set(op++, (uint8_t)((7 << 5) + (int32_t)(distance >> 8)));
+                out.set(op++, (uint8_t)(len - 7));
+                out.set(op++, (uint8_t)(distance & 255));
             }
         }
         int32_t hv = hashf(in, ip, lim);
@@ -186,25 +188,26 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, ui
         hv = hashf(in, ip, lim);
         HSET(hv, ip);
         ip++;
-        out[op++] = MAX_COPY - 1;
+        out.set(op++, MAX_COPY - 1);
     }
     ipBound++;
     while (ip <= ipBound) {
-        out[op++] = in[ip++];
+        out.set(op++, in[ip++]);
         copy++;
         if (copy == MAX_COPY) {
             copy = 0;
-            out[op++] = MAX_COPY - 1;
+            out.set(op++, MAX_COPY - 1);
         }
     }
     if (copy != 0) {
-        out[op - copy - 1] = (uint8_t)(copy - 1);
+        out.set(op - copy - 1, (uint32_t)(copy - 1));
     } else {
         op--;
     }
-    if (level == 2) out[0] |= 1 << 5;
+    if (level == 2) out.set(0, out.get(0) | (1u << 5));
 #undef HGET
 #undef HSET
+    out.finish(op);
     return op;
 }
 
@@ -307,6 +310,11 @@ __global__ void __launch_bounds__(256) k_compress(const uint8_t* __restrict__ in
     uint32_t tid, nthreads;
     if (!chunk_slot<SPREAD>(tid, nthreads)) return;
     uint32_t* htab = ws + (size_t)tid * HASH_SIZE;
+    uint8_t* slot = nullptr;
+    if constexpr (!SPREAD) {
+        __shared__ __attribute__((aligned(16))) uint8_t stages[256 * kStageStride];
+        slot = &stages[threadIdx.x * kStageStride];
+    }
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
         const uint32_t len = in_len[c];
@@ -318,7 +326,13 @@ __global__ void __launch_bounds__(256) k_compress(const uint8_t* __restrict__ in
         }
         const int32_t l16 = lim ? lim[c] : (int32_t)len;
         const uint32_t stamp = ((stamp_base + iter) % 65535u) + 1u;
-        out_len[c] = (uint32_t)compress(in + in_off[c], (int32_t)len, out + out_off[c], lv, l16, htab, stamp);
+        if (SPREAD) {
+            GOut o{out + out_off[c]};
+            out_len[c] = (uint32_t)compress(in + in_off[c], (int32_t)len, o, lv, l16, htab, stamp);
+        } else {
+            ByteStage o(slot, out + out_off[c]);  // dense form: whole 128-byte units (nx_common.hpp)
+            out_len[c] = (uint32_t)compress(in + in_off[c], (int32_t)len, o, lv, l16, htab, stamp);
+        }
         status[c] = NX_OK;
     }
 }

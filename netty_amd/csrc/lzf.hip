@@ -28,8 +28,9 @@ __device__ __forceinline__ int32_t first2(const uint8_t* in, int32_t p) {  // Ch
 // zero (position 0).  Whether the chunk starts the Java array or continues a message does not change
 // the bytes: a never-written slot or an earlier chunk's entry can never pass the 3-byte check
 // (oracle/netty_oracle.c orc_lzf_compress_body).
-__device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, uint8_t* __restrict__ out, uint32_t* __restrict__ htab,
-                                 uint32_t stamp) {
+// The body goes to output positions 7.. (after the LZFChunk header, written last).
+template <class O>
+__device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& out, uint32_t* __restrict__ htab, uint32_t stamp) {
     const uint32_t stag = stamp << 16;
     const int32_t inEnd = n - 4;
     int32_t ip = 0, op = 1, lit = 0;
@@ -44,9 +45,9 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, uint
         int32_t off = ip - ref;
         if (ref < 0 || ref >= ip || off > MAX_OFF || in[ref + 2] != p2 || in[ref + 1] != (uint8_t)(seen >> 8) ||
             in[ref] != (uint8_t)(seen >> 16)) {
-            out[op++] = in[ip++];
+            out.set(7 + op++, in[ip++]);
             if (++lit == MAX_LIT) {
-                out[op - 33] = 31;
+                out.set(7 + op - 33, 31);
                 lit = 0;
                 op++;
             }
@@ -57,7 +58,7 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, uint
         if (lit == 0) {
             op--;
         } else {
-            out[op - lit - 1] = (uint8_t)(lit - 1);
+            out.set(7 + op - lit - 1, (uint8_t)(lit - 1));
             lit = 0;
         }
         int32_t len = 3;
@@ -65,12 +66,12 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, uint
         len -= 2;
         --off;
         if (len < 7) {
-            out[op++] = (uint8_t)((off >> 8) + (len << 5));
+            out.set(7 + op++, (uint8_t)((off >> 8) + (len << 5)));
         } else {
-            out[op++] = (uint8_t)((off >> 8) + (7 << 5));
-            out[op++] = (uint8_t)(len - 7);
+            out.set(7 + op++, (uint8_t)((off >> 8) + (7 << 5)));
+            out.set(7 + op++, (uint8_t)(len - 7));
         }
-        out[op++] = (uint8_t)off;
+        out.set(7 + op++, (uint8_t)off);
         op++;
         ip += len;  // matchEnd - 2 (<= n - 4)
         seen = first2(in, ip);
@@ -82,15 +83,15 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, uint
         ++ip;
     }
     while (ip < n) {  // handleTail
-        out[op++] = in[ip++];
+        out.set(7 + op++, in[ip++]);
         if (++lit == MAX_LIT) {
-            out[op - lit - 1] = (uint8_t)(lit - 1);
+            out.set(7 + op - lit - 1, (uint8_t)(lit - 1));
             lit = 0;
             op++;
         }
     }
     if (lit) {
-        out[op - lit - 1] = (uint8_t)(lit - 1);
+        out.set(7 + op - lit - 1, (uint8_t)(lit - 1));
     } else {
         op--;
     }
@@ -98,26 +99,29 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, uint
 }
 
 // One LZFChunk.  Writes the compressed body at out+7 first; falls back to a raw block.
-__device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t n, uint8_t* __restrict__ out, uint32_t* htab, uint32_t stamp) {
+template <class O>
+__device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t n, O& out, uint32_t* htab, uint32_t stamp) {
     if (n >= 16) {
-        const int32_t clen = compress_body(in, n, out + 7, htab, stamp);
+        const int32_t clen = compress_body(in, n, out, htab, stamp);
         if (clen + 7 < n + 5) {
-            out[0] = 'Z';
-            out[1] = 'V';
-            out[2] = 1;
-            out[3] = (uint8_t)(clen >> 8);
-            out[4] = (uint8_t)clen;
-            out[5] = (uint8_t)(n >> 8);
-            out[6] = (uint8_t)n;
+            out.set(0, 'Z');
+            out.set(1, 'V');
+            out.set(2, 1);
+            out.set(3, (uint8_t)(clen >> 8));
+            out.set(4, (uint8_t)clen);
+            out.set(5, (uint8_t)(n >> 8));
+            out.set(6, (uint8_t)n);
+            out.finish(clen + 7);
             return (uint32_t)clen + 7;
         }
     }
-    out[0] = 'Z';
-    out[1] = 'V';
-    out[2] = 0;
-    out[3] = (uint8_t)(n >> 8);
-    out[4] = (uint8_t)n;
-    for (int32_t i = 0; i < n; ++i) out[5 + i] = in[i];
+    out.set(0, 'Z');
+    out.set(1, 'V');
+    out.set(2, 0);
+    out.set(3, (uint8_t)(n >> 8));
+    out.set(4, (uint8_t)n);
+    for (int32_t i = 0; i < n; ++i) out.set(5 + i, in[i]);
+    out.finish(n + 5);
     return (uint32_t)n + 5;
 }
 
@@ -158,6 +162,11 @@ __global__ void __launch_bounds__(256) k_encode(const uint8_t* __restrict__ in, 
     uint32_t tid, nthreads;
     if (!chunk_slot<SPREAD>(tid, nthreads)) return;
     uint32_t* htab = ws + (size_t)tid * HSIZE;
+    uint8_t* slot = nullptr;
+    if constexpr (!SPREAD) {
+        __shared__ __attribute__((aligned(16))) uint8_t stages[256 * kStageStride];
+        slot = &stages[threadIdx.x * kStageStride];
+    }
     uint32_t iter = 0;
     for (uint32_t c = tid; c < n; c += nthreads, ++iter) {
         const uint32_t len = in_len[c];
@@ -167,7 +176,13 @@ __global__ void __launch_bounds__(256) k_encode(const uint8_t* __restrict__ in, 
             continue;
         }
         const uint32_t stamp = ((stamp_base + iter) % 65535u) + 1u;
-        out_len[c] = encode_chunk(in + in_off[c], (int32_t)len, out + out_off[c], htab, stamp);
+        if (SPREAD) {
+            GOut o{out + out_off[c]};
+            out_len[c] = encode_chunk(in + in_off[c], (int32_t)len, o, htab, stamp);
+        } else {
+            ByteStage o(slot, out + out_off[c]);  // dense form: whole 128-byte units (nx_common.hpp)
+            out_len[c] = encode_chunk(in + in_off[c], (int32_t)len, o, htab, stamp);
+        }
         status[c] = NX_OK;
     }
 }

@@ -3,8 +3,18 @@
 // repeated), encoded R times with nx_snappy_encode_batch; prints the best kernel ms and an output
 // checksum (equal checksums = identical bytes).
 #include ENC_SRC
+#ifdef ENC_FASTLZ  // level AUTO (1 below 64 KiB), u16 limit = chunk length
+static int32_t fastlz_ab(const uint8_t* in, const uint64_t* io, const uint32_t* il, uint8_t* out, const uint64_t* oo, uint32_t* ol,
+                         int32_t* st, uint32_t n, void* s) {
+    return nx_fastlz_compress_batch(in, io, il, out, oo, ol, nullptr, nullptr, st, n, s);
+}
+#define ENC_FN fastlz_ab
+#endif
 #ifndef ENC_FN
 #define ENC_FN nx_snappy_encode_batch
+#endif
+#ifndef ENC_LEN
+#define ENC_LEN 65536
 #endif
 #include "../../include/netty_amd_textgen.h"
 #include <stdio.h>
@@ -12,7 +22,7 @@
 #include <vector>
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 262144, R = argc > 2 ? atoi(argv[2]) : 3;
-    const int L = 65536;
+    const int L = ENC_LEN;
     static nx_textgen_tables tg;
     nx_textgen_build(&tg);
     std::vector<uint8_t> h((size_t)1024 * L);
