@@ -211,8 +211,8 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
     return op;
 }
 
-__device__ int32_t decompress(const uint8_t* __restrict__ in, int32_t inLength, int32_t in_avail, uint8_t* __restrict__ out,
-                              int32_t outLength) {
+template <class O>
+__device__ int32_t decompress(const uint8_t* __restrict__ in, int32_t inLength, int32_t in_avail, O& out, int32_t outLength) {
     bool oob = false;
 #define FIN(i) ((i) < in_avail ? (int32_t)in[(i)] : (oob = true, 0))
     if (in_avail < 1) return NX_ERR_FASTLZ_INPUT_OOB;
@@ -268,21 +268,21 @@ __device__ int32_t decompress(const uint8_t* __restrict__ in, int32_t inLength, 
                 loop = 0;
             }
             if (ref == op) {
-                const uint8_t b = out[ref - 1];
-                out[op++] = b;
-                out[op++] = b;
-                out[op++] = b;
+                const uint32_t b = out.get((int32_t)ref - 1);
+                out.set(op++, b);
+                out.set(op++, b);
+                out.set(op++, b);
                 while (len != 0) {
-                    out[op++] = b;
+                    out.set(op++, b);
                     --len;
                 }
             } else {
                 ref--;
-                out[op++] = out[ref++];
-                out[op++] = out[ref++];
-                out[op++] = out[ref++];
+                out.set(op++, out.get((int32_t)ref++));
+                out.set(op++, out.get((int32_t)ref++));
+                out.set(op++, out.get((int32_t)ref++));
                 while (len != 0) {
-                    out[op++] = out[ref++];
+                    out.set(op++, out.get((int32_t)ref++));
                     --len;
                 }
             }
@@ -290,13 +290,14 @@ __device__ int32_t decompress(const uint8_t* __restrict__ in, int32_t inLength, 
             ctrl++;
             if (op + ctrl > outLength) return 0;
             if (ip + ctrl > inLength) return 0;
-            out[op++] = in[ip++];
-            for (--ctrl; ctrl != 0; ctrl--) out[op++] = in[ip++];
+            out.set(op++, in[ip++]);
+            for (--ctrl; ctrl != 0; ctrl--) out.set(op++, in[ip++]);
             loop = ip < inLength ? 1 : 0;
             if (loop) ctrl = in[ip++];
         }
     } while (loop != 0);
 #undef FIN
+    out.finish(op);
     return op;
 }
 
@@ -341,12 +342,15 @@ __global__ void __launch_bounds__(256) k_decompress(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ in_avail,
                                                     uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
                                                     const uint32_t* __restrict__ out_lim, int32_t* __restrict__ result, uint32_t n) {
+    // output through 64-byte LDS units (nx_common.hpp ByteStageT; 17 KiB per block keeps 8 blocks/CU)
+    __shared__ __attribute__((aligned(16))) uint8_t stages[256 * 68];
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nthreads = gridDim.x * blockDim.x;
     for (uint32_t c = tid; c < n; c += nthreads) {
         const uint32_t il = in_len[c];
         const uint32_t av = in_avail ? in_avail[c] : il;
-        result[c] = decompress(in + in_off[c], (int32_t)il, (int32_t)av, out + out_off[c], (int32_t)out_lim[c]);
+        ByteStageT<64> o(&stages[threadIdx.x * 68], out + out_off[c]);
+        result[c] = decompress(in + in_off[c], (int32_t)il, (int32_t)av, o, (int32_t)out_lim[c]);
     }
 }
 

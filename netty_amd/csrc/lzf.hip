@@ -125,7 +125,8 @@ __device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t n, O& o
     return (uint32_t)n + 5;
 }
 
-__device__ int32_t decode_chunk(const uint8_t* __restrict__ in, int32_t in_len, uint8_t* __restrict__ out, int32_t out_len) {
+template <class O>
+__device__ int32_t decode_chunk(const uint8_t* __restrict__ in, int32_t in_len, O& out, int32_t out_len) {
     int32_t ip = 0, op = 0;
     do {
         if (ip >= in_len) return NX_ERR_LZF_CORRUPT;
@@ -133,7 +134,7 @@ __device__ int32_t decode_chunk(const uint8_t* __restrict__ in, int32_t in_len, 
         if (ctrl < 32) {
             const int32_t k = ctrl + 1;
             if (ip + k > in_len || op + k > out_len) return NX_ERR_LZF_CORRUPT;
-            for (int32_t i = 0; i < k; ++i) out[op + i] = in[ip + i];
+            for (int32_t i = 0; i < k; ++i) out.set(op + i, in[ip + i]);
             ip += k;
             op += k;
             continue;
@@ -148,9 +149,10 @@ __device__ int32_t decode_chunk(const uint8_t* __restrict__ in, int32_t in_len, 
         ref -= in[ip++];
         len += 2;
         if (ref < 0 || op + len > out_len) return NX_ERR_LZF_CORRUPT;
-        for (int32_t i = 0; i < len; ++i) out[op + i] = out[ref + i];
+        for (int32_t i = 0; i < len; ++i) out.set(op + i, out.get(ref + i));
         op += len;
     } while (op < out_len);
+    out.finish(op);
     return op == out_len ? NX_OK : NX_ERR_LZF_CORRUPT;
 }
 
@@ -191,10 +193,14 @@ __global__ void __launch_bounds__(256) k_decode(const uint8_t* __restrict__ in, 
                                                 const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                 const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_len,
                                                 int32_t* __restrict__ status, uint32_t n) {
+    // output through 64-byte LDS units (nx_common.hpp ByteStageT; 17 KiB per block keeps 8 blocks/CU)
+    __shared__ __attribute__((aligned(16))) uint8_t stages[256 * 68];
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nthreads = gridDim.x * blockDim.x;
-    for (uint32_t c = tid; c < n; c += nthreads)
-        status[c] = decode_chunk(in + in_off[c], (int32_t)in_len[c], out + out_off[c], (int32_t)out_len[c]);
+    for (uint32_t c = tid; c < n; c += nthreads) {
+        ByteStageT<64> o(&stages[threadIdx.x * 68], out + out_off[c]);
+        status[c] = decode_chunk(in + in_off[c], (int32_t)in_len[c], o, (int32_t)out_len[c]);
+    }
 }
 
 }  // namespace lzf

@@ -105,25 +105,27 @@ struct GOut {
     __device__ __forceinline__ uint32_t get(int32_t pos) const { return p[pos]; }
     __device__ __forceinline__ void finish(int32_t) {}
 };
-struct ByteStage {
+// UNIT-byte units (64 or 128) in a lane slot of UNIT + 4 bytes
+template <uint32_t UNIT>
+struct ByteStageT {
     uint8_t* st;   // the lane's LDS slot
     uint8_t* dst;  // output byte 0
     int32_t u0;    // position of the staged unit's byte 0 (negative for the first, partial unit)
-    __device__ __forceinline__ ByteStage(uint8_t* slot, uint8_t* out)
-        : st(slot), dst(out), u0(-(int32_t)((uintptr_t)out & (kStageUnit - 1))) {}
+    __device__ __forceinline__ ByteStageT(uint8_t* slot, uint8_t* out)
+        : st(slot), dst(out), u0(-(int32_t)((uintptr_t)out & (UNIT - 1))) {}
     __device__ __forceinline__ void flush_unit() {
         const uint32_t* s32 = reinterpret_cast<const uint32_t*>(st);
         if (u0 >= 0) {
             uint4* g = reinterpret_cast<uint4*>(dst + u0);
 #pragma unroll
-            for (int q = 0; q < (int)kStageUnit / 16; ++q) g[q] = make_uint4(s32[4 * q], s32[4 * q + 1], s32[4 * q + 2], s32[4 * q + 3]);
+            for (int q = 0; q < (int)UNIT / 16; ++q) g[q] = make_uint4(s32[4 * q], s32[4 * q + 1], s32[4 * q + 2], s32[4 * q + 3]);
         } else {
-            for (int32_t j = -u0; j < (int32_t)kStageUnit; ++j) dst[u0 + j] = st[j];
+            for (int32_t j = -u0; j < (int32_t)UNIT; ++j) dst[u0 + j] = st[j];
         }
-        u0 += (int32_t)kStageUnit;
+        u0 += (int32_t)UNIT;
     }
     __device__ __forceinline__ void set(int32_t pos, uint32_t v) {
-        while (pos >= u0 + (int32_t)kStageUnit) flush_unit();
+        while (pos >= u0 + (int32_t)UNIT) flush_unit();
         if (pos >= u0)
             st[pos - u0] = (uint8_t)v;
         else
@@ -141,6 +143,7 @@ struct ByteStage {
         for (; j < end - u0; ++j) dst[u0 + j] = st[j];
     }
 };
+using ByteStage = ByteStageT<kStageUnit>;
 
 // Kernel launch helper: grid-stride sizes.
 inline unsigned grid_for(uint64_t threads, unsigned block) {
