@@ -3,6 +3,7 @@
 // allocate a fresh one.  Each trial prints the best of R launches and the workspace / buffer
 // addresses, to tell placement effects from clock or box effects.
 #include ENC_SRC
+#include "../../netty_amd/tools/probe_ceiling.hip"
 #include "../../include/netty_amd_textgen.h"
 #include <stdio.h>
 #include <string.h>
@@ -32,6 +33,16 @@ int main(int argc, char** argv) {
     hipEventCreate(&a); hipEventCreate(&b);
     std::vector<void*> spacers;
     for (int t = 0; t < T; ++t) {
+        if (mode == 2 || mode == 3) {  // workspace allocated here: 2 = physically contiguous, 3 = default flags
+            const size_t bytes = (size_t)262144 * 16384 * 8;
+            void* p = nullptr;
+            if (hipExtMallocWithFlags(&p, bytes, mode == 2 ? hipDeviceMallocContiguous : hipDeviceMallocDefault) != hipSuccess) {
+                printf("alloc failed\n");
+                return 5;
+            }
+            hipMemset(p, 0, bytes);
+            g_ws[{0, (hipStream_t)0}] = Workspace{(uint64_t*)p, 262144, 0};
+        }
         float best = 1e30f, worst = 0.f;
         for (int r = 0; r < R; ++r) {
             hipEventRecord(a);
@@ -45,7 +56,22 @@ int main(int argc, char** argv) {
         }
         void* wsp = nullptr;
         for (auto& kv : g_ws) wsp = kv.second.ws;
-        printf("%s trial %d best %.2f worst %.2f ms  ws %p in %p out %p\n", ENC_NAME, t, best, worst, wsp, (void*)din, (void*)dout);
+        // the same workspace under the encoder's request pattern without compute (probe_ceiling.hip)
+        float pms[2] = {0.f, 0.f};
+        for (int k = 0; k < 2; ++k)
+            nx_probe_ceiling((uint64_t*)wsp, (const uint32_t*)din, olen, (uint32_t)std::min(N, 262144), k ? 1024u : 256u, 258u, &pms[k], 0);
+        printf("%s trial %d best %.2f worst %.2f ms  probe256 %.3f probe1024 %.3f ms  ws %p in %p out %p\n", ENC_NAME, t, best, worst,
+               pms[0], pms[1], wsp, (void*)din, (void*)dout);
+        if (mode >= 1) {  // the same probe over each 4 GiB piece of the workspace alone (32 768 lanes)
+            printf("   pieces:");
+            for (int k = 0; k < 8; ++k) {
+                float m = 0.f;
+                nx_probe_ceiling((uint64_t*)wsp + (size_t)k * 32768 * 16384, (const uint32_t*)(din + (size_t)k * 32768 * L), olen, 32768u,
+                                 512u, 258u, &m, 0);
+                printf(" %.3f", m);
+            }
+            printf("\n");
+        }
         fflush(stdout);
         for (auto& kv : g_ws) hipFree(kv.second.ws);
         g_ws.clear();
