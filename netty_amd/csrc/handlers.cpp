@@ -113,9 +113,23 @@ extern "C" int64_t nx_snappy_frame_encoder_encode(nx_snappy_frame_encoder* e, co
                                g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), g.a4.as<int32_t>(), ns, g.s);
     if (r != NX_OK) return r;
     std::vector<uint32_t> clen(ns), crc(ns);
-    std::vector<uint8_t> hout(ocur);
-    ok = g.d2h(clen.data(), g.a3.p, 4ull * ns) && g.d2h(crc.data(), g.a5.p, 4ull * ns) && g.d2h(hout.data(), g.dout.p, ocur) && g.sync();
+    ok = g.d2h(clen.data(), g.a3.p, 4ull * ns) && g.d2h(crc.data(), g.a5.p, 4ull * ns) && g.sync();
     if (!ok) return NX_ERR_HIP;
+    // the framed layout is known once the lengths are: each compressed chunk's bytes (and nothing
+    // else of its slot) go straight to their place in `out`
+    {
+        size_t q = op;
+        for (uint32_t i = 0; i < ns && ok; ++i) {
+            if (sl[i].comp) {
+                if ((clen[i] + 4) >> 24) return NX_ERR_INVALID_ARG;  // setChunkLength (:126-132)
+                ok = g.d2h(out + q + 8, g.dout.as<uint8_t>() + ooff[i], clen[i]);
+                q += 8 + clen[i];
+            } else {
+                q += 8 + sl[i].len;
+            }
+        }
+        if (!ok || !g.sync()) return NX_ERR_HIP;
+    }
     for (uint32_t i = 0; i < ns; ++i) {
         if (sl[i].comp) {
             const uint32_t chunkLength = clen[i] + 4;  // setChunkLength (:126-132)
@@ -125,9 +139,7 @@ extern "C" int64_t nx_snappy_frame_encoder_encode(nx_snappy_frame_encoder* e, co
             out[op++] = (uint8_t)(chunkLength >> 8);
             out[op++] = (uint8_t)(chunkLength >> 16);
             memcpy(out + op, &crc[i], 4);
-            op += 4;
-            memcpy(out + op, hout.data() + ooff[i], clen[i]);
-            op += clen[i];
+            op += 4 + clen[i];  // payload already copied from the device
         } else {
             const uint32_t cl = sl[i].len + 4;
             out[op++] = 1;
@@ -210,7 +222,7 @@ extern "C" int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, co
         const uint32_t ncomp = (uint32_t)comp_idx.size(), nunc = (uint32_t)unc_idx.size(), nj = ncomp + nunc;
         std::vector<uint32_t> olen(ncomp), cons(ncomp), ucrc(nunc);
         std::vector<int32_t> st(ncomp);
-        std::vector<uint8_t> hout((size_t)ncomp * 65536);
+        std::vector<std::vector<uint8_t>> outs(ncomp);  // each decoded chunk, exactly olen bytes
         Gpu& g = d->g;
         if (nj) {
             const size_t span = hi - lo;
@@ -249,9 +261,15 @@ extern "C" int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, co
                 if (r != NX_OK) return finish(r);
             }
             ok = g.d2h(olen.data(), g.a3.p, 4ull * ncomp) && g.d2h(cons.data(), g.a4.p, 4ull * ncomp) &&
-                 g.d2h(st.data(), d_st, 4ull * ncomp) && g.d2h(ucrc.data(), d_ucrc, 4ull * nunc) &&
-                 g.d2h(hout.data(), g.dout.p, (size_t)ncomp * 65536) && g.sync();
+                 g.d2h(st.data(), d_st, 4ull * ncomp) && g.d2h(ucrc.data(), d_ucrc, 4ull * nunc) && g.sync();
             if (!ok) return finish(NX_ERR_HIP);
+            // only the bytes each chunk produced cross PCIe (a message's olen, not its 64 KiB slot)
+            for (uint32_t j = 0; j < ncomp && ok; ++j) {
+                if (st[j] != NX_OK && st[j] != NX_ERR_SNAPPY_CRC_MISMATCH) continue;
+                outs[j].resize(olen[j]);
+                ok = g.d2h(outs[j].data(), g.dout.as<uint8_t>() + (size_t)j * 65536, olen[j]);
+            }
+            if (!ok || !g.sync()) return finish(NX_ERR_HIP);
         }
         // ---- apply in stream order (the first failing chunk ends the call, as the Java exception does)
         bool reparse = false;
@@ -268,13 +286,13 @@ extern "C" int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, co
                 ml.msgs.push_back({in + a.data, a.dlen});  // readRetainedSlice: a view of the cumulation
             } else if (a.kind == SAct::Comp) {
                 const int j = a.job;
-                const uint8_t* outj = hout.data() + (size_t)j * 65536;
                 if (st[j] == NX_ERR_SNAPPY_CRC_MISMATCH) {
-                    snprintf(buf, sizeof buf, "mismatching checksum: %x (expected: %x)", nx::host_mask(nx::host_crc32c(outj, olen[j])), a.crc);
+                    snprintf(buf, sizeof buf, "mismatching checksum: %x (expected: %x)",
+                             nx::host_mask(nx::host_crc32c(outs[j].data(), olen[j])), a.crc);
                     return corrupt(a.end, st[j], buf);
                 }
                 if (st[j] != NX_OK) return corrupt(a.end, st[j], nx_status_string(st[j]));
-                ml.owned.emplace_back(outj, outj + olen[j]);
+                ml.owned.push_back(std::move(outs[j]));
                 ml.msgs.push_back({ml.owned.back().data(), olen[j]});
                 if (d->validate && cons[j] < a.dlen) {
                     // validating mode restores the writer index and leaves the unread chunk bytes in
