@@ -372,9 +372,7 @@ extern "C" int64_t nx_fastlz_frame_encoder_encode(nx_fastlz_frame_encoder* e, co
         if (r != NX_OK) return r;
     }
     std::vector<uint32_t> clen(nc);
-    std::vector<uint8_t> hout(oc);
-    ok = g.d2h(clen.data(), g.a3.p, 4ull * nc) && g.d2h(hout.data(), g.dout.p, oc) && (!e->checksum || g.d2h(ad.data(), g.a4.p, 4ull * nc)) &&
-         g.sync();
+    ok = g.d2h(clen.data(), g.a3.p, 4ull * nc) && (!e->checksum || g.d2h(ad.data(), g.a4.p, 4ull * nc)) && g.sync();
     if (!ok) return NX_ERR_HIP;
     size_t op = 0;
     for (uint32_t i = 0; i < nc; ++i) {
@@ -399,7 +397,8 @@ extern "C" int64_t nx_fastlz_frame_encoder_encode(nx_fastlz_frame_encoder* e, co
             out[outputOffset] = (uint8_t)(chunkLength >> 8);
             out[outputOffset + 1] = (uint8_t)chunkLength;
             outputOffset += 2;
-            memcpy(out + outputOffset + 2, hout.data() + ooff[i], chunkLength);
+            // only the compressed bytes cross PCIe, straight into their framed position
+            if (!g.d2h(out + outputOffset + 2, g.dout.as<uint8_t>() + ooff[i], chunkLength)) return NX_ERR_HIP;
         } else {
             blockType = 0;
             chunkLength = length;
@@ -410,6 +409,7 @@ extern "C" int64_t nx_fastlz_frame_encoder_encode(nx_fastlz_frame_encoder* e, co
         out[outputIdx + 3] = (uint8_t)(blockType | (e->checksum ? 0x10 : 0));
         op = outputOffset + 2 + chunkLength;
     }
+    if (!g.sync()) return NX_ERR_HIP;
     return (int64_t)op;
 }
 
@@ -704,14 +704,14 @@ extern "C" int64_t nx_lzf_encoder_encode(nx_lzf_encoder* e, const uint8_t* in, s
                                     g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), g.a4.as<int32_t>(), nc, g.s);
     if (r != NX_OK) return r;
     std::vector<uint32_t> olen(nc);
-    std::vector<uint8_t> hout(oc);
-    ok = g.d2h(olen.data(), g.a3.p, 4ull * nc) && g.d2h(hout.data(), g.dout.p, oc) && g.sync();
+    ok = g.d2h(olen.data(), g.a3.p, 4ull * nc) && g.sync();
     if (!ok) return NX_ERR_HIP;
     size_t op = 0;
-    for (uint32_t i = 0; i < nc; ++i) {
-        memcpy(out + op, hout.data() + ooff[i], olen[i]);
+    for (uint32_t i = 0; i < nc && ok; ++i) {  // each block's bytes only, concatenated in place
+        ok = g.d2h(out + op, g.dout.as<uint8_t>() + ooff[i], olen[i]);
         op += olen[i];
     }
+    if (!ok || !g.sync()) return NX_ERR_HIP;
     return (int64_t)op;
 }
 
@@ -930,17 +930,20 @@ int64_t lz4_flush_blocks(nx_lz4_frame_encoder* e, const uint8_t* src, size_t n, 
     if (r != NX_OK) return r;
     std::vector<uint32_t> olen(nb);
     std::vector<int32_t> st(nb);
-    std::vector<uint8_t> hout(oc);
-    ok = g.d2h(olen.data(), g.a3.p, 4ull * nb) && g.d2h(st.data(), g.a4.p, 4ull * nb) && g.d2h(hout.data(), g.dout.p, oc) &&
-         g.sync();
+    ok = g.d2h(olen.data(), g.a3.p, 4ull * nb) && g.d2h(st.data(), g.a4.p, 4ull * nb) && g.sync();
     if (!ok) return NX_ERR_HIP;
     size_t op = 0;
     for (uint32_t i = 0; i < nb; ++i) {
         if (st[i] != NX_OK) return st[i];
         if (op + olen[i] > out_cap) return NX_ERR_INVALID_ARG;
-        memcpy(out + op, hout.data() + ooff[i], olen[i]);
         op += olen[i];
     }
+    op = 0;
+    for (uint32_t i = 0; i < nb && ok; ++i) {  // each framed block's bytes only, concatenated in place
+        ok = g.d2h(out + op, g.dout.as<uint8_t>() + ooff[i], olen[i]);
+        op += olen[i];
+    }
+    if (!ok || !g.sync()) return NX_ERR_HIP;
     return (int64_t)op;
 }
 }  // namespace
