@@ -328,22 +328,25 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
         // source bytes lie in this pass depends on the contiguous piece range that produces them,
         // and runs in the first round after all of those are done.  The map aliases `scratch`
         // (its piece marks were consumed above).
+        // Only a near copy whose source reaches into this pass's output [ps, pe) can depend on it;
+        // passes without one (all literals, far or older sources) skip the map and run one round.
         const uint32_t psal = ps & ~3u;
+        const uint32_t dhi = overlap ? tstart : sp + nbytes;  // end of the source bytes this piece reads
+        const bool dep = valid && !lit && !gl && dhi > ps;
         uint64_t need = 0;
-        wave_sync();
-        {
-            const uint32_t mm = valid ? bmask : 0u;
-            const uint32_t maddr = lds_base + (uint32_t)offsetof(WaveLds, scratch) + (valid ? 4u * ((x0 >> 2) - (psal >> 2)) : 0u);
-            asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(maddr), "v"(mm), "v"(((uint32_t)lane * 0x01010101u) & mm) : "memory");
-        }
-        wave_sync();
-        if (valid && !lit && !gl) {
-            const uint32_t lo0 = overlap ? tstart - xo : sp;
-            const uint32_t hi = overlap ? tstart : sp + nbytes;
-            if (hi > ps) {
+        if (__ballot(dep)) {
+            wave_sync();
+            {
+                const uint32_t mm = valid ? bmask : 0u;
+                const uint32_t maddr = lds_base + (uint32_t)offsetof(WaveLds, scratch) + (valid ? 4u * ((x0 >> 2) - (psal >> 2)) : 0u);
+                asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(maddr), "v"(mm), "v"(((uint32_t)lane * 0x01010101u) & mm) : "memory");
+            }
+            wave_sync();
+            if (dep) {
+                const uint32_t lo0 = overlap ? tstart - xo : sp;
                 const uint8_t* M8 = reinterpret_cast<const uint8_t*>(L.scratch);
                 const uint32_t lo = lo0 > ps ? lo0 : ps;
-                const uint32_t pa = M8[lo - psal], pb = M8[hi - 1u - psal];
+                const uint32_t pa = M8[lo - psal], pb = M8[dhi - 1u - psal];
                 need = (pb >= 63u ? ~0ull : ((2ull << pb) - 1ull)) & ~((1ull << (pa & 63u)) - 1ull);
             }
         }
