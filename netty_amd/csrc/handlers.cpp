@@ -117,18 +117,19 @@ extern "C" int64_t nx_snappy_frame_encoder_encode(nx_snappy_frame_encoder* e, co
     if (!ok) return NX_ERR_HIP;
     // the framed layout is known once the lengths are: each compressed chunk's bytes (and nothing
     // else of its slot) go straight to their place in `out`
+    for (uint32_t i = 0; i < ns; ++i)
+        if (sl[i].comp && ((clen[i] + 4) >> 24)) return NX_ERR_INVALID_ARG;  // setChunkLength (:126-132)
     {
         size_t q = op;
         for (uint32_t i = 0; i < ns && ok; ++i) {
             if (sl[i].comp) {
-                if ((clen[i] + 4) >> 24) return NX_ERR_INVALID_ARG;  // setChunkLength (:126-132)
                 ok = g.d2h(out + q + 8, g.dout.as<uint8_t>() + ooff[i], clen[i]);
                 q += 8 + clen[i];
             } else {
                 q += 8 + sl[i].len;
             }
         }
-        if (!ok || !g.sync()) return NX_ERR_HIP;
+        if (!g.sync() || !ok) return NX_ERR_HIP;
     }
     for (uint32_t i = 0; i < ns; ++i) {
         if (sl[i].comp) {
@@ -269,7 +270,7 @@ extern "C" int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, co
                 outs[j].resize(olen[j]);
                 ok = g.d2h(outs[j].data(), g.dout.as<uint8_t>() + (size_t)j * 65536, olen[j]);
             }
-            if (!ok || !g.sync()) return finish(NX_ERR_HIP);
+            if (!g.sync() || !ok) return finish(NX_ERR_HIP);
         }
         // ---- apply in stream order (the first failing chunk ends the call, as the Java exception does)
         bool reparse = false;
@@ -398,7 +399,7 @@ extern "C" int64_t nx_fastlz_frame_encoder_encode(nx_fastlz_frame_encoder* e, co
             out[outputOffset + 1] = (uint8_t)chunkLength;
             outputOffset += 2;
             // only the compressed bytes cross PCIe, straight into their framed position
-            if (!g.d2h(out + outputOffset + 2, g.dout.as<uint8_t>() + ooff[i], chunkLength)) return NX_ERR_HIP;
+            ok = ok && g.d2h(out + outputOffset + 2, g.dout.as<uint8_t>() + ooff[i], chunkLength);
         } else {
             blockType = 0;
             chunkLength = length;
@@ -409,7 +410,7 @@ extern "C" int64_t nx_fastlz_frame_encoder_encode(nx_fastlz_frame_encoder* e, co
         out[outputIdx + 3] = (uint8_t)(blockType | (e->checksum ? 0x10 : 0));
         op = outputOffset + 2 + chunkLength;
     }
-    if (!g.sync()) return NX_ERR_HIP;
+    if (!g.sync() || !ok) return NX_ERR_HIP;  // every queued copy has landed (or failed) before returning
     return (int64_t)op;
 }
 
@@ -711,7 +712,7 @@ extern "C" int64_t nx_lzf_encoder_encode(nx_lzf_encoder* e, const uint8_t* in, s
         ok = g.d2h(out + op, g.dout.as<uint8_t>() + ooff[i], olen[i]);
         op += olen[i];
     }
-    if (!ok || !g.sync()) return NX_ERR_HIP;
+    if (!g.sync() || !ok) return NX_ERR_HIP;
     return (int64_t)op;
 }
 
@@ -943,7 +944,7 @@ int64_t lz4_flush_blocks(nx_lz4_frame_encoder* e, const uint8_t* src, size_t n, 
         ok = g.d2h(out + op, g.dout.as<uint8_t>() + ooff[i], olen[i]);
         op += olen[i];
     }
-    if (!ok || !g.sync()) return NX_ERR_HIP;
+    if (!g.sync() || !ok) return NX_ERR_HIP;
     return (int64_t)op;
 }
 }  // namespace
