@@ -61,6 +61,11 @@ int main(int argc, char** argv) {
         for (uint32_t k = 0; k < ol[i]; ++k) sum = sum * 1000003ull + ob[k];
     }
     for (int i = 0; i < N; ++i) tot += ol[i];
+#ifdef ENC_SEL_DIAG
+    printf("  candidates:");
+    for (int k = 0; k < g_pn; ++k) printf(" %.3f", g_pms[k]);
+    printf("  pick %d\n", g_pick);
+#endif
     printf("%s N=%d best %.2f ms  %.1f GiB/s  out %llu B  checksum %016llx\n", ENC_NAME, N, best, (double)N * L / (best / 1e3) / (1 << 30), tot, sum);
     return 0;
 }

@@ -59,8 +59,8 @@ int main(int argc, char** argv) {
         // the same workspace under the encoder's request pattern without compute (probe_ceiling.hip)
         float pms[2] = {0.f, 0.f};
         for (int k = 0; k < 2; ++k)
-            nx_probe_ceiling((uint64_t*)wsp, (const uint32_t*)din, olen, (uint32_t)std::min(N, 262144), k ? 1024u : 256u, 258u, &pms[k], 0);
-        printf("%s trial %d best %.2f worst %.2f ms  probe256 %.3f probe1024 %.3f ms  ws %p in %p out %p\n", ENC_NAME, t, best, worst,
+            nx_probe_ceiling((uint64_t*)wsp, (const uint32_t*)din, olen, (uint32_t)std::min(N, 262144), k ? 1024u : 256u, k ? 258u : 0u, &pms[k], 0);
+        printf("%s trial %d best %.2f worst %.2f ms  probe256(exchanges only) %.3f probe1024(+25.8%% loads) %.3f ms  ws %p in %p out %p\n", ENC_NAME, t, best, worst,
                pms[0], pms[1], wsp, (void*)din, (void*)dout);
         if (mode >= 1) {  // the same probe over each 4 GiB piece of the workspace alone (32 768 lanes)
             printf("   pieces:");
