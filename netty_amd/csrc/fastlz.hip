@@ -449,8 +449,7 @@ extern "C" int32_t nx_fastlz_compress_batch(const uint8_t* in, const uint64_t* i
     if (W.ws == nullptr || W.slots < g.slots) {
         if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
         W.ws = nullptr;
-        NX_HIP_CHECK(hipMalloc(&W.ws, g.slots * per));
-        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, g.slots * per, st));
+        NX_HIP_CHECK(nx::alloc_placed_workspace<uint32_t>(g.slots, nx::flz::HASH_LOG, st, &W.ws));
         W.slots = g.slots;
         W.stamp = 0;
     }

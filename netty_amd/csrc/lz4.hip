@@ -222,8 +222,7 @@ extern "C" int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off
     if (W.ws == nullptr || W.threads < threads) {
         if (W.ws) NX_HIP_CHECK(hipFree(W.ws));
         W.ws = nullptr;
-        NX_HIP_CHECK(hipMalloc(&W.ws, threads * per));
-        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, threads * per, st));
+        NX_HIP_CHECK(nx::alloc_placed_workspace<uint32_t>(threads, 13, st, &W.ws));  // 8192 slots per table
         W.threads = threads;
         W.stamp = 0;
     }

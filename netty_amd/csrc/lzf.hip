@@ -235,8 +235,7 @@ extern "C" int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off
     if (W.ws == nullptr || W.slots < g.slots) {
         if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
         W.ws = nullptr;
-        NX_HIP_CHECK(hipMalloc(&W.ws, g.slots * per));
-        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, g.slots * per, st));
+        NX_HIP_CHECK(nx::alloc_placed_workspace<uint32_t>(g.slots, 14, st, &W.ws));  // HSIZE = 2^14
         W.slots = g.slots;
         W.stamp = 0;
     }

@@ -145,6 +145,78 @@ struct ByteStageT {
 };
 using ByteStage = ByteStageT<kStageUnit>;
 
+// Hash-table workspace placement (the lane-per-chunk encoders' per-lane tables).  How fast the memory
+// system serves a lane's chain of random table exchanges depends on where the workspace landed: the
+// Snappy encoder runs 260-274 or 330-345 ms per 262 144 chunks on the same box depending only on the
+// placement of its 32 GiB workspace, and a 3-4 ms run of k_ws_probe — lane t: `steps` dependent
+// exchanges at pseudo-random slots of its own table, the encoders' probe request without their
+// compute — predicts which (profiles/r02/s3/placement_selection.log).
+template <typename E>
+__global__ void __launch_bounds__(256) k_ws_probe(E* __restrict__ ws, uint32_t per_lane, uint32_t lg, uint32_t steps) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    E* tab = ws + (size_t)t * per_lane;
+    uint32_t h = t * 0x9E3779B9u + 1u;
+    for (uint32_t i = 0; i < steps; ++i) {
+        const E v = __hip_atomic_exchange(&tab[(h * 0x1e35a7bdu) >> (32u - lg)], (E)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h = h * 0x85EBCA77u + (uint32_t)v + i;
+    }
+}
+constexpr size_t kPlaceMinBytes = (size_t)2 << 30;  // smaller workspaces (handler / batcher sizes): allocated directly
+constexpr int kPlaceCandidates = 6;
+constexpr uint32_t kPlaceSteps = 256;
+
+// Allocate a zeroed workspace of `lanes` tables of 2^lg entries each.  A large one is the fastest of
+// up to kPlaceCandidates allocations under k_ws_probe (the others stay allocated while the next is
+// drawn, so it lands elsewhere, and are freed after); a candidate is only drawn while 8 GiB stay free.
+template <typename E>
+inline hipError_t alloc_placed_workspace(size_t lanes, uint32_t lg, hipStream_t st, E** out) {
+    const size_t bytes = lanes * ((size_t)sizeof(E) << lg);
+    *out = nullptr;
+    if (bytes < kPlaceMinBytes || lanes % 256 != 0) {
+        hipError_t e = hipMalloc(out, bytes);
+        if (e == hipSuccess) e = hipMemsetAsync(*out, 0, bytes, st);
+        return e;
+    }
+    E* cand[kPlaceCandidates];
+    float ms[kPlaceCandidates];
+    int nc = 0;
+    hipEvent_t a = nullptr, b = nullptr;
+    hipError_t e = hipEventCreate(&a);
+    if (e == hipSuccess) e = hipEventCreate(&b);
+    while (nc < kPlaceCandidates && e == hipSuccess) {
+        size_t free_b = 0, total_b = 0;
+        if (nc > 0 && (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + ((size_t)8 << 30))) break;
+        E* p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();  // no memory for another candidate: choose among those drawn
+            break;
+        }
+        cand[nc] = p;
+        ms[nc] = 3.4e38f;
+        ++nc;
+        e = hipMemsetAsync(p, 0, bytes, st);  // first touch outside the timed probe
+        if (e == hipSuccess) e = hipEventRecord(a, st);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_ws_probe<E>, dim3((unsigned)(lanes / 256)), dim3(256), 0, st, p, 1u << lg, lg, kPlaceSteps);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipEventRecord(b, st);
+        if (e == hipSuccess) e = hipEventSynchronize(b);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms[nc - 1], a, b);
+    }
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    int best = 0;
+    for (int k = 1; k < nc; ++k)
+        if (ms[k] < ms[best]) best = k;
+    for (int k = 0; k < nc; ++k)
+        if (k != best || e != hipSuccess) (void)hipFree(cand[k]);
+    if (e != hipSuccess) return e;
+    if (nc == 0) return hipErrorOutOfMemory;
+    *out = cand[best];
+    return hipMemsetAsync(*out, 0, bytes, st);  // the probe wrote entries: back to a zeroed table
+}
+
 // Kernel launch helper: grid-stride sizes.
 inline unsigned grid_for(uint64_t threads, unsigned block) {
     uint64_t g = (threads + block - 1) / block;

@@ -650,21 +650,6 @@ __global__ void __launch_bounds__(64) k_snappy_encode_lds(const uint8_t* __restr
     }
 }
 
-// Workspace placement probe: lane t runs `steps` dependent exchanges at pseudo-random slots of its
-// own 16 384-entry table — the encoder's probe request without its compute.  How fast the memory
-// system serves this pattern depends on where the workspace landed (profiles/r02/s3/
-// encoder_output_staging.md: 3.1-3.3 ms per 256 steps over 262 144 lanes in the placements where the
-// encoder takes 263-274 ms per 262 144 chunks, 3.8-3.9 ms where it takes 336-345 ms).
-__global__ void __launch_bounds__(256) k_ws_probe(uint64_t* __restrict__ ws, uint32_t steps) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t* tab = ws + (size_t)t * 16384u;
-    uint32_t h = t * 0x9E3779B9u + 1u;
-    for (uint32_t i = 0; i < steps; ++i) {
-        const uint64_t v = __hip_atomic_exchange(&tab[(h * 0x1e35a7bdu) >> 18], (uint64_t)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        h = h * 0x85EBCA77u + (uint32_t)v + i;
-    }
-}
-
 }  // namespace enc
 }  // namespace nx
 
@@ -682,63 +667,6 @@ constexpr unsigned kEncBlock = 256;
 constexpr unsigned kEncWavesPerCU = 16;
 constexpr uint32_t kMaxStamp = 63;  // 6-bit stamps 1..63
 constexpr uint32_t kSpreadMaxChunks = 16384;  // above this the dense form is faster
-constexpr size_t kPlaceMinBytes = (size_t)4 << 30;    // workspaces this large choose their placement
-constexpr int kPlaceCandidates = 6;
-constexpr uint32_t kPlaceSteps = 256;
-
-// Allocate a zeroed dense-form workspace of `slots` tables.  The encoder's speed depends on where its
-// tables land (up to 30 % on one box, `profiles/r02/s3/`), and a 3-4 ms probe of the encoder's own
-// request pattern over a candidate predicts it; a large workspace therefore takes the fastest of up
-// to kPlaceCandidates allocations (the others stay allocated while the next is drawn, so it lands
-// elsewhere, and are freed after), as long as free memory keeps 8 GiB of headroom.  Small
-// workspaces (handler / batcher sizes) are allocated directly.
-hipError_t alloc_workspace(size_t slots, size_t bytes, hipStream_t st, uint64_t** out) {
-    *out = nullptr;
-    if (bytes < kPlaceMinBytes || slots % 256 != 0) {
-        hipError_t e = hipMalloc(out, bytes);
-        if (e == hipSuccess) e = hipMemsetAsync(*out, 0, bytes, st);
-        return e;
-    }
-    std::vector<uint64_t*> cand;
-    std::vector<float> ms;
-    hipEvent_t a = nullptr, b = nullptr;
-    hipError_t e = hipEventCreate(&a);
-    if (e == hipSuccess) e = hipEventCreate(&b);
-    for (int k = 0; k < kPlaceCandidates && e == hipSuccess; ++k) {
-        size_t free_b = 0, total_b = 0;
-        if (k > 0 && (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + ((size_t)8 << 30))) break;
-        uint64_t* p = nullptr;
-        if (hipMalloc(&p, bytes) != hipSuccess) {
-            (void)hipGetLastError();  // out of memory for another candidate: choose among those we have
-            break;
-        }
-        cand.push_back(p);
-        float t = 0.f;
-        e = hipMemsetAsync(p, 0, bytes, st);  // first touch outside the timed probe
-        if (e == hipSuccess) e = hipEventRecord(a, st);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(nx::enc::k_ws_probe, dim3((unsigned)(slots / 256)), dim3(256), 0, st, p, kPlaceSteps);
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess) e = hipEventRecord(b, st);
-        if (e == hipSuccess) e = hipEventSynchronize(b);
-        if (e == hipSuccess) e = hipEventElapsedTime(&t, a, b);
-        ms.push_back(t);
-    }
-    if (a) (void)hipEventDestroy(a);
-    if (b) (void)hipEventDestroy(b);
-    size_t best = 0;
-    for (size_t k = 1; k < ms.size(); ++k)
-        if (ms[k] < ms[best]) best = k;
-    for (size_t k = 0; k < cand.size(); ++k)
-        if (k != best) (void)hipFree(cand[k]);
-    if (e != hipSuccess || cand.empty()) {
-        if (!cand.empty()) (void)hipFree(cand[best]);
-        return e != hipSuccess ? e : hipErrorOutOfMemory;
-    }
-    *out = cand[best];
-    return hipMemsetAsync(*out, 0, bytes, st);  // the probe wrote entries: back to Java's zeroed table
-}
 }  // namespace
 
 extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
@@ -773,7 +701,8 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
     if (W.ws == nullptr || W.threads < slots) {
         if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
         W.ws = nullptr;
-        NX_HIP_CHECK(alloc_workspace(spread ? 0 : slots, slots * per, st, &W.ws));
+        // dense form: the fastest of several placements (nx_common.hpp alloc_placed_workspace)
+        NX_HIP_CHECK(nx::alloc_placed_workspace<uint64_t>(slots, 14, st, &W.ws));
         W.threads = slots;
         W.stamp = 0;
     }
