@@ -389,6 +389,19 @@ def probe_ceiling(torch, dev, lanes=262144, steps=16384):
     del tabs, inp, sink
     torch.cuda.empty_cache()
     return best
+def encoder_placement():
+    """Probe times of the candidate placements the encoder's workspace was chosen from."""
+    import ctypes
+    from netty_amd import _lib
+    L = _lib.load()
+    ms = (ctypes.c_float * 8)()
+    n, pick = ctypes.c_int32(0), ctypes.c_int32(-1)
+    if L.nx_snappy_encode_placement(ms, 8, ctypes.byref(n), ctypes.byref(pick)) != 0:
+        return None
+    return {"note": "k_ws_probe ms per candidate workspace (256 dependent exchanges per lane); the encoder keeps the fastest",
+            "probe_ms": [round(ms[k], 3) for k in range(n.value)], "pick": pick.value}
+
+
 DEC_KERNELS = ["nx::dec::k_parse", "nx::dec::k_expand"]
 
 
@@ -460,6 +473,8 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
             "ceiling_probes_per_s": round(ceil / 1e9, 3) * 1e9 if ceil else None,
             "frac": round(got / ceil, 4) if ceil else None,
             "ceiling_source": "netty_amd/tools/probe_ceiling.hip, same request mix without compute, 262144 lanes, timed live, fastest of up to 3 table placements (as the encoder chooses its workspace)"}
+    if gpu:
+        r_enc["workspace_placement"] = encoder_placement()
     dominant = r_enc if t_enc >= t_dec else r_dec
     value = args.total_chunks * CHUNK / elapsed * args.steps / 2**30
     line = {

@@ -51,6 +51,11 @@ int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const 
                                uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
                                int32_t* status, uint32_t n, void* stream);
 
+/* Diagnostics (no reference counterpart): the probe times in ms of the candidate workspace placements
+ * the encoder's last large hash-table workspace was chosen from, and the index kept
+ * (DESIGN.md §3).  *n = 0 before any such workspace exists. */
+int32_t nx_snappy_encode_placement(float* probe_ms, int32_t cap, int32_t* n, int32_t* pick);
+
 /* Replaces Snappy.decode(ByteBuf in, ByteBuf out)  Snappy.java:315-393 as driven by
  * SnappyFrameDecoder.decode for one COMPRESSED_DATA chunk (SnappyFrameDecoder.java:194-224),
  * fused with Snappy.validateChecksum over the output (Snappy.java:700-707).

@@ -168,8 +168,13 @@ constexpr uint32_t kPlaceSteps = 256;
 // Allocate a zeroed workspace of `lanes` tables of 2^lg entries each.  A large one is the fastest of
 // up to kPlaceCandidates allocations under k_ws_probe (the others stay allocated while the next is
 // drawn, so it lands elsewhere, and are freed after); a candidate is only drawn while 8 GiB stay free.
+struct PlacementReport {
+    int n = 0;      // candidates probed (0: allocated directly, below kPlaceMinBytes)
+    int pick = -1;  // the one kept
+    float ms[kPlaceCandidates] = {};
+};
 template <typename E>
-inline hipError_t alloc_placed_workspace(size_t lanes, uint32_t lg, hipStream_t st, E** out) {
+inline hipError_t alloc_placed_workspace(size_t lanes, uint32_t lg, hipStream_t st, E** out, PlacementReport* rep = nullptr) {
     const size_t bytes = lanes * ((size_t)sizeof(E) << lg);
     *out = nullptr;
     if (bytes < kPlaceMinBytes || lanes % 256 != 0) {
@@ -214,6 +219,11 @@ inline hipError_t alloc_placed_workspace(size_t lanes, uint32_t lg, hipStream_t 
     if (e != hipSuccess) return e;
     if (nc == 0) return hipErrorOutOfMemory;
     *out = cand[best];
+    if (rep) {
+        rep->n = nc;
+        rep->pick = best;
+        for (int k = 0; k < nc; ++k) rep->ms[k] = ms[k];
+    }
     return hipMemsetAsync(*out, 0, bytes, st);  // the probe wrote entries: back to a zeroed table
 }
 

@@ -662,6 +662,7 @@ struct Workspace {
     uint32_t stamp = 0;  // last stamp used; entries carry 6-bit stamps 1..63
 };
 std::mutex g_ws_mu;
+nx::PlacementReport g_place;  // the last dense-form workspace placement (nx_snappy_encode_placement)
 std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
 constexpr unsigned kEncBlock = 256;
 constexpr unsigned kEncWavesPerCU = 16;
@@ -702,7 +703,7 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
         if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
         W.ws = nullptr;
         // dense form: the fastest of several placements (nx_common.hpp alloc_placed_workspace)
-        NX_HIP_CHECK(nx::alloc_placed_workspace<uint64_t>(slots, 14, st, &W.ws));
+        NX_HIP_CHECK(nx::alloc_placed_workspace<uint64_t>(slots, 14, st, &W.ws, &g_place));
         W.threads = slots;
         W.stamp = 0;
     }
@@ -726,5 +727,16 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
         NX_HIP_CHECK(hipGetLastError());
         W.stamp += iters;
     }
+    return NX_OK;
+}
+
+// The probe times (ms) of the candidate placements the last large encoder workspace was chosen from
+// and the index kept; *n = 0 when no workspace has been placed yet.  Diagnostics only.
+extern "C" int32_t nx_snappy_encode_placement(float* probe_ms, int32_t cap, int32_t* n, int32_t* pick) {
+    if (!n || !pick || (cap > 0 && !probe_ms)) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    *n = g_place.n;
+    *pick = g_place.pick;
+    for (int32_t k = 0; k < g_place.n && k < cap; ++k) probe_ms[k] = g_place.ms[k];
     return NX_OK;
 }
