@@ -150,3 +150,28 @@ def test_lzf_decoder_units_unaligned(dev, B, oracle):
     st = B.lzf_decode(inp, off, ln, buf, ooff, olen)
     assert int((st != 0).sum()) == 0
     _check(buf, ooff, olen, dict(enumerate(plain)))
+
+
+def test_encoder_workspace_placement_report(dev, B, oracle):
+    """A dense-form encoder workspace of >= 2 GiB is the fastest of several probed placements
+    (nx_common.hpp alloc_placed_workspace); nx_snappy_encode_placement reports the probe times and
+    the index kept, which must be the fastest."""
+    import ctypes
+    from netty_amd import _lib
+    s = torch.cuda.Stream(dev)  # a fresh stream gets its own workspace, placed now
+    chunks = [b"placement" * 7] * N_DENSE
+    inp, off, ln = B.pack(chunks, dev, align=1)
+    out, ooff = B.out_slots([B.snappy_max_compressed_length(len(c)) for c in chunks], dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        olen, st = B.snappy_encode(inp, off, ln, out, ooff)
+    s.synchronize()
+    assert int((st != 0).sum()) == 0
+    L = _lib.load()
+    ms = (ctypes.c_float * 8)()
+    n, pick = ctypes.c_int32(0), ctypes.c_int32(-1)
+    assert L.nx_snappy_encode_placement(ms, 8, ctypes.byref(n), ctypes.byref(pick)) == 0
+    assert 1 <= n.value <= 6 and 0 <= pick.value < n.value
+    probe = [ms[k] for k in range(n.value)]
+    assert all(p > 0 for p in probe)
+    assert probe[pick.value] == min(probe)
