@@ -13,15 +13,19 @@
 #include <string.h>
 #include <vector>
 #define nx_snappy_encode_batch enc_a_batch
+#define nx_snappy_encode_placement enc_a_placement
 namespace va {
 #include ENC_A
 }
 #undef nx_snappy_encode_batch
+#undef nx_snappy_encode_placement
 #define nx_snappy_encode_batch enc_b_batch
+#define nx_snappy_encode_placement enc_b_placement
 namespace vb {
 #include ENC_B
 }
 #undef nx_snappy_encode_batch
+#undef nx_snappy_encode_placement
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 262144, R = argc > 2 ? atoi(argv[2]) : 4;
     const int L = 65536;
