@@ -243,6 +243,11 @@ class SnappyRoundTrip:
         self.first, self.n, self.sub = first, n, max(1, min(sub, n))
         self.cap = (B.snappy_max_compressed_length(CHUNK) + 15) // 16 * 16
         s = self.sub
+        # place the encoder's table workspace before the shard's buffers take the memory its
+        # placement choice draws candidates from (as a server would at start-up)
+        from netty_amd import _lib
+        rc = _lib.load().nx_snappy_encoder_reserve(s, torch.cuda.current_stream(dev).cuda_stream)
+        assert rc == 0, f"nx_snappy_encoder_reserve: {rc}"
         self.src = torch.empty(n * CHUNK, dtype=torch.uint8, device=dev)
         for lo in range(0, n, s):  # textgen in pieces keeps its temporaries small
             B.textgen(self.src[lo * CHUNK:], first + lo, min(s, n - lo), CHUNK)

@@ -51,6 +51,12 @@ int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const 
                                uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
                                int32_t* status, uint32_t n, void* stream);
 
+/* Places and zeroes the encoder's hash-table workspace on `stream` for batches of up to max_chunks
+ * chunks now (a server calls it at start-up, before allocating its own buffers, so the placement
+ * choice has memory to draw candidates from).  Optional: nx_snappy_encode_batch
+ * allocates on demand.  No reference counterpart (Snappy.java:187-211 allocates per call). */
+int32_t nx_snappy_encoder_reserve(uint32_t max_chunks, void* stream);
+
 /* Diagnostics (no reference counterpart): the probe times in ms of the candidate workspace placements
  * the encoder's last large hash-table workspace was chosen from, and the index kept
  * (DESIGN.md §3).  *n = 0 before any such workspace exists. */

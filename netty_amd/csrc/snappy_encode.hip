@@ -670,6 +670,44 @@ constexpr uint32_t kMaxStamp = 63;  // 6-bit stamps 1..63
 constexpr uint32_t kSpreadMaxChunks = 16384;  // above this the dense form is faster
 }  // namespace
 
+namespace {
+// table slots a batch of n chunks (n > CUs) uses: one per wave (spread form) or per lane (dense form)
+size_t ws_slots(uint32_t n, int cus) {
+    const bool spread = n <= kSpreadMaxChunks;
+    const size_t want = (size_t)cus * kEncWavesPerCU * (spread ? 1 : 64);
+    return n < want ? (spread ? n : ((n + kEncBlock - 1) / kEncBlock) * kEncBlock) : want;
+}
+// (re)allocate W for `slots` tables; the caller holds g_ws_mu
+hipError_t ensure_ws(Workspace& W, size_t slots, hipStream_t st) {
+    if (W.ws != nullptr && W.threads >= slots) return hipSuccess;
+    if (W.ws) {
+        const hipError_t e = hipFree(W.ws);  // hipFree synchronises with pending work
+        if (e != hipSuccess) return e;
+    }
+    W.ws = nullptr;
+    // large (dense-form) workspaces: the fastest of several placements (nx_common.hpp alloc_placed_workspace)
+    const hipError_t e = nx::alloc_placed_workspace<uint64_t>(slots, 14, st, &W.ws, &g_place);
+    if (e != hipSuccess) return e;
+    W.threads = slots;
+    W.stamp = 0;
+    return hipSuccess;
+}
+}  // namespace
+
+// Place and zero the encoder's table workspace on `stream` for batches of up to max_chunks chunks
+// now, so a server sets it up at start-up, before its own buffers take the memory the placement
+// choice draws candidates from.  Optional: nx_snappy_encode_batch allocates on demand.
+extern "C" int32_t nx_snappy_encoder_reserve(uint32_t max_chunks, void* stream) {
+    int dev = 0, cus = 256;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (max_chunks <= (uint32_t)cus) return NX_OK;  // the LDS form needs no workspace
+    const hipStream_t st = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    NX_HIP_CHECK(ensure_ws(g_ws[{dev, st}], ws_slots(max_chunks, cus), st));
+    return NX_OK;
+}
+
 extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                           const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream) {
     if (n == 0) return NX_OK;
@@ -694,19 +732,11 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
         return NX_OK;
     }
     const bool spread = n <= kSpreadMaxChunks;
-    const size_t want = (size_t)cus * kEncWavesPerCU * (spread ? 1 : 64);  // table slots: waves or lanes
-    const size_t slots = n < want ? (spread ? n : ((n + kEncBlock - 1) / kEncBlock) * kEncBlock) : want;
+    const size_t slots = ws_slots(n, cus);
     const size_t per = 16384u * sizeof(uint64_t);
     std::lock_guard<std::mutex> lk(g_ws_mu);
     Workspace& W = g_ws[{dev, st}];
-    if (W.ws == nullptr || W.threads < slots) {
-        if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
-        W.ws = nullptr;
-        // dense form: the fastest of several placements (nx_common.hpp alloc_placed_workspace)
-        NX_HIP_CHECK(nx::alloc_placed_workspace<uint64_t>(slots, 14, st, &W.ws, &g_place));
-        W.threads = slots;
-        W.stamp = 0;
-    }
+    NX_HIP_CHECK(ensure_ws(W, slots, st));
     // Each launch gives a table slot at most kMaxStamp - 1 chunks (one stamp each).
     const size_t per_launch = slots * (kMaxStamp - 1);
     for (size_t base = 0; base < n; base += per_launch) {
