@@ -148,8 +148,11 @@ int32_t nx_adler32_batch(const uint8_t* in, const uint64_t* off, const uint32_t*
                          uint32_t* out, uint32_t n, void* stream);
 
 /* Replaces ChunkEncoder.appendEncodedChunk(...) as LZFEncoder.appendEncoded calls it per 65535-byte
- * chunk (LzfEncoder.java:218-221; compress-lzf 1.0.3 ChunkEncoder.tryCompress, fresh table): writes
- * a complete "ZV" block (compressed if it saves bytes, else non-compressed).  in_len[i] <= 65535.
+ * chunk (LzfEncoder.java:218-221; compress-lzf 1.0.3 ChunkEncoder.tryCompress): writes a complete
+ * "ZV" block (compressed if it saves bytes, else non-compressed).  in_len[i] <= 65535.  Each chunk
+ * gets a fresh table, which writes exactly what LzfEncoder's long-lived table (kept across chunks and
+ * messages, LzfEncoder.java:57,161-163) writes: no stale entry can pass tryCompress's 3-byte check
+ * (oracle/netty_oracle.c, above lzf_try_compress).
  * PARITY UNPINNED vs com.ning:compress-lzf (third-party, not in the reference). */
 int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                             uint8_t* out, const uint64_t* out_off, uint32_t* out_len,

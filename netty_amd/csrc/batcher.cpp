@@ -114,14 +114,22 @@ __global__ void __launch_bounds__(256) k_gather_host(const GatherOp* __restrict_
 }
 
 // one wave per encoder job: [stream identifier] then [type][len+4: u24 LE][masked crc LE][payload] per slice
+// res_len[j]: the job's framed bytes, or (negative) the Snappy.encode status of its first failing slice
 __global__ void __launch_bounds__(256) k_enc_finish(const uint8_t* __restrict__ din, const uint8_t* __restrict__ slots,
                                                     const EncSlice* __restrict__ sl, const uint32_t* __restrict__ clen,
-                                                    const uint32_t* __restrict__ crc, const EncJob* __restrict__ jobs, uint32_t njobs,
-                                                    uint8_t* __restrict__ out, uint64_t* __restrict__ res_len) {
+                                                    const int32_t* __restrict__ est, const uint32_t* __restrict__ crc,
+                                                    const EncJob* __restrict__ jobs, uint32_t njobs, uint8_t* __restrict__ out,
+                                                    int64_t* __restrict__ res_len) {
     const int lane = threadIdx.x & 63;
     const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (j >= njobs) return;
     const EncJob J = jobs[j];
+    for (uint32_t s = J.s0; s < J.s0 + J.ns; ++s) {
+        if (sl[s].comp && est[s] != NX_OK) {
+            if (lane == 0) res_len[j] = est[s];
+            return;
+        }
+    }
     uint8_t* o = out + J.out_off;
     uint64_t pos = 0;
     if (J.stream_start) {  // ff 06 00 00 "sNaPpY" (SnappyFrameEncoder.java:52-54)
@@ -141,7 +149,7 @@ __global__ void __launch_bounds__(256) k_enc_finish(const uint8_t* __restrict__ 
         wave_copy(o + pos + 8, S.comp ? slots + S.slot_off : din + S.in_off, L, lane);
         pos += 8 + L;
     }
-    if (lane == 0) res_len[j] = pos;
+    if (lane == 0) res_len[j] = (int64_t)pos;
 }
 
 // one wave per decoder job: the decoded messages back to back, stopping at the first failing chunk
@@ -370,7 +378,7 @@ Batch* collecting(nx_batcher* b) {
 }
 
 // Launch everything `bt` collected (batcher lock held).
-int32_t launch(nx_batcher* b, Batch* bt) {
+int32_t launch_inner(nx_batcher* b, Batch* bt) {
     const hipStream_t s = b->s[b->flushes % kStreams];
     const uint32_t nes = (uint32_t)bt->esl.size(), nej = (uint32_t)bt->ejob.size(), nda = (uint32_t)bt->dact.size();
     const uint32_t ndj = (uint32_t)bt->djob.size(), ndc = (uint32_t)bt->dc_off.size(), ndu = (uint32_t)bt->du_off.size();
@@ -456,8 +464,8 @@ int32_t launch(nx_batcher* b, Batch* bt) {
                                    (uint32_t*)(D + o_eclen), (int32_t*)(D + o_est), nes, s);
         if (r != NX_OK) return r;
         hipLaunchKernelGGL(nx::bt::k_enc_finish, dim3((nej + 3) / 4), dim3(256), 0, s, din, slots, (const EncSlice*)(A + o_esl),
-                           (const uint32_t*)(D + o_eclen), (const uint32_t*)(D + o_ecrc), (const EncJob*)(A + o_ejob), nej, bt->out.d,
-                           (uint64_t*)(bt->out.d + bt->res_enc));
+                           (const uint32_t*)(D + o_eclen), (const int32_t*)(D + o_est), (const uint32_t*)(D + o_ecrc),
+                           (const EncJob*)(A + o_ejob), nej, bt->out.d, (int64_t*)(bt->out.d + bt->res_enc));
         if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
         b->launches += 3;
         b->chunks += nes;
@@ -491,15 +499,44 @@ int32_t launch(nx_batcher* b, Batch* bt) {
     return NX_OK;
 }
 
+// A launch that failed part-way: wait for whatever of it reached the stream, then complete every job
+// of the batch with the error (each decoder it touched turns corrupted, as after the reference's
+// exception), so poll() reports them done and result() returns the error.  The batch is not in the
+// flush order (it never got a sequence number) and is reused once its jobs are released.
+int32_t fail_batch(nx_batcher* b, Batch* bt, int32_t code) {
+    (void)hipStreamSynchronize(b->s[b->flushes % kStreams]);
+    for (Job* j : bt->jobs) {
+        j->applied = true;
+        j->status = code;
+        j->err = "GPU batch launch failed";
+        j->msgs.clear();
+        if (j->kind == 1 && j->dec) j->dec->corrupted = true;
+    }
+    bt->inflight = false;
+    bt->done = true;
+    return code;
+}
+
+int32_t launch(nx_batcher* b, Batch* bt) {
+    const int32_t r = launch_inner(b, bt);
+    return r == NX_OK ? NX_OK : fail_batch(b, bt, r);
+}
+
 // The batch is complete: turn the result records into each job's messages, in submission order.
 void apply(Batch* bt) {
-    const uint64_t* res_len = reinterpret_cast<const uint64_t*>(bt->out.h + bt->res_enc);
+    const int64_t* res_len = reinterpret_cast<const int64_t*>(bt->out.h + bt->res_enc);
     const DecRes* dres = reinterpret_cast<const DecRes*>(bt->out.h + bt->res_dec);
     char buf[160];
     for (Job* j : bt->jobs) {
         if (j->kind == 0) {
             const EncJob& E = bt->ejob[j->index];
-            j->msgs.push_back({bt->out.h + E.out_off, (size_t)res_len[j->index]});
+            const int64_t r = res_len[j->index];
+            if (r < 0) {  // a slice the encoder failed: the job fails (no framed bytes)
+                j->status = (int32_t)r;
+                j->err = nx_status_string((int32_t)r);
+            } else {
+                j->msgs.push_back({bt->out.h + E.out_off, (size_t)r});
+            }
             j->applied = true;
             continue;
         }
@@ -640,8 +677,7 @@ extern "C" int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx
         return NX_ERR_HIP;
     }
     if (n) {  // SnappyFrameEncoder.encode (:79-117): !in.isReadable() writes nothing
-        E.stream_start = e->started ? 0u : 1u;
-        e->started = true;
+        E.stream_start = e->started ? 0u : 1u;  // e->started is set below, once the submit cannot fail
         uint64_t base = 0;
         const uint8_t* dsrc = in_registered ? registered_device_ptr(in, n) : nullptr;
         if (in_registered && !dsrc) {
@@ -690,6 +726,7 @@ extern "C" int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx
         } else {
             add(0, (uint32_t)n, false);
         }
+        e->started = true;
     }
     E.ns = (uint32_t)bt->esl.size() - E.s0;
     j->index = (uint32_t)bt->ejob.size();
@@ -697,8 +734,8 @@ extern "C" int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx
     bt->jobs.push_back(j);
     bt->live += 1;
     b->tickets[j->ticket] = {bt, j};
-    const int32_t r = maybe_autoflush(b, bt);
-    return r == NX_OK ? (int64_t)j->ticket : (int64_t)r;
+    (void)maybe_autoflush(b, bt);  // a failed launch completes the job with the error (result())
+    return (int64_t)j->ticket;
 }
 
 namespace {
@@ -712,7 +749,7 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
     j->kind = 1;
     j->dec = d;
     size_t p = 0;
-    if (d->corrupted) {  // (:86-89)
+    if (d->corrupted || d->parse_failed) {  // (:86-89): an earlier input failed
         p = n;
     } else {
         // the chunk-header walk runs now, so the decoder's started/skip state advances in call order
@@ -728,7 +765,9 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
         }
         d->started = started;
         d->skip = skip;
-        if (j->has_parse_err) d->corrupted = true;  // later submits skip their input (:227-230)
+        // later submits skip their input (:227-230); the decoder turns corrupted when this job is
+        // applied, after the jobs submitted before it have delivered their messages
+        if (j->has_parse_err) d->parse_failed = true;
     }
     *consumed = p;
     // on a failure below the batch's arrays go back to their sizes at entry (other jobs stay valid)
@@ -802,8 +841,8 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
     bt->jobs.push_back(j);
     bt->live += 1;
     b->tickets[j->ticket] = {bt, j};
-    const int32_t r = maybe_autoflush(b, bt);
-    return r == NX_OK ? (int64_t)j->ticket : (int64_t)r;
+    (void)maybe_autoflush(b, bt);  // a failed launch completes the job with the error (result())
+    return (int64_t)j->ticket;
 }
 }  // namespace
 
@@ -844,9 +883,9 @@ extern "C" int32_t nx_batcher_wait(nx_batcher* b, int64_t ticket) {
         bt = it->second.first;
         if (bt == b->cur) {  // not flushed yet: flush now
             b->cur = nullptr;
-            const int32_t r = launch(b, bt);
-            if (r != NX_OK) return r;
+            (void)launch(b, bt);  // a failed launch completes the batch's jobs with the error
         }
+        if (bt->done) return NX_OK;
     }
     if (hipEventSynchronize(bt->ev) != hipSuccess) return NX_ERR_HIP;
     std::lock_guard<std::mutex> lk(b->mu);

@@ -78,6 +78,7 @@ struct nx_snappy_frame_decoder {
     bool validate;
     bool started = false;
     bool corrupted = false;
+    bool parse_failed = false;  // batcher: a submitted input failed its header walk (applied later, in order)
     uint64_t skip = 0;  // numBytesToSkip
     nx::h::MsgList ml;
 };

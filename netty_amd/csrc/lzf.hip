@@ -25,9 +25,11 @@ __device__ __forceinline__ int32_t first2(const uint8_t* in, int32_t p) {  // Ch
 }
 
 // Returns body length.  htab entries: (stamp << 16) | (position + 1); a stamp mismatch is the Java
-// zero (position 0).  Whether the chunk starts the Java array or continues a message does not change
-// the bytes: a never-written slot or an earlier chunk's entry can never pass the 3-byte check
-// (oracle/netty_oracle.c orc_lzf_compress_body).
+// zero (position 0).  A fresh table per chunk is exact for Netty's long-lived per-handler encoder
+// (LzfEncoder.java:57,161-163,219), whose table keeps earlier chunks' and messages' entries: the first
+// occurrence of every trigram in a chunk is written before any probe reads its slot, so a stale entry
+// (or a never-written slot) can never pass the 3-byte check (oracle/netty_oracle.c, above
+// lzf_try_compress; tests/test_oracle_kat.py::test_lzf_encoder_state_across_messages).
 // The body goes to output positions 7.. (after the LZFChunk header, written last).
 template <class O>
 __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& out, uint32_t* __restrict__ htab, uint32_t stamp) {

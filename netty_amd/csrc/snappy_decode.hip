@@ -40,6 +40,7 @@
 // read once (4 B per tag) + output written once (+ far-copy re-reads, mostly served from MALL).
 #include <stddef.h>
 #include <stdlib.h>
+#include <string.h>
 #include <algorithm>
 #include <map>
 #include <mutex>
@@ -211,43 +212,55 @@ struct FrameIO {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) o[i] = (uint8_t)((i < 4 ? d.x : d.y) >> (8 * (i & 3)));
             }
-            if (do_crc) acc = shift_byte_tab(sSH, acc) ^ raw8(sT, d.x, d.y);
+            // output bytes 0..3 enter the CRC XORed with 0xFF: the ~0 initial state folded into the data
+            if (do_crc) acc = shift_byte_tab(sSH, acc) ^ raw8(sT, (flushed == 0u && lane == 0) ? ~d.x : d.x, d.y);
             flushed += (uint32_t)kFB;
         }
     }
-    // store what is left in the ring and return the CRC32C of output bytes [0, O)
+    // Store what is left in the ring and return the CRC32C of output bytes [0, O).  The ~0 initial
+    // state is folded into the data (output bytes 0..3 enter the CRC XORed with 0xFF), so the CRC is
+    // ~raw(M) with raw the state-0 CRC, and no x^(8n) product is needed: raw(M) = shift(raw(flushed
+    // blocks), tail) ^ raw(tail), the flushed blocks folded from the 64 lane accumulators (XOR_l acc_l *
+    // x^(8*8*(63-l))), the tail's whole 8-byte slots right-aligned in lanes 64-k..63 (leading zero
+    // slots add nothing to a state-0 CRC) and folded the same way, its last partial slot byte by byte.
+    // A frame shorter than 8 bytes is CRCed byte by byte from ~0.
     __device__ uint32_t finish(uint32_t O, const uint32_t* __restrict__ gNS) {
         const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);
         flush_to(O);
         wave_sync();
-        uint32_t crc = 0;
-        const uint32_t rem = O - flushed;
+        const uint32_t rem = O - flushed;  // < kFB
+        const uint32_t k = rem >> 3;       // whole 8-byte tail slots
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t b0 = 8u * lane;
-        const uint32_t end = b0 + 8u < rem ? b0 + 8u : rem;
-        uint32_t c = 0;
-        for (uint32_t i = b0; i < end; ++i) {
-            const uint8_t by = ring8[(flushed + i) & (kRing - 1)];
-            dst[flushed + i] = by;
-            c = (c >> 8) ^ sT[(c ^ by) & 0xFFu];
+        {
+            const uint32_t b0 = 8u * lane, b1 = b0 + 8u < rem ? b0 + 8u : rem;
+            for (uint32_t i = b0; i < b1; ++i) dst[flushed + i] = ring8[(flushed + i) & (kRing - 1)];
         }
+        uint32_t crc = 0;
         if (do_crc) {
-            // full blocks: total = XOR_l acc_l * x^(8*8*(63-l)) — 6-level tree with the nibble tables
-            uint32_t fa = acc;
+            auto fold = [&](uint32_t v) {
 #pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                const uint32_t other = __shfl_xor(fa, 1 << j);
-                const bool is_lo = ((lane >> j) & 1) == 0;
-                fa = shift_nib_tab(gNS + j * 128, is_lo ? fa : other) ^ (is_lo ? other : fa);
+                for (int j = 0; j < 6; ++j) {
+                    const uint32_t other = __shfl_xor(v, 1 << j);
+                    const bool is_lo = ((lane >> j) & 1) == 0;
+                    v = shift_nib_tab(gNS + j * 128, is_lo ? v : other) ^ (is_lo ? other : v);
+                }
+                return v;
+            };
+            uint32_t R = fold(acc);  // raw CRC of the flushed blocks
+            uint32_t c2 = 0;
+            if ((uint32_t)lane >= 64u - k) {  // tail slot j = lane - (64 - k), right-aligned
+                const uint32_t pos = flushed + 8u * ((uint32_t)lane - (64u - k));
+                const uint2 d = *reinterpret_cast<const uint2*>(&ring8[pos & (kRing - 1)]);
+                c2 = raw8(sT, pos == 0u ? ~d.x : d.x, d.y);
             }
-            // tail bytes: per-lane raw CRC shifted by the bytes after its slot
-            const uint32_t after = end > b0 ? rem - end : 0u;
-            c = end > b0 ? gf_multmodp(gf_x8n(after), c) : 0u;
+            c2 = fold(c2);
 #pragma unroll
-            for (int j = 0; j < 6; ++j) c ^= __shfl_xor(c, 1 << j);
-            // raw(M) = fold(full) * x^(8*rem) ^ raw(tail); crc = ~(~0 * x^(8|M|) ^ raw(M))
-            const uint32_t raw = gf_multmodp(gf_x8n(rem), fa) ^ c;
-            crc = ~(gf_multmodp(gf_x8n(O), 0xFFFFFFFFu) ^ raw);
+            for (int j = 0; j < 6; ++j)  // R * x^(8 * 8k)
+                if ((k >> j) & 1u) R = shift_nib_tab(gNS + j * 128, R);
+            R ^= c2;
+            if (O < 8u) R = 0xFFFFFFFFu;  // short frame: the plain CRC from ~0 (no fold)
+            for (uint32_t i = flushed + 8u * k; i < O; ++i) R = (R >> 8) ^ sT[(R ^ ring8[i & (kRing - 1)]) & 0xFFu];
+            crc = ~R;
         }
         return crc;
     }
@@ -913,6 +926,7 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
     }
 }
 
+
 // =====================================================================================
 // LZ4 blocks through the same record expander
 // =====================================================================================
@@ -1150,6 +1164,17 @@ static hipError_t dec_workspace(int dev, hipStream_t st, uint32_t sb, DecWorkspa
     return hipSuccess;
 }
 
+// one launch of the record expander over m frames
+static hipError_t launch_expand(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
+                                const uint32_t* rec, const uint32_t* nrec, uint32_t* out_len, int32_t* status, const uint32_t* expect,
+                                uint32_t* crc_out, uint32_t m, int cus, size_t lds, unsigned blocks_per_cu, hipStream_t st) {
+    using namespace nx::dec;
+    const uint64_t want = (uint64_t)cus * blocks_per_cu, need = (m + kWaves - 1) / kWaves;
+    hipLaunchKernelGGL(k_expand, dim3((unsigned)(need < want ? need : want)), dim3(kWaves * 64), lds, st, in, in_off, in_len, out,
+                       out_off, rec, nrec, out_len, status, expect, crc_out, m, nx::crc_tables_dev());
+    return hipGetLastError();
+}
+
 static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
                             const uint32_t* out_cap, uint32_t* out_len, uint32_t* consumed, int32_t* status,
                             const uint32_t* expected_masked_crc, uint32_t* crc_out, uint32_t n, void* stream, bool fused_only) {
@@ -1187,11 +1212,9 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
                            out_cap ? out_cap + base : nullptr, W.rec, W.nrec, out_len + base, consumed ? consumed + base : nullptr,
                            status + base, m);
         NX_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(k_expand, dim3(wave_grid(m)), dim3(kWaves * 64), lds, st, in, in_off + base, in_len + base, out,
-                           out_off + base, W.rec, W.nrec, out_len + base, status + base,
-                           expected_masked_crc ? expected_masked_crc + base : nullptr, crc_out ? crc_out + base : nullptr, m,
-                           nx::crc_tables_dev());
-        NX_HIP_CHECK(hipGetLastError());
+        NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W.rec, W.nrec, out_len + base, status + base,
+                                   expected_masked_crc ? expected_masked_crc + base : nullptr, crc_out ? crc_out + base : nullptr, m,
+                                   cus, lds, blocks_per_cu, st));
         // frames k_parse could not slot (more than kRecCap records, or input >= 32 MiB)
         hipLaunchKernelGGL(k_decode_fused, dim3(wave_grid(m)), dim3(kWaves * 64), lds, st, in, in_off + base, in_len + base, out,
                            out_off + base, out_cap ? out_cap + base : nullptr, out_len + base, consumed ? consumed + base : nullptr,
@@ -1247,10 +1270,10 @@ extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off
         hipLaunchKernelGGL(k_parse_lz4, dim3((m + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, st, in, in_off + base,
                            in_len + base, out_len + base, W->rec, W->nrec, W->olen, status + base, m);
         NX_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(k_expand, dim3((unsigned)(need < want ? need : want)), dim3(kWaves * 64), lds, st, in, in_off + base,
-                           in_len + base, out, out_off + base, W->rec, W->nrec, W->olen, status + base, nullptr, nullptr, m,
-                           nx::crc_tables_dev());
-        NX_HIP_CHECK(hipGetLastError());
+        (void)need;
+        (void)want;
+        NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W->rec, W->nrec, W->olen, status + base, nullptr,
+                                   nullptr, m, cus, lds, blocks_per_cu, st));
         hipLaunchKernelGGL(k_lz4_serial, dim3((m + 255) / 256), dim3(256), 0, st, in, in_off + base, in_len + base, out_len + base,
                            out, out_off + base, status + base, m);
         NX_HIP_CHECK(hipGetLastError());

@@ -749,20 +749,31 @@ int32_t orc_lzf_decode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out, in
  * Netty's LzfEncoder takes ChunkEncoderFactory.optimalNonAllocatingInstance (LzfEncoder.java:161-163)
  * → UnsafeChunkEncoderLE on x86, whose output equals the safe ChunkEncoder's restated here:
  *   - int[16384] table (calcHashLen(max(65535, ...)) for the default totalLength = MAX_CHUNK_LEN),
- *     zero-initialised, entries = absolute input positions; hash(h) = ((h * 57321) >> 9) & 16383 on
- *     Java int (wrapping multiply, arithmetic shift) of `seen` = the big-endian int of the bytes
- *     [p-1, p, p+1, p+2] (at the first probe and after a match its top byte is the sign of in[p]);
+ *     created with the encoder and kept for its lifetime: entries are absolute positions in the
+ *     message array, zero-initialised (a Java zero is position 0); hash(h) = ((h * 57321) >> 9) &
+ *     16383 on Java int (wrapping multiply, arithmetic shift) of `seen` = the big-endian int of the
+ *     bytes [p-1, p, p+1, p+2] (at the first probe and after a match its top byte is the sign of in[p]);
  *   - a candidate ref is taken iff firstPos <= ref < p, p - ref <= MAX_OFF (8192) and the 3 bytes at
- *     ref equal those at p.  The hash depends only on the low 23 bits of `seen` (bytes p+1, p+2 and
- *     7 bits of p), and the first probe (p = firstPos) writes its slot, so a never-written slot (a
- *     Java zero, array position 0) or an entry of an earlier chunk (< firstPos) can never pass the
- *     3-byte check: every chunk encodes as with a fresh table, whatever its position in the message;
+ *     ref equal those at p (firstPos = the chunk's start: entries of earlier chunks are refused, but
+ *     entries a PREVIOUS message left at positions >= firstPos are candidates — LzfEncoder keeps one
+ *     ChunkEncoder per handler, LzfEncoder.java:57,161-163,219);
  *   - matches extend to min(MAX_REF = 264, inEnd - p + 2) bytes (inEnd = end - TAIL_LENGTH 4), are
  *     emitted as (len-2, off-1), and insert positions matchEnd-2 and matchEnd-1;
  *   - literal runs of at most 32 bytes, the header byte reserved ahead (handleTail for the last 4).
- * PARITY UNPINNED: no reference bytes exist offline (LzfEncoderTest.java:31-38 only round-trips).
- * A long-lived Java encoder keeps its table across messages, so a later message may take an older
- * (still valid) match than a fresh table would; this restates a fresh encoder's output. */
+ * A direct ByteBuf message is copied to position 0 of a byte[] (LzfEncoder.java:174-181), so every
+ * message's positions start at 0.
+ * The table's history never changes the bytes: within a chunk, the first occurrence of every trigram
+ * is written to the table before any later probe can read that slot (every probe position writes its
+ * slot; a position skipped inside a match repeats an earlier occurrence of its trigram, and the two
+ * positions inserted after a match cover the trigrams that straddle its end), so an entry left by an
+ * earlier chunk or message (or a Java zero) is only ever read for a trigram that has not occurred in
+ * the chunk yet, and then fails the 3-byte check — exactly as a fresh table's zero does.  A long-lived
+ * encoder therefore writes what a fresh one writes (tests/test_oracle_kat.py:: 
+ * test_lzf_encoder_state_across_messages checks it over repeated / shifted messages), and the batch
+ * kernels' per-chunk fresh tables are exact for Netty's per-handler encoder too.  (By the same argument
+ * a hash array recycled from an encoder closed earlier on the thread, BufferRecycler.allocEncodingHash,
+ * changes nothing either.)
+ * PARITY UNPINNED: no reference bytes exist offline (LzfEncoderTest.java:31-38 only round-trips). */
 #define LZF_HSIZE 16384
 #define LZF_MAX_OFF 8192
 #define LZF_MAX_REF 264
@@ -770,20 +781,20 @@ int32_t orc_lzf_decode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out, in
 
 static inline int32_t lzf_jhash(int32_t h) { return ((int32_t)((uint32_t)h * 57321u) >> 9) & (LZF_HSIZE - 1); }
 
-int32_t orc_lzf_compress_body(const uint8_t* in, int32_t n, uint8_t* out) {
-    int32_t* ht = (int32_t*)calloc(LZF_HSIZE, sizeof(int32_t)); /* position + 1; 0 = the Java zero */
-    int32_t ip = 0, op = 1, lit = 0; /* ++outPos: literal-length byte reserved */
-    const int32_t inEnd = n - 4;
-    int32_t seen = (int32_t)((uint32_t)(int32_t)(int8_t)in[0] << 8) + in[1]; /* first(in, inPos) */
+/* tryCompress(in, pos0, pos0 + n, out, 0) over the message array `in` with the encoder's table:
+ * returns the body length written to out. */
+static int32_t lzf_try_compress(const uint8_t* in, int32_t pos0, int32_t n, uint8_t* out, int32_t* ht) {
+    int32_t ip = pos0, op = 1, lit = 0; /* ++outPos: literal-length byte reserved */
+    const int32_t firstPos = pos0, inEnd = pos0 + n - 4;
+    int32_t seen = (int32_t)((uint32_t)(int32_t)(int8_t)in[ip] << 8) + in[ip + 1]; /* first(in, inPos) */
     while (ip < inEnd) {
         const uint8_t p2 = in[ip + 2];
         seen = (int32_t)(((uint32_t)seen << 8) + p2);
         const int32_t h = lzf_jhash(seen);
-        const int32_t e = ht[h];
-        const int32_t ref = e ? e - 1 : 0;
-        ht[h] = ip + 1;
+        const int32_t ref = ht[h];
+        ht[h] = ip;
         int32_t off = ip - ref;
-        if (ref < 0 || ref >= ip || off > LZF_MAX_OFF || in[ref + 2] != p2 || in[ref + 1] != (uint8_t)(seen >> 8) ||
+        if (ref >= ip || ref < firstPos || off > LZF_MAX_OFF || in[ref + 2] != p2 || in[ref + 1] != (uint8_t)(seen >> 8) ||
             in[ref] != (uint8_t)(seen >> 16)) {
             out[op++] = in[ip++];
             if (++lit == LZF_MAX_LIT) {
@@ -813,17 +824,18 @@ int32_t orc_lzf_compress_body(const uint8_t* in, int32_t n, uint8_t* out) {
         }
         out[op++] = (uint8_t)off;
         op++;
-        ip += len; /* matchEnd - 2 (<= n - 4) */
+        ip += len; /* matchEnd - 2 (<= end - 4) */
         seen = (int32_t)((uint32_t)(int32_t)(int8_t)in[ip] << 8) + in[ip + 1];
         seen = (int32_t)(((uint32_t)seen << 8) + in[ip + 2]);
-        ht[lzf_jhash(seen)] = ip + 1;
+        ht[lzf_jhash(seen)] = ip;
         ++ip;
         seen = (int32_t)(((uint32_t)seen << 8) + in[ip + 2]);
-        ht[lzf_jhash(seen)] = ip + 1;
+        ht[lzf_jhash(seen)] = ip;
         ++ip;
     }
     /* handleTail */
-    while (ip < n) {
+    const int32_t end = pos0 + n;
+    while (ip < end) {
         out[op++] = in[ip++];
         if (++lit == LZF_MAX_LIT) {
             out[op - lit - 1] = (uint8_t)(lit - 1);
@@ -836,15 +848,22 @@ int32_t orc_lzf_compress_body(const uint8_t* in, int32_t n, uint8_t* out) {
     } else {
         op--;
     }
-    free(ht);
     return op;
 }
 
-/* One LZFChunk (ChunkEncoder.appendEncodedChunk): compressed "ZV 01 clen ulen body" if it beats
- * "ZV 00 len data", else the latter. */
-size_t orc_lzf_encode_chunk(const uint8_t* in, int32_t n, uint8_t* out) {
+/* A fresh encoder's first chunk (the batch API's semantics: each chunk through a new LzfEncoder). */
+int32_t orc_lzf_compress_body(const uint8_t* in, int32_t n, uint8_t* out) {
+    int32_t* ht = (int32_t*)calloc(LZF_HSIZE, sizeof(int32_t));
+    const int32_t r = lzf_try_compress(in, 0, n, out, ht);
+    free(ht);
+    return r;
+}
+
+/* ChunkEncoder.appendEncodedChunk over in[pos0, pos0 + n): compressed "ZV 01 clen ulen body" if it
+ * beats "ZV 00 len data", else the latter (the table keeps tryCompress's writes either way). */
+static size_t lzf_append_chunk(const uint8_t* in, int32_t pos0, int32_t n, uint8_t* out, int32_t* ht) {
     if (n >= 16) {
-        int32_t clen = orc_lzf_compress_body(in, n, out + 7);
+        int32_t clen = lzf_try_compress(in, pos0, n, out + 7, ht);
         if (clen + 7 < n + 5) {
             out[0] = 'Z'; out[1] = 'V'; out[2] = 1;
             out[3] = (uint8_t)(clen >> 8); out[4] = (uint8_t)clen;
@@ -854,21 +873,40 @@ size_t orc_lzf_encode_chunk(const uint8_t* in, int32_t n, uint8_t* out) {
     }
     out[0] = 'Z'; out[1] = 'V'; out[2] = 0;
     out[3] = (uint8_t)(n >> 8); out[4] = (uint8_t)n;
-    memcpy(out + 5, in, (size_t)n);
+    memcpy(out + 5, in + pos0, (size_t)n);
     return (size_t)n + 5;
+}
+
+size_t orc_lzf_encode_chunk(const uint8_t* in, int32_t n, uint8_t* out) {
+    int32_t* ht = (int32_t*)calloc(LZF_HSIZE, sizeof(int32_t));
+    const size_t r = lzf_append_chunk(in, 0, n, out, ht);
+    free(ht);
+    return r;
 }
 
 size_t orc_lzf_frame_max_encoded(size_t n) { return (n / 65535 + 1) * 7 + n + n / 32 + 64 + 66; }
 
-/* LzfEncoder.encode (LzfEncoder.java:169-216): split into 65535-byte chunks
- * (LZFEncoder.appendEncoded), or non-compressed chunks below compressThreshold (:197-203). */
-size_t orc_lzf_frame_encode(const uint8_t* in, size_t n, int32_t compress_threshold, uint8_t* out) {
+/* One LzfEncoder instance (its ChunkEncoder's table persists across encode() calls). */
+struct orc_lzf_encoder {
+    int32_t ht[LZF_HSIZE];
+    int32_t threshold;
+};
+orc_lzf_encoder* orc_lzf_encoder_new(int32_t compress_threshold) {
+    orc_lzf_encoder* e = (orc_lzf_encoder*)calloc(1, sizeof(orc_lzf_encoder));
+    if (e) e->threshold = compress_threshold;
+    return e;
+}
+void orc_lzf_encoder_free(orc_lzf_encoder* e) { free(e); }
+
+/* LzfEncoder.encode (LzfEncoder.java:169-216): 65535-byte chunks (LZFEncoder.appendEncoded), or
+ * non-compressed chunks below compressThreshold (:197-203, lzfEncodeNonCompress :223-239: an empty
+ * message still yields one empty chunk). */
+size_t orc_lzf_encoder_encode(orc_lzf_encoder* e, const uint8_t* in, size_t n, uint8_t* out) {
     size_t op = 0, ip = 0;
-    /* an empty message still yields one empty non-compressed chunk (lzfEncodeNonCompress :223-239) */
     do {
         int32_t len = (int32_t)((n - ip) < 65535 ? (n - ip) : 65535);
-        if ((int64_t)n >= compress_threshold) {
-            op += orc_lzf_encode_chunk(in + ip, len, out + op);
+        if ((int64_t)n >= e->threshold) {
+            op += lzf_append_chunk(in, (int32_t)ip, len, out + op, e->ht);
         } else {
             out[op] = 'Z'; out[op + 1] = 'V'; out[op + 2] = 0;
             out[op + 3] = (uint8_t)(len >> 8); out[op + 4] = (uint8_t)len;
@@ -878,6 +916,14 @@ size_t orc_lzf_frame_encode(const uint8_t* in, size_t n, int32_t compress_thresh
         ip += (size_t)len;
     } while (ip < n);
     return op;
+}
+
+/* A message through a new LzfEncoder. */
+size_t orc_lzf_frame_encode(const uint8_t* in, size_t n, int32_t compress_threshold, uint8_t* out) {
+    orc_lzf_encoder* e = orc_lzf_encoder_new(compress_threshold);
+    const size_t r = orc_lzf_encoder_encode(e, in, n, out);
+    orc_lzf_encoder_free(e);
+    return r;
 }
 
 /* =====================================================================================

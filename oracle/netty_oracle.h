@@ -72,6 +72,11 @@ int32_t orc_lzf_decode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out, in
  * returns body length (may exceed in_len). */
 int32_t orc_lzf_compress_body(const uint8_t* in, int32_t in_len, uint8_t* out);
 size_t orc_lzf_frame_encode(const uint8_t* in, size_t n, int32_t compress_threshold, uint8_t* out);
+/* One LzfEncoder instance: its ChunkEncoder table persists across encode() calls. */
+typedef struct orc_lzf_encoder orc_lzf_encoder;
+orc_lzf_encoder* orc_lzf_encoder_new(int32_t compress_threshold);
+void orc_lzf_encoder_free(orc_lzf_encoder* e);
+size_t orc_lzf_encoder_encode(orc_lzf_encoder* e, const uint8_t* in, size_t n, uint8_t* out);
 size_t orc_lzf_frame_max_encoded(size_t n);
 
 /* LZ4 block format (lz4-java 1.8.0, a third-party dependency absent from the reference: pom.xml

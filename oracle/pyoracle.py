@@ -74,6 +74,12 @@ def lib():
         L.orc_lzf_compress_body.argtypes = [C.c_char_p, C.c_int32, C.c_void_p]
         L.orc_lzf_frame_encode.restype = C.c_size_t
         L.orc_lzf_frame_encode.argtypes = [C.c_char_p, C.c_size_t, C.c_int32, C.c_void_p]
+        L.orc_lzf_encoder_new.restype = C.c_void_p
+        L.orc_lzf_encoder_new.argtypes = [C.c_int32]
+        L.orc_lzf_encoder_free.restype = None
+        L.orc_lzf_encoder_free.argtypes = [C.c_void_p]
+        L.orc_lzf_encoder_encode.restype = C.c_size_t
+        L.orc_lzf_encoder_encode.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.c_void_p]
         L.orc_lzf_frame_max_encoded.restype = C.c_size_t
         L.orc_lzf_frame_max_encoded.argtypes = [C.c_size_t]
         L.orc_java_random_bytes.restype = None
@@ -302,6 +308,25 @@ def lz4_frame_scan(buf: bytes, state: int = 0, cap: int | None = None):
     if res < 0:
         corrupted = True  # :257-259
     return ents, p, int(finished) | (int(corrupted) << 1), res
+
+
+class LzfEncoderState:
+    """One LzfEncoder: its ChunkEncoder hash table persists across encode() calls
+    (LzfEncoder.java:57,161-163,219)."""
+
+    def __init__(self, compress_threshold: int = 16):
+        self._e = lib().orc_lzf_encoder_new(compress_threshold)
+
+    def encode(self, data: bytes) -> bytes:
+        L = lib()
+        out = _buf(L.orc_lzf_frame_max_encoded(len(data)))
+        n = L.orc_lzf_encoder_encode(self._e, bytes(data), len(data), out)
+        return bytes(out[:n])
+
+    def __del__(self):
+        if getattr(self, "_e", None):
+            lib().orc_lzf_encoder_free(self._e)
+            self._e = None
 
 
 def lzf_frame_encode(data: bytes, compress_threshold: int = 16) -> bytes:

@@ -201,3 +201,46 @@ def test_batcher_autoflush_ordered_across_streams(nx, oracle):
         b.result(t_bad)
     assert b"".join(b"".join(b.result(t)) for t in t_ok) == data
     assert b.result(t_after) == []
+
+
+def test_batcher_header_error_after_good_job_same_decoder(nx, oracle):
+    """A header-level error found at submit (a reserved unskippable chunk, SnappyFrameDecoder.java:151-157)
+    fails its own job with the reference message when the batch is applied; the job submitted before it
+    on the same decoder still delivers its messages, and the job after it delivers nothing (the decoder
+    is corrupted, :86-89).  Same sequence as the synchronous decoder."""
+    msg = oracle.textgen_chunk(11, 5000)
+    good, _ = oracle.snappy_frame_encode(msg)
+    bad = bytes([0x02, 0x01, 0x00, 0x00, 0x00])
+    later, _ = oracle.snappy_frame_encode(b"later bytes of the stream", started=True)
+    b = nx.Batcher()
+    d = nx.SnappyFrameDecoder(True)
+    t1 = b.submit_decode(d, good)
+    t2 = b.submit_decode(d, bad)
+    t3 = b.submit_decode(d, later)
+    b.flush()
+    b.wait(t3)
+    assert b"".join(b.result(t1)) == msg
+    with pytest.raises(nx.DecompressionException, match="Found reserved unskippable chunk type: 0x2"):
+        b.result(t2)
+    assert b.result(t3) == []
+    # the synchronous decoder over the same reads
+    s = nx.SnappyFrameDecoder(True)
+    assert b"".join(s.channel_read(good)) == msg
+    with pytest.raises(nx.DecompressionException, match="Found reserved unskippable chunk type: 0x2"):
+        s.channel_read(bad)
+    assert s.channel_read(later) == []
+
+
+def test_batcher_rejected_encoder_submit_keeps_stream_identifier(nx, oracle):
+    """A submit that fails its checks (input outside any registered range) leaves the encoder as it was:
+    the next submit still writes the stream identifier (SnappyFrameEncoder.java:84-87)."""
+    data = oracle.textgen_chunk(5, 1000)
+    b = nx.Batcher()
+    e = nx.SnappyFrameEncoder()
+    buf = C.create_string_buffer(data, len(data))  # never registered
+    with pytest.raises(RuntimeError):
+        b.submit_encode(e, data, registered_ptr=C.addressof(buf))
+    t = b.submit_encode(e, data)
+    b.flush()
+    b.wait(t)
+    assert b.result(t) == [oracle.snappy_frame_encode(data)[0]]

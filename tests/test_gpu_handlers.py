@@ -243,6 +243,22 @@ def test_fastlz_decoder_errors(nx, oracle):
     assert b"".join(nx.FastLzFrameDecoder(False).channel_read(bytes(bad))) == oracle.textgen_chunk(1, 5000)
 
 
+def test_lzf_encoder_messages_through_one_handle(nx, oracle):
+    """Several repetitive messages through ONE LzfEncoder (its ChunkEncoder table persists across
+    encode() calls, LzfEncoder.java:57,161-163,219): each message's bytes equal the stateful oracle's
+    (orc_lzf_encoder_*), and the decoder restores every message."""
+    import random
+    r = random.Random(23)
+    words = [bytes(r.randrange(97, 101) for _ in range(r.randrange(2, 6))) for _ in range(10)]
+    base = b" ".join(r.choice(words) for _ in range(3000))
+    msgs = [base, base, base[5:], base[:999] + b"!" + base[999:], oracle.textgen_chunk(4, 140000), base * 30]
+    enc, st, dec = nx.LzfEncoder(16), oracle.LzfEncoderState(16), nx.LzfDecoder()
+    for i, m in enumerate(msgs):
+        comp = enc.encode(m)
+        assert comp == st.encode(m), i
+        assert b"".join(dec.channel_read(comp)) == m, i
+
+
 @pytest.mark.parametrize("threshold", [16, 1000])
 def test_lzf_identity(nx, oracle, kat, threshold):
     for name, data in _corpus(oracle, kat).items():

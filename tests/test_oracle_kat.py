@@ -182,77 +182,99 @@ def test_lzf_roundtrip(oracle):
     assert oracle.lzf_decode_chunk(bytes([0x20, 0x05]), 3)[0] == -30
 
 
-def _lzf_try_compress_py(inp: bytes) -> bytes:
-    """Second, independent restatement of compress-lzf 1.0.3 ChunkEncoder.tryCompress (Java int
-    arithmetic spelled out) to cross-check the C oracle's transcription (parity unpinned vs the
-    library itself, which is not available offline)."""
-    def i32(x):
+class _LzfEncoderPy:
+    """Second, independent restatement of compress-lzf 1.0.3 (ChunkEncoder.tryCompress /
+    appendEncodedChunk, LZFEncoder.appendEncoded) as one LzfEncoder drives it (Java int arithmetic
+    spelled out; the table persists across messages, LzfEncoder.java:57,161-163,219) to cross-check the
+    C oracle's transcription (parity unpinned vs the library itself, which is not available offline)."""
+
+    def __init__(self, threshold=16):
+        self.ht = [0] * 16384
+        self.threshold = threshold
+
+    @staticmethod
+    def _i32(x):
         x &= 0xFFFFFFFF
         return x - (1 << 32) if x >= 1 << 31 else x
 
-    def jhash(h):  # ((h * 57321) >> 9) & _hashModulo, _hashModulo = 16383
-        return (i32(h * 57321) >> 9) & 16383
+    def _try_compress(self, inp, pos0, n):
+        i32, ht = self._i32, self.ht
 
-    def first(p):  # (in[p] << 8) + (in[p + 1] & 0xFF), in[] signed
-        b = inp[p] - 256 if inp[p] >= 128 else inp[p]
-        return i32((b << 8) + inp[p + 1])
+        def jhash(h):  # ((h * 57321) >> 9) & _hashModulo, _hashModulo = 16383
+            return (i32(h * 57321) >> 9) & 16383
 
-    n = len(inp)
-    ht = [0] * 16384
-    out = bytearray(2 * n + 64)
-    ip, op, lit, in_end = 0, 1, 0, n - 4
-    seen = first(0)
-    while ip < in_end:
-        p2 = inp[ip + 2]
-        seen = i32((seen << 8) + p2)
-        h = jhash(seen)
-        ref = ht[h]
-        ht[h] = ip
-        off = ip - ref
-        if (ref >= ip or off > 8192 or inp[ref + 2] != p2 or inp[ref + 1] != (seen >> 8) & 255
-                or inp[ref] != (seen >> 16) & 255):
+        def first(p):  # (in[p] << 8) + (in[p + 1] & 0xFF), in[] signed
+            b = inp[p] - 256 if inp[p] >= 128 else inp[p]
+            return i32((b << 8) + inp[p + 1])
+
+        out = bytearray(2 * n + 64)
+        ip, op, lit, in_end = pos0, 1, 0, pos0 + n - 4
+        seen = first(ip)
+        while ip < in_end:
+            p2 = inp[ip + 2]
+            seen = i32((seen << 8) + p2)
+            h = jhash(seen)
+            ref = ht[h]
+            ht[h] = ip
+            off = ip - ref
+            if (ref >= ip or ref < pos0 or off > 8192 or inp[ref + 2] != p2 or inp[ref + 1] != (seen >> 8) & 255
+                    or inp[ref] != (seen >> 16) & 255):
+                out[op] = inp[ip]
+                op, ip, lit = op + 1, ip + 1, lit + 1
+                if lit == 32:
+                    out[op - 33] = 31
+                    lit, op = 0, op + 1
+                continue
+            max_len = min(264, in_end - ip + 2)
+            if lit == 0:
+                op -= 1
+            else:
+                out[op - lit - 1] = lit - 1
+                lit = 0
+            ln = 3
+            while ln < max_len and inp[ref + ln] == inp[ip + ln]:
+                ln += 1
+            ln, off = ln - 2, off - 1
+            if ln < 7:
+                out[op] = ((off >> 8) + (ln << 5)) & 255
+                op += 1
+            else:
+                out[op], out[op + 1] = ((off >> 8) + (7 << 5)) & 255, ln - 7
+                op += 2
+            out[op] = off & 255
+            op += 2
+            ip += ln
+            seen = i32((first(ip) << 8) + inp[ip + 2])
+            ht[jhash(seen)] = ip
+            ip += 1
+            seen = i32((seen << 8) + inp[ip + 2])
+            ht[jhash(seen)] = ip
+            ip += 1
+        while ip < pos0 + n:  # handleTail
             out[op] = inp[ip]
             op, ip, lit = op + 1, ip + 1, lit + 1
             if lit == 32:
-                out[op - 33] = 31
+                out[op - lit - 1] = lit - 1
                 lit, op = 0, op + 1
-            continue
-        max_len = min(264, in_end - ip + 2)
-        if lit == 0:
+        if lit:
+            out[op - lit - 1] = lit - 1
+        else:
             op -= 1
-        else:
-            out[op - lit - 1] = lit - 1
-            lit = 0
-        ln = 3
-        while ln < max_len and inp[ref + ln] == inp[ip + ln]:
-            ln += 1
-        ln, off = ln - 2, off - 1
-        if ln < 7:
-            out[op] = ((off >> 8) + (ln << 5)) & 255
-            op += 1
-        else:
-            out[op], out[op + 1] = ((off >> 8) + (7 << 5)) & 255, ln - 7
-            op += 2
-        out[op] = off & 255
-        op += 2
-        ip += ln
-        seen = i32((first(ip) << 8) + inp[ip + 2])
-        ht[jhash(seen)] = ip
-        ip += 1
-        seen = i32((seen << 8) + inp[ip + 2])
-        ht[jhash(seen)] = ip
-        ip += 1
-    while ip < n:  # handleTail
-        out[op] = inp[ip]
-        op, ip, lit = op + 1, ip + 1, lit + 1
-        if lit == 32:
-            out[op - lit - 1] = lit - 1
-            lit, op = 0, op + 1
-    if lit:
-        out[op - lit - 1] = lit - 1
-    else:
-        op -= 1
-    return bytes(out[:op])
+        return bytes(out[:op])
+
+    def encode(self, inp):
+        res, p = bytearray(), 0
+        while True:
+            n = min(65535, len(inp) - p)
+            chunk = inp[p:p + n]
+            body = self._try_compress(inp, p, n) if len(inp) >= self.threshold and n >= 16 else None
+            if body is not None and len(body) + 7 < n + 5:
+                res += b"ZV\x01" + len(body).to_bytes(2, "big") + n.to_bytes(2, "big") + body
+            else:
+                res += b"ZV\x00" + n.to_bytes(2, "big") + chunk
+            p += n
+            if p >= len(inp):
+                return bytes(res)
 
 
 def test_lzf_encoder_restatements_agree(oracle):
@@ -262,7 +284,32 @@ def test_lzf_encoder_restatements_agree(oracle):
              bytes(r.randrange(256) for _ in range(999)), b"ab" * 700 + bytes(range(256)) * 3,
              bytes(r.randrange(3) | 0x80 for _ in range(2000)), bytes(16), b"abc" + b"xyz" * 30 + b"abcd" * 40]
     for c in cases:
-        assert oracle.lzf_compress_body(c) == _lzf_try_compress_py(c)
+        assert oracle.lzf_compress_body(c) == _LzfEncoderPy()._try_compress(c, 0, len(c))
+
+
+def test_lzf_encoder_state_across_messages(oracle):
+    """One LzfEncoder over many messages: its ChunkEncoder table persists (LzfEncoder.java:57,161-163,
+    219), restated by the C oracle (orc_lzf_encoder_*) and the independent Python class above.  Both
+    agree message by message, and every message equals a FRESH encoder's bytes: an entry left by an
+    earlier message (or chunk) can never pass tryCompress's 3-byte check before this chunk has written
+    that slot itself, because the first occurrence of every trigram in a chunk is written to the table
+    (a probe, or one of the two inserts after a match; a position skipped inside a match repeats an
+    earlier occurrence).  So the batch kernels' per-chunk fresh tables are exact for a long-lived
+    encoder too (netty_oracle.c, lzf.hip)."""
+    import random
+    r = random.Random(11)
+    msgs = []
+    for trial in range(30):
+        words = [bytes(r.randrange(97, 100) for _ in range(r.randrange(2, 6))) for _ in range(8)]
+        base = b" ".join(r.choice(words) for _ in range(r.randrange(20, 500)))
+        msgs += [base, base, base[7:], base[:100] + b"#" + base[100:]]
+    msgs += [oracle.textgen_chunk(9, 70000), oracle.textgen_chunk(9, 65535 + 40), oracle.textgen_chunk(9, 70000)[3:],
+             bytes(15), bytes(5000), b"ab" * 9000]
+    enc, py = oracle.LzfEncoderState(16), _LzfEncoderPy(16)
+    for i, m in enumerate(msgs):
+        got = enc.encode(m)
+        assert got == py.encode(m), i
+        assert got == oracle.lzf_frame_encode(m, 16), i
 
 
 def test_textgen_deterministic(oracle):
