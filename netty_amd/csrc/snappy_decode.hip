@@ -713,37 +713,39 @@ struct BurstWin {
     }
 };
 
-// Record writer: records gather 16 at a time in registers and leave as one 64-byte run (four
-// back-to-back 16-byte stores), so a lane's record slot is written in half-lines the L2 merges
-// instead of scattered 16-byte partial-line writes (k_parse 17.2-17.5 -> 15.7-15.8 ms per 262 144
-// frames, scripts/experiments/dec_bench.cpp).
+// Record writer: a lane's records gather 16 at a time in its LDS queue row and leave as one 64-byte
+// run (four back-to-back 16-byte stores), so the record slot is written in half-lines the L2 merges
+// instead of scattered partial-line writes.  The row is LDS, not registers: a register queue needs a
+// 16-way select per record (32 VALU: v_cmp + v_cndmask per entry), an LDS row one ds_write.
+constexpr int kQDw = 20;  // queue row stride in dwords (16 records; 16-byte aligned rows)
 struct RecWriter {
     uint4* slot;
-    uint32_t n;  // records emitted
-    uint32_t q[16];
+    uint32_t* q;  // this lane's LDS row
+    uint32_t n;   // records emitted
+    __device__ __forceinline__ void flush16(uint32_t base) {
+        const uint4* qq = reinterpret_cast<const uint4*>(q);
+        uint4* d = slot + (base >> 2);
+        d[0] = qq[0];
+        d[1] = qq[1];
+        d[2] = qq[2];
+        d[3] = qq[3];
+    }
     __device__ __forceinline__ bool put(uint32_t r) {
         if (n >= kRecCap) return false;
-        const uint32_t k = n & 15u;
-#pragma unroll
-        for (uint32_t j = 0; j < 16; ++j) q[j] = k == j ? r : q[j];
-        if (k == 15) {
-            uint4* d = slot + (n >> 4) * 4;
-            d[0] = make_uint4(q[0], q[1], q[2], q[3]);
-            d[1] = make_uint4(q[4], q[5], q[6], q[7]);
-            d[2] = make_uint4(q[8], q[9], q[10], q[11]);
-            d[3] = make_uint4(q[12], q[13], q[14], q[15]);
-        }
+        q[n & 15u] = r;
+        if ((n & 15u) == 15u) flush16(n - 15u);
         ++n;
         return true;
     }
     __device__ __forceinline__ void finish() {
         const uint32_t k = n & 15u;
         if (k) {
-            uint4* d = slot + (n >> 4) * 4;
-            d[0] = make_uint4(q[0], q[1], q[2], q[3]);
-            if (k > 4) d[1] = make_uint4(q[4], q[5], q[6], q[7]);
-            if (k > 8) d[2] = make_uint4(q[8], q[9], q[10], q[11]);
-            if (k > 12) d[3] = make_uint4(q[12], q[13], q[14], q[15]);
+            const uint4* qq = reinterpret_cast<const uint4*>(q);
+            uint4* d = slot + ((n - k) >> 2);
+            d[0] = qq[0];
+            if (k > 4) d[1] = qq[1];
+            if (k > 8) d[2] = qq[2];
+            if (k > 12) d[3] = qq[3];
         }
     }
 };
@@ -754,6 +756,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
                                                        uint32_t* __restrict__ out_len, uint32_t* __restrict__ consumed_a,
                                                        int32_t* __restrict__ status, uint32_t n) {
     __shared__ uint32_t wins[kParseBlock * kWinDw + 4];
+    __shared__ __attribute__((aligned(16))) uint32_t recq[kParseBlock * kQDw];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
     const uint32_t in_len = in_len_a[c];
@@ -765,7 +768,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
     }
     BurstWin win;
     win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
-    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), 0, {}};
+    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
     uint32_t ip = 0, op = 0;
     int32_t st = NX_OK;
     bool run = false;
@@ -948,6 +951,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lz4(const uint8_t* __rest
                                                            uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
                                                            uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t n) {
     __shared__ uint32_t wins[kParseBlock * kWinDw + 4];
+    __shared__ __attribute__((aligned(16))) uint32_t recq[kParseBlock * kQDw];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
     const uint32_t in_len = in_len_a[c];
@@ -960,7 +964,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lz4(const uint8_t* __rest
     }
     BurstWin win;
     win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
-    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), 0, {}};
+    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
     uint32_t ip = 0, op = 0;
     int32_t st = NX_OK;
     bool fit = true;
