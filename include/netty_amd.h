@@ -51,11 +51,27 @@ int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const 
                                uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
                                int32_t* status, uint32_t n, void* stream);
 
-/* Places and zeroes the encoder's hash-table workspace on `stream` for batches of up to max_chunks
- * chunks now (a server calls it at start-up, before allocating its own buffers, so the placement
- * choice has memory to draw candidates from).  Optional: nx_snappy_encode_batch
- * allocates on demand.  No reference counterpart (Snappy.java:187-211 allocates per call). */
+/* Device workspaces (no reference counterpart: Snappy.java:187-211 allocates its table per call).
+ * The encoders' hash tables and the decoder's record slots live in one workspace per device and
+ * kind, shared by every stream: a batch's launches wait on the device for the previous batch's (the
+ * host never blocks).  The standalone batch calls grow a workspace on demand (blocking, once per
+ * size); batchers and handles reserve their share when created (nx_batcher_new, nx_*_new), never
+ * grow it in submit / flush / encode / decode (a larger batch caps its grid to the reserved slots),
+ * and the last of them to be freed frees it.
+ *
+ * nx_snappy_encoder_reserve places and zeroes the Snappy table workspace for batches of up to
+ * max_chunks chunks now (a server calls it at start-up, before allocating its own buffers, so the
+ * placement choice has memory to draw candidates from); kept until trimmed.
+ * nx_workspaces_trim frees, on the current device, every workspace no batcher or handle holds.
+ * nx_workspace_info reports the bytes and owners of one kind (NX_WS_*). */
+#define NX_WS_SNAPPY_ENC 0
+#define NX_WS_LZ4_ENC 1
+#define NX_WS_FASTLZ_ENC 2
+#define NX_WS_LZF_ENC 3
+#define NX_WS_DEC_RECORDS 4
 int32_t nx_snappy_encoder_reserve(uint32_t max_chunks, void* stream);
+int32_t nx_workspaces_trim(void);
+int32_t nx_workspace_info(int32_t kind, uint64_t* bytes, int32_t* owners);
 
 /* Diagnostics (no reference counterpart): the probe times in ms of the candidate workspace placements
  * the encoder's last large hash-table workspace was chosen from, and the index kept

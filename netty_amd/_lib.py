@@ -105,6 +105,8 @@ _SIGS = {
                                          C.POINTER(sz), C.POINTER(C.c_char_p)]),
     "nx_snappy_encoder_reserve": (i32, [u32, vp]),
     "nx_snappy_encode_placement": (i32, [C.POINTER(C.c_float), i32, C.POINTER(i32), C.POINTER(i32)]),
+    "nx_workspaces_trim": (i32, []),
+    "nx_workspace_info": (i32, [i32, C.POINTER(C.c_uint64), C.POINTER(i32)]),
     "nx_lzf_decoder_new": (vp, []),
     "nx_lzf_decoder_free": (None, [vp]),
     "nx_lzf_decoder_decode": (i32, [vp, C.c_char_p, sz, C.POINTER(sz), C.POINTER(C.POINTER(NxMsg)),

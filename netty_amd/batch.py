@@ -24,6 +24,23 @@ def _chk(rc, what):
         raise RuntimeError(f"{what} failed: {rc} ({_lib.status_string(rc)})")
 
 
+# Shared device workspaces (include/netty_amd.h NX_WS_*; csrc/workspace.hpp)
+WS_SNAPPY_ENC, WS_LZ4_ENC, WS_FASTLZ_ENC, WS_LZF_ENC, WS_DEC_RECORDS = range(5)
+
+
+def workspace_info(kind: int) -> tuple[int, int]:
+    """(bytes, owners) of the current device's workspace of `kind`."""
+    import ctypes as C
+    b, o = C.c_uint64(0), C.c_int32(0)
+    _chk(_lib.load().nx_workspace_info(kind, C.byref(b), C.byref(o)), "nx_workspace_info")
+    return b.value, o.value
+
+
+def workspaces_trim():
+    """Free the current device's workspaces that no batcher or handle holds."""
+    _chk(_lib.load().nx_workspaces_trim(), "nx_workspaces_trim")
+
+
 def snappy_max_compressed_length(n: int) -> int:
     return _lib.load().nx_snappy_max_compressed_length(n)
 

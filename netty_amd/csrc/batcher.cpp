@@ -42,6 +42,7 @@
 #include "frame_parse.hpp"
 #include "handles.hpp"
 #include "nx_common.hpp"
+#include "workspace.hpp"
 
 namespace nx {
 namespace bt {
@@ -152,8 +153,19 @@ __global__ void __launch_bounds__(256) k_enc_finish(const uint8_t* __restrict__ 
     if (lane == 0) res_len[j] = (int64_t)pos;
 }
 
+// Bytes a Snappy block of clen bytes can decode to: at most 64 per 3 input bytes (a copy-2 tag; a
+// copy-1 gives 11 per 2, a copy-4 64 per 5, a literal its own length), and never more than the frame
+// decoder's 65536-byte buffer (SnappyFrameDecoder.java:203).  Sizes the decode slots and the job's
+// output reservation, so a flush of many small chunks does not take 64 KiB for each.
+__host__ __device__ inline uint32_t snappy_decoded_bound(uint32_t clen) {
+    const uint64_t b = 64ull * ((clen + 2ull) / 3ull);
+    return b < 65536u ? (uint32_t)b : 65536u;
+}
+inline uint64_t dec_slot_bytes(uint32_t clen) { return ((uint64_t)snappy_decoded_bound(clen) + 64u + 15u) & ~15ull; }
+
 // one wave per decoder job: the decoded messages back to back, stopping at the first failing chunk
 __global__ void __launch_bounds__(256) k_dec_finish(const uint8_t* __restrict__ din, const uint8_t* __restrict__ slots,
+                                                    const uint64_t* __restrict__ dslot,
                                                     const DecAct* __restrict__ acts, const DecJob* __restrict__ jobs, uint32_t njobs,
                                                     const uint32_t* __restrict__ dlen, const uint32_t* __restrict__ dcons,
                                                     const int32_t* __restrict__ dstat, const uint32_t* __restrict__ dcrc,
@@ -180,7 +192,7 @@ __global__ void __launch_bounds__(256) k_dec_finish(const uint8_t* __restrict__ 
             R.len = dlen[A.chunk];
             R.crc = dcrc[A.chunk];
             R.cons = dcons[A.chunk];
-            if (R.status == NX_OK) wave_copy(out + pos, slots + (uint64_t)A.chunk * 65536u, R.len, lane);
+            if (R.status == NX_OK) wave_copy(out + pos, slots + dslot[A.chunk], R.len, lane);
         }
         if (lane == 0) res[a] = R;
         if (R.status != NX_OK) break;
@@ -342,6 +354,8 @@ constexpr int kStreams = 4;
 struct nx_batcher {
     std::mutex mu;
     hipStream_t s[kStreams] = {};
+    int dev = 0;
+    bool held_enc = false, held_dec = false;  // shared workspaces reserved at creation (workspace.hpp)
     std::deque<Batch*> all;  // every batch object (collecting, in flight, or done)
     Batch* cur = nullptr;    // the collecting batch
     std::unordered_map<uint64_t, std::pair<Batch*, Job*>> tickets;
@@ -380,6 +394,7 @@ Batch* collecting(nx_batcher* b) {
 // Launch everything `bt` collected (batcher lock held).
 int32_t launch_inner(nx_batcher* b, Batch* bt) {
     const hipStream_t s = b->s[b->flushes % kStreams];
+    const nx::NoGrowScope no_grow;  // the workspaces reserved at nx_batcher_new: a flush never allocates them
     const uint32_t nes = (uint32_t)bt->esl.size(), nej = (uint32_t)bt->ejob.size(), nda = (uint32_t)bt->dact.size();
     const uint32_t ndj = (uint32_t)bt->djob.size(), ndc = (uint32_t)bt->dc_off.size(), ndu = (uint32_t)bt->du_off.size();
     struct Lay {
@@ -418,7 +433,11 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         eslot[i] = bt->esl[i].slot_off;
         elen[i] = bt->esl[i].len;
     }
-    for (uint32_t i = 0; i < ndc; ++i) dslot[i] = (uint64_t)i * 65536u;
+    uint64_t dslot_bytes = 0;
+    for (uint32_t i = 0; i < ndc; ++i) {
+        dslot[i] = dslot_bytes;
+        dslot_bytes += nx::bt::dec_slot_bytes(bt->dc_len[i]);
+    }
     auto cp = [&](uint64_t off, const void* src, size_t n) {
         if (n) memcpy(h + off, src, n);
     };
@@ -437,11 +456,11 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
     cp(o_dulen, bt->du_len.data(), 4ull * ndu);
     // result records in the mapped arena, after the job outputs
     if (!bt->reserve_out(8ull * nej + 8, &bt->res_enc) || !bt->reserve_out(sizeof(DecRes) * nda + 8, &bt->res_dec)) return NX_ERR_HIP;
-    if (!bt->din.ensure(d0 + bt->direct_used + 16) || !bt->slots.ensure(bt->eslots + (uint64_t)ndc * 65536u + Ld.at + 64)) return NX_ERR_HIP;
+    if (!bt->din.ensure(d0 + bt->direct_used + 16) || !bt->slots.ensure(bt->eslots + dslot_bytes + Ld.at + 64)) return NX_ERR_HIP;
     uint8_t* din = bt->din.as<uint8_t>();
     uint8_t* slots = bt->slots.as<uint8_t>();
     uint8_t* dslots = slots + bt->eslots;
-    uint8_t* D = dslots + (uint64_t)ndc * 65536u;
+    uint8_t* D = dslots + dslot_bytes;
     D = reinterpret_cast<uint8_t*>(((uintptr_t)D + 15) & ~(uintptr_t)15);
     if (hipMemcpyAsync(din, bt->staging.h, bt->st_used, hipMemcpyHostToDevice, s) != hipSuccess) return NX_ERR_HIP;
     if (!bt->direct.empty()) {  // registered inputs: one gather launch reading the mapped host pages
@@ -484,7 +503,8 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
             if (r != NX_OK) return r;
             b->launches += 1;
         }
-        hipLaunchKernelGGL(nx::bt::k_dec_finish, dim3((ndj + 3) / 4), dim3(256), 0, s, din, dslots, (const DecAct*)(A + o_dact),
+        hipLaunchKernelGGL(nx::bt::k_dec_finish, dim3((ndj + 3) / 4), dim3(256), 0, s, din, dslots, (const uint64_t*)(A + o_dslot),
+                           (const DecAct*)(A + o_dact),
                            (const DecJob*)(A + o_djob), ndj, (const uint32_t*)(D + o_dlen), (const uint32_t*)(D + o_dcons),
                            (const int32_t*)(D + o_dst), (const uint32_t*)(D + o_dcrc), (const uint32_t*)(D + o_ducrc), bt->out.d,
                            (DecRes*)(bt->out.d + bt->res_dec));
@@ -628,6 +648,15 @@ extern "C" nx_batcher* nx_batcher_new(void) {
             return nullptr;
         }
     }
+    // One Snappy table workspace and one record workspace for the whole batcher, whichever of its
+    // streams a flush lands on (a flush waits on the device for the previous flush's kernels).
+    b->held_enc = hipGetDevice(&b->dev) == hipSuccess &&
+                  nx::ws_hold(nx::WsKind::SnappyEnc, b->dev, nx::kBatcherHoldUnits, b->s[0]) == NX_OK;
+    b->held_dec = b->held_enc && nx::ws_hold(nx::WsKind::DecRecords, b->dev, nx::kBatcherHoldUnits, b->s[0]) == NX_OK;
+    if (!b->held_dec) {
+        nx_batcher_free(b);
+        return nullptr;
+    }
     return b;
 }
 
@@ -636,6 +665,8 @@ extern "C" void nx_batcher_free(nx_batcher* b) {
     for (int i = 0; i < kStreams; ++i) (void)hipStreamSynchronize(b->s[i]);
     for (Batch* x : b->all) delete x;
     for (int i = 0; i < kStreams; ++i) (void)hipStreamDestroy(b->s[i]);
+    if (b->held_enc) nx::ws_unhold(nx::WsKind::SnappyEnc, b->dev);
+    if (b->held_dec) nx::ws_unhold(nx::WsKind::DecRecords, b->dev);
     delete b;
 }
 
@@ -823,7 +854,7 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
             bt->dc_crc.push_back(a.crc);
             bt->dc_direct.push_back(dir);
             if (d->validate) bt->dc_validate = true;
-            out_need += 65536;
+            out_need += nx::bt::snappy_decoded_bound(a.dlen);
         } else {
             A.kind = 1;
             A.chunk = (uint32_t)bt->du_off.size();

@@ -419,19 +419,10 @@ __global__ void __launch_bounds__(256) k_adler32(const uint8_t* __restrict__ in,
 }  // namespace flz
 }  // namespace nx
 
-#include <map>
-#include <mutex>
-namespace {
-// Hash-table workspace, one per (device, stream): launches on one stream are ordered and may share
-// it; launches on different streams (or devices) may overlap and must not.
-struct FlzWorkspace {
-    uint32_t* ws = nullptr;
-    size_t slots = 0;
-    uint32_t stamp = 0;
-};
-std::mutex g_mu;
-std::map<std::pair<int, hipStream_t>, FlzWorkspace> g_flz_ws;
-}  // namespace
+#include "workspace.hpp"
+static_assert(nx::kWsSpec[(int)nx::WsKind::FastLzEnc].entry_bytes == sizeof(uint32_t) &&
+                  (int)nx::kWsSpec[(int)nx::WsKind::FastLzEnc].lg == nx::flz::HASH_LOG,
+              "FastLZ table geometry");
 
 extern "C" int32_t nx_fastlz_compress_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                             const uint64_t* out_off, uint32_t* out_len, const int32_t* level,
@@ -441,29 +432,24 @@ extern "C" int32_t nx_fastlz_compress_batch(const uint8_t* in, const uint64_t* i
     int dev = 0, cus = 256;
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const nx::LaneGrid g = nx::lane_grid(n, cus, 8);
     const hipStream_t st = (hipStream_t)stream;
     const size_t per = (size_t)nx::flz::HASH_SIZE * sizeof(uint32_t);
-    std::lock_guard<std::mutex> lk(g_mu);
-    FlzWorkspace& W = g_flz_ws[{dev, st}];
-    if (W.ws == nullptr || W.slots < g.slots) {
-        if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
-        W.ws = nullptr;
-        NX_HIP_CHECK(nx::alloc_placed_workspace<uint32_t>(g.slots, nx::flz::HASH_LOG, st, &W.ws));
-        W.slots = g.slots;
-        W.stamp = 0;
-    }
+    nx::WsLease lease(nx::WsKind::FastLzEnc, dev, st);
+    NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::FastLzEnc, n, cus)));
+    nx::SharedWs& W = lease.ws();
+    const nx::LaneGrid g = nx::ws_grid(nx::WsKind::FastLzEnc, n, cus, W.slots);
+    uint32_t* ws = static_cast<uint32_t*>(W.p);
     const uint32_t iters = (uint32_t)((n + g.slots - 1) / g.slots);
     if ((uint64_t)W.stamp + iters >= 65535u) {
-        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.slots * per, st));
+        NX_HIP_CHECK(hipMemsetAsync(ws, 0, W.slots * per, st));
         W.stamp = 0;
     }
     if (g.spread)
         hipLaunchKernelGGL(nx::flz::k_compress<true>, dim3(g.grid), dim3(g.block), 0, st, in, in_off, in_len, out, out_off, out_len, level,
-                           u16_limit, status, n, W.ws, W.stamp);
+                           u16_limit, status, n, ws, W.stamp);
     else
         hipLaunchKernelGGL(nx::flz::k_compress<false>, dim3(g.grid), dim3(g.block), 0, st, in, in_off, in_len, out, out_off, out_len,
-                           level, u16_limit, status, n, W.ws, W.stamp);
+                           level, u16_limit, status, n, ws, W.stamp);
     NX_HIP_CHECK(hipGetLastError());
     W.stamp += iters;
     return NX_OK;

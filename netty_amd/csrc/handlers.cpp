@@ -44,7 +44,7 @@ inline uint32_t be32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint3
 
 extern "C" nx_snappy_frame_encoder* nx_snappy_frame_encoder_new(int32_t jumbo) {
     auto* e = new nx_snappy_frame_encoder();
-    if (!e->g.ok) {
+    if (!e->g.hold(nx::WsKind::SnappyEnc)) {
         delete e;
         return nullptr;
     }
@@ -56,6 +56,7 @@ extern "C" size_t nx_snappy_frame_max_encoded_length(size_t n) { return 10 + (n 
 
 extern "C" int64_t nx_snappy_frame_encoder_encode(nx_snappy_frame_encoder* e, const uint8_t* in, size_t n, uint8_t* out,
                                                   size_t out_cap) {
+    const nx::NoGrowScope no_grow;
     if (!e) return NX_ERR_INVALID_ARG;
     if (n == 0) return 0;  // !in.isReadable()
     if (out_cap < nx_snappy_frame_max_encoded_length(n)) return NX_ERR_INVALID_ARG;
@@ -160,7 +161,7 @@ extern "C" int64_t nx_snappy_frame_encoder_encode(nx_snappy_frame_encoder* e, co
 
 extern "C" nx_snappy_frame_decoder* nx_snappy_frame_decoder_new(int32_t validate) {
     auto* d = new nx_snappy_frame_decoder();
-    if (!d->g.ok) {
+    if (!d->g.hold(nx::WsKind::DecRecords)) {
         delete d;
         return nullptr;
     }
@@ -175,6 +176,7 @@ using nx::fr::snappy_parse_one;
 
 extern "C" int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
                                                   const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {
+    const nx::NoGrowScope no_grow;
     if (!d || (!in && n)) return NX_ERR_INVALID_ARG;
     MsgList& ml = d->ml;
     ml.clear();
@@ -322,7 +324,7 @@ struct nx_fastlz_frame_encoder {
 extern "C" nx_fastlz_frame_encoder* nx_fastlz_frame_encoder_new(int32_t level, int32_t checksum) {
     if (level != 0 && level != 1 && level != 2) return nullptr;  // FastLzFrameEncoder.java:101-105
     auto* e = new nx_fastlz_frame_encoder();
-    if (!e->g.ok) {
+    if (!e->g.hold(nx::WsKind::FastLzEnc)) {
         delete e;
         return nullptr;
     }
@@ -335,6 +337,7 @@ extern "C" size_t nx_fastlz_frame_max_encoded_length(size_t n) { return (n / 655
 
 extern "C" int64_t nx_fastlz_frame_encoder_encode(nx_fastlz_frame_encoder* e, const uint8_t* buf, size_t r0, size_t n,
                                                   uint8_t* out, size_t out_cap) {
+    const nx::NoGrowScope no_grow;
     if (!e) return NX_ERR_INVALID_ARG;
     if (n == 0) return 0;
     if (out_cap < nx_fastlz_frame_max_encoded_length(n)) return NX_ERR_INVALID_ARG;
@@ -437,6 +440,7 @@ extern "C" void nx_fastlz_frame_decoder_free(nx_fastlz_frame_decoder* d) { delet
 
 extern "C" int32_t nx_fastlz_frame_decoder_decode(nx_fastlz_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
                                                   const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {
+    const nx::NoGrowScope no_grow;
     if (!d || (!in && n)) return NX_ERR_INVALID_ARG;
     MsgList& ml = d->ml;
     ml.clear();
@@ -656,7 +660,7 @@ struct nx_lzf_encoder {
 extern "C" nx_lzf_encoder* nx_lzf_encoder_new(int32_t compress_threshold) {
     if (compress_threshold < 16) return nullptr;  // LzfEncoder.java:155-160
     auto* e = new nx_lzf_encoder();
-    if (!e->g.ok) {
+    if (!e->g.hold(nx::WsKind::LzfEnc)) {
         delete e;
         return nullptr;
     }
@@ -667,6 +671,7 @@ extern "C" void nx_lzf_encoder_free(nx_lzf_encoder* e) { delete e; }
 extern "C" size_t nx_lzf_frame_max_encoded_length(size_t n) { return (n / 65535 + 1) * 7 + n + n / 32 + 64; }
 
 extern "C" int64_t nx_lzf_encoder_encode(nx_lzf_encoder* e, const uint8_t* in, size_t n, uint8_t* out, size_t out_cap) {
+    const nx::NoGrowScope no_grow;
     if (!e) return NX_ERR_INVALID_ARG;
     if (out_cap < nx_lzf_frame_max_encoded_length(n)) return NX_ERR_INVALID_ARG;
     if ((int64_t)n < e->threshold) {  // encodeNonCompress (LzfEncoder.java:197-203,223-246)
@@ -735,6 +740,7 @@ extern "C" void nx_lzf_decoder_free(nx_lzf_decoder* d) { delete d; }
 
 extern "C" int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, size_t n, size_t* consumed, const nx_msg** msgs,
                                          size_t* n_msgs, const char** err_msg) {
+    const nx::NoGrowScope no_grow;
     if (!d || (!in && n)) return NX_ERR_INVALID_ARG;
     MsgList& ml = d->ml;
     ml.clear();
@@ -888,7 +894,7 @@ extern "C" nx_lz4_frame_encoder* nx_lz4_frame_encoder_new(int32_t block_size) {
     // compressionLevel(blockSize) :158-166; the device block encoder takes blocks below 32 MiB
     if (block_size < 64 || block_size > (1 << 25)) return nullptr;
     auto* e = new nx_lz4_frame_encoder();
-    if (!e->g.ok) {
+    if (!e->g.hold(nx::WsKind::Lz4Enc)) {
         delete e;
         return nullptr;
     }
@@ -951,6 +957,7 @@ int64_t lz4_flush_blocks(nx_lz4_frame_encoder* e, const uint8_t* src, size_t n, 
 
 extern "C" int64_t nx_lz4_frame_encoder_encode(nx_lz4_frame_encoder* e, const uint8_t* in, size_t n, uint8_t* out,
                                                size_t out_cap) {
+    const nx::NoGrowScope no_grow;
     if (!e || (!in && n)) return NX_ERR_INVALID_ARG;
     if (e->finished) {  // :233-239 — after close() the bytes pass through
         if (out_cap < n) return NX_ERR_INVALID_ARG;
@@ -980,6 +987,7 @@ extern "C" int64_t nx_lz4_frame_encoder_encode(nx_lz4_frame_encoder* e, const ui
 }
 
 extern "C" int64_t nx_lz4_frame_encoder_flush(nx_lz4_frame_encoder* e, uint8_t* out, size_t out_cap) {
+    const nx::NoGrowScope no_grow;
     if (!e) return NX_ERR_INVALID_ARG;  // flush() :291-300
     const int64_t w = lz4_flush_blocks(e, e->buf.data(), e->buf.size(), out, out_cap);
     if (w >= 0) e->buf.clear();
@@ -987,6 +995,7 @@ extern "C" int64_t nx_lz4_frame_encoder_flush(nx_lz4_frame_encoder* e, uint8_t* 
 }
 
 extern "C" int64_t nx_lz4_frame_encoder_close(nx_lz4_frame_encoder* e, uint8_t* out, size_t out_cap) {
+    const nx::NoGrowScope no_grow;
     if (!e) return NX_ERR_INVALID_ARG;
     if (e->finished) return 0;  // finishEncode :318-321
     const int64_t w = nx_lz4_frame_encoder_flush(e, out, out_cap);
@@ -1010,7 +1019,7 @@ struct nx_lz4_frame_decoder {
 
 extern "C" nx_lz4_frame_decoder* nx_lz4_frame_decoder_new(int32_t validate_checksums) {
     auto* d = new nx_lz4_frame_decoder();
-    if (!d->g.ok) {
+    if (!d->g.hold(nx::WsKind::DecRecords)) {
         delete d;
         return nullptr;
     }
@@ -1021,6 +1030,7 @@ extern "C" void nx_lz4_frame_decoder_free(nx_lz4_frame_decoder* d) { delete d; }
 
 extern "C" int32_t nx_lz4_frame_decoder_decode(nx_lz4_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
                                                const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {
+    const nx::NoGrowScope no_grow;
     if (!d || (!in && n) || !consumed || !msgs || !n_msgs) return NX_ERR_INVALID_ARG;
     MsgList& ml = d->ml;
     ml.clear();

@@ -7,6 +7,7 @@
 #include <vector>
 #include "../../include/netty_amd.h"
 #include "nx_common.hpp"
+#include "workspace.hpp"
 
 namespace nx {
 namespace h {
@@ -35,15 +36,28 @@ struct DevBuf {
 
 struct Gpu {
     hipStream_t s = nullptr;
+    int dev = 0;
     bool ok = false;
+    uint32_t held = 0;  // bit per WsKind whose shared workspace this handle holds (workspace.hpp)
     DevBuf din, dout, a0, a1, a2, a3, a4, a5, a6;
     Gpu() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return;
+        if (hipGetDevice(&dev) != hipSuccess) return;
         if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
         ok = nx::crc_tables_init() == NX_OK;
     }
+    // Reserve the device workspace of kind k for this handle's launches, at construction (its
+    // encode/decode calls then never allocate: they run in a NoGrowScope).
+    bool hold(WsKind k) {
+        if (!ok || ws_hold(k, dev, kHandleHoldUnits, s) != NX_OK) return false;
+        held |= 1u << (int)k;
+        return true;
+    }
     ~Gpu() {
+        if (s) (void)hipStreamSynchronize(s);
+        for (int k = 0; k < (int)WsKind::Count; ++k)
+            if (held & (1u << k)) ws_unhold((WsKind)k, dev);
         if (s) (void)hipStreamDestroy(s);
     }
     bool h2d(void* d, const void* h, size_t n) { return n == 0 || hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s) == hipSuccess; }

@@ -17,9 +17,8 @@
 // a large block zeroes its 4096 slots before and after itself, so none of its raw indices can pass
 // a later small block's stamp check.
 #include <algorithm>
-#include <map>
-#include <mutex>
 #include "nx_common.hpp"
+#include "workspace.hpp"
 
 namespace nx {
 namespace lz4 {
@@ -192,14 +191,10 @@ __global__ void __launch_bounds__(256) k_lz4_encode(const uint8_t* __restrict__ 
 }  // namespace nx
 
 namespace {
-struct Lz4Workspace {
-    uint32_t* ws = nullptr;
-    size_t threads = 0;
-    uint32_t stamp = 0;
-};
-std::mutex g_lz4_mu;
-std::map<std::pair<int, hipStream_t>, Lz4Workspace> g_lz4_ws;
 constexpr uint32_t kMaxStamp = 0xFFFFu;
+static_assert(nx::kWsSpec[(int)nx::WsKind::Lz4Enc].entry_bytes == sizeof(uint32_t) &&
+                  (1u << nx::kWsSpec[(int)nx::WsKind::Lz4Enc].lg) == nx::lz4::kTableSlots,
+              "LZ4 table geometry");
 }  // namespace
 
 extern "C" size_t nx_lz4_max_compressed_length(size_t n) { return n + n / 255 + 16; }
@@ -214,29 +209,23 @@ extern "C" int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const hipStream_t st = (hipStream_t)stream;
-    const nx::LaneGrid g = nx::lane_grid(n, cus, 16);  // 16 waves per CU, as the Snappy encoder
-    const size_t threads = g.slots;
     const size_t per = nx::lz4::kTableSlots * sizeof(uint32_t);
-    std::lock_guard<std::mutex> lk(g_lz4_mu);
-    Lz4Workspace& W = g_lz4_ws[{dev, st}];
-    if (W.ws == nullptr || W.threads < threads) {
-        if (W.ws) NX_HIP_CHECK(hipFree(W.ws));
-        W.ws = nullptr;
-        NX_HIP_CHECK(nx::alloc_placed_workspace<uint32_t>(threads, 13, st, &W.ws));  // 8192 slots per table
-        W.threads = threads;
-        W.stamp = 0;
-    }
-    const uint32_t iters = (uint32_t)((n + threads - 1) / threads);
+    nx::WsLease lease(nx::WsKind::Lz4Enc, dev, st);
+    NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::Lz4Enc, n, cus)));
+    nx::SharedWs& W = lease.ws();
+    const nx::LaneGrid g = nx::ws_grid(nx::WsKind::Lz4Enc, n, cus, W.slots);  // 16 waves per CU, as the Snappy encoder
+    uint32_t* ws = static_cast<uint32_t*>(W.p);
+    const uint32_t iters = (uint32_t)((n + g.slots - 1) / g.slots);
     if (W.stamp + iters >= kMaxStamp) {
-        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.threads * per, st));
+        NX_HIP_CHECK(hipMemsetAsync(ws, 0, W.slots * per, st));
         W.stamp = 0;
     }
     if (g.spread)
         hipLaunchKernelGGL(nx::lz4::k_lz4_encode<true>, dim3(g.grid), dim3(g.block), 0, st, in, in_off, in_len, out, out_off, out_len,
-                           status, n, W.ws, W.stamp);
+                           status, n, ws, W.stamp);
     else
         hipLaunchKernelGGL(nx::lz4::k_lz4_encode<false>, dim3(g.grid), dim3(g.block), 0, st, in, in_off, in_len, out, out_off, out_len,
-                           status, n, W.ws, W.stamp);
+                           status, n, ws, W.stamp);
     NX_HIP_CHECK(hipGetLastError());
     W.stamp += iters;
     return NX_OK;

@@ -208,19 +208,10 @@ __global__ void __launch_bounds__(256) k_decode(const uint8_t* __restrict__ in, 
 }  // namespace lzf
 }  // namespace nx
 
-#include <map>
-#include <mutex>
-namespace {
-// Hash-table workspace, one per (device, stream): launches on one stream are ordered and may share
-// it; launches on different streams (or devices) may overlap and must not.
-struct LzfWorkspace {
-    uint32_t* ws = nullptr;
-    size_t slots = 0;
-    uint32_t stamp = 0;
-};
-std::mutex g_mu;
-std::map<std::pair<int, hipStream_t>, LzfWorkspace> g_lzf_ws;
-}  // namespace
+#include "workspace.hpp"
+static_assert(nx::kWsSpec[(int)nx::WsKind::LzfEnc].entry_bytes == sizeof(uint32_t) &&
+                  (1 << nx::kWsSpec[(int)nx::WsKind::LzfEnc].lg) == nx::lzf::HSIZE,
+              "LZF table geometry");
 
 extern "C" int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                        const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream) {
@@ -229,29 +220,24 @@ extern "C" int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off
     int dev = 0, cus = 256;
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const nx::LaneGrid g = nx::lane_grid(n, cus, 8);
     const hipStream_t st = (hipStream_t)stream;
     const size_t per = (size_t)nx::lzf::HSIZE * sizeof(uint32_t);
-    std::lock_guard<std::mutex> lk(g_mu);
-    LzfWorkspace& W = g_lzf_ws[{dev, st}];
-    if (W.ws == nullptr || W.slots < g.slots) {
-        if (W.ws) NX_HIP_CHECK(hipFree(W.ws));  // hipFree synchronises with pending work
-        W.ws = nullptr;
-        NX_HIP_CHECK(nx::alloc_placed_workspace<uint32_t>(g.slots, 14, st, &W.ws));  // HSIZE = 2^14
-        W.slots = g.slots;
-        W.stamp = 0;
-    }
+    nx::WsLease lease(nx::WsKind::LzfEnc, dev, st);
+    NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::LzfEnc, n, cus)));
+    nx::SharedWs& W = lease.ws();
+    const nx::LaneGrid g = nx::ws_grid(nx::WsKind::LzfEnc, n, cus, W.slots);
+    uint32_t* ws = static_cast<uint32_t*>(W.p);
     const uint32_t iters = (uint32_t)((n + g.slots - 1) / g.slots);
     if ((uint64_t)W.stamp + iters >= 65535u) {
-        NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.slots * per, st));
+        NX_HIP_CHECK(hipMemsetAsync(ws, 0, W.slots * per, st));
         W.stamp = 0;
     }
     if (g.spread)
         hipLaunchKernelGGL(nx::lzf::k_encode<true>, dim3(g.grid), dim3(g.block), 0, st, in, in_off, in_len, out, out_off, out_len, status,
-                           n, W.ws, W.stamp);
+                           n, ws, W.stamp);
     else
         hipLaunchKernelGGL(nx::lzf::k_encode<false>, dim3(g.grid), dim3(g.block), 0, st, in, in_off, in_len, out, out_off, out_len,
-                           status, n, W.ws, W.stamp);
+                           status, n, ws, W.stamp);
     NX_HIP_CHECK(hipGetLastError());
     W.stamp += iters;
     return NX_OK;

@@ -45,6 +45,7 @@
 #include <map>
 #include <mutex>
 #include "nx_common.hpp"
+#include "workspace.hpp"
 
 namespace nx {
 namespace dec {
@@ -1119,18 +1120,23 @@ __global__ void __launch_bounds__(256) k_lz4_serial(const uint8_t* __restrict__ 
 }  // namespace dec
 }  // namespace nx
 
-namespace {
-// Record workspace for the parse/expand pair, one per (device, stream): launches on one stream
-// are ordered and may share it; launches on different streams may overlap and must not.
-struct DecWorkspace {
-    uint32_t* rec = nullptr;
-    uint32_t* nrec = nullptr;
-    uint32_t* olen = nullptr;  // LZ4: bytes produced per block (the caller's lengths are inputs)
-    size_t frames = 0;
+static_assert(nx::kDecSlotBytes == nx::dec::kRecCap * sizeof(uint32_t) + 2 * sizeof(uint32_t) &&
+                  nx::kDecMaxFrames == nx::dec::kSubBatch,
+              "record workspace geometry");
+
+// The record slots of the device's shared workspace (workspace.hpp): rec[frames][kRecCap], then the
+// record counts and (LZ4) the block lengths produced.
+struct DecSlots {
+    uint32_t* rec;
+    uint32_t* nrec;
+    uint32_t* olen;
+    uint32_t frames;
 };
-std::mutex g_dws_mu;
-std::map<std::pair<int, hipStream_t>, DecWorkspace> g_dws;
-}  // namespace
+static DecSlots dec_slots(nx::SharedWs& W) {
+    uint32_t* p = static_cast<uint32_t*>(W.p);
+    const size_t f = W.slots;
+    return {p, p + f * nx::dec::kRecCap, p + f * nx::dec::kRecCap + f, (uint32_t)f};
+}
 
 // Dynamic-LDS limit of the wave kernels, set once per process.
 static hipError_t wave_kernel_attrs(size_t lds) {
@@ -1141,31 +1147,6 @@ static hipError_t wave_kernel_attrs(size_t lds) {
             if (attr_err == hipSuccess) attr_err = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     return attr_err;
-}
-
-// The (device, stream) record workspace with room for `sb` frames; caller holds g_dws_mu.
-static hipError_t dec_workspace(int dev, hipStream_t st, uint32_t sb, DecWorkspace** out) {
-    DecWorkspace& W = g_dws[{dev, st}];
-#define NX_HIP_CHECK_E(x)                \
-    do {                                 \
-        hipError_t e_ = (x);             \
-        if (e_ != hipSuccess) return e_; \
-    } while (0)
-    if (W.rec == nullptr || W.frames < sb) {
-        if (W.rec) NX_HIP_CHECK_E(hipFree(W.rec));  // hipFree synchronises with pending work
-        if (W.nrec) NX_HIP_CHECK_E(hipFree(W.nrec));
-        if (W.olen) NX_HIP_CHECK_E(hipFree(W.olen));
-        W.rec = nullptr;
-        W.nrec = nullptr;
-        W.olen = nullptr;
-        NX_HIP_CHECK_E(hipMalloc(&W.rec, (size_t)sb * nx::dec::kRecCap * sizeof(uint32_t)));
-        NX_HIP_CHECK_E(hipMalloc(&W.nrec, (size_t)sb * sizeof(uint32_t)));
-        NX_HIP_CHECK_E(hipMalloc(&W.olen, (size_t)sb * sizeof(uint32_t)));
-        W.frames = sb;
-    }
-#undef NX_HIP_CHECK_E
-    *out = &W;
-    return hipSuccess;
 }
 
 // one launch of the record expander over m frames
@@ -1205,11 +1186,10 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
         NX_HIP_CHECK(hipGetLastError());
         return NX_OK;
     }
-    const uint32_t sb = n < kSubBatch ? n : kSubBatch;
-    std::lock_guard<std::mutex> lk(g_dws_mu);
-    DecWorkspace* Wp = nullptr;
-    NX_HIP_CHECK(dec_workspace(dev, st, sb, &Wp));
-    DecWorkspace& W = *Wp;
+    nx::WsLease lease(nx::WsKind::DecRecords, dev, st);
+    NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::DecRecords, n, cus)));
+    const DecSlots W = dec_slots(lease.ws());
+    const uint32_t sb = n < W.frames ? n : W.frames;  // a held workspace caps the sub-batch
     for (uint32_t base = 0; base < n; base += sb) {
         const uint32_t m = n - base < sb ? n - base : sb;
         hipLaunchKernelGGL(k_parse, dim3((m + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, st, in, in_off + base, in_len + base,
@@ -1264,10 +1244,11 @@ extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off
     if (blocks_per_cu < 1) blocks_per_cu = 1;
     const hipStream_t st = (hipStream_t)stream;
     const uint64_t want = (uint64_t)cus * blocks_per_cu;
-    const uint32_t sb = n < kSubBatch ? n : kSubBatch;
-    std::lock_guard<std::mutex> lk(g_dws_mu);
-    DecWorkspace* W = nullptr;
-    NX_HIP_CHECK(dec_workspace(dev, st, sb, &W));
+    nx::WsLease lease(nx::WsKind::DecRecords, dev, st);
+    NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::DecRecords, n, cus)));
+    const DecSlots Ws = dec_slots(lease.ws());
+    const DecSlots* W = &Ws;
+    const uint32_t sb = n < W->frames ? n : W->frames;
     for (uint32_t base = 0; base < n; base += sb) {
         const uint32_t m = n - base < sb ? n - base : sb;
         const uint64_t need = (m + kWaves - 1) / kWaves;

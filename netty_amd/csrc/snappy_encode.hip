@@ -29,10 +29,10 @@
 // memory traffic differs.
 #include <stdlib.h>
 #include <algorithm>
-#include <map>
 #include <mutex>
 #include <vector>
 #include "nx_common.hpp"
+#include "workspace.hpp"
 
 namespace nx {
 namespace enc {
@@ -654,57 +654,30 @@ __global__ void __launch_bounds__(64) k_snappy_encode_lds(const uint8_t* __restr
 }  // namespace nx
 
 namespace {
-// Encoder hash-table workspace, one per (device, stream): launches on one stream are ordered, so
-// they may share a workspace; launches on different streams may overlap and must not.
-struct Workspace {
-    uint64_t* ws = nullptr;
-    size_t threads = 0;  // table slots (lanes of the dense form, waves of the spread form)
-    uint32_t stamp = 0;  // last stamp used; entries carry 6-bit stamps 1..63
-};
-std::mutex g_ws_mu;
-nx::PlacementReport g_place;  // the last dense-form workspace placement (nx_snappy_encode_placement)
-std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
 constexpr unsigned kEncBlock = 256;
-constexpr unsigned kEncWavesPerCU = 16;
 constexpr uint32_t kMaxStamp = 63;  // 6-bit stamps 1..63
-constexpr uint32_t kSpreadMaxChunks = 16384;  // above this the dense form is faster
+static_assert(nx::kWsSpec[(int)nx::WsKind::SnappyEnc].entry_bytes == sizeof(uint64_t) &&
+                  nx::kWsSpec[(int)nx::WsKind::SnappyEnc].lg == 14 && nx::kWsSpec[(int)nx::WsKind::SnappyEnc].waves_per_cu == 16,
+              "Snappy table geometry: 16384 64-bit entries, 16 waves per CU");
 }  // namespace
 
-namespace {
-// table slots a batch of n chunks (n > CUs) uses: one per wave (spread form) or per lane (dense form)
-size_t ws_slots(uint32_t n, int cus) {
-    const bool spread = n <= kSpreadMaxChunks;
-    const size_t want = (size_t)cus * kEncWavesPerCU * (spread ? 1 : 64);
-    return n < want ? (spread ? n : ((n + kEncBlock - 1) / kEncBlock) * kEncBlock) : want;
-}
-// (re)allocate W for `slots` tables; the caller holds g_ws_mu
-hipError_t ensure_ws(Workspace& W, size_t slots, hipStream_t st) {
-    if (W.ws != nullptr && W.threads >= slots) return hipSuccess;
-    if (W.ws) {
-        const hipError_t e = hipFree(W.ws);  // hipFree synchronises with pending work
-        if (e != hipSuccess) return e;
-    }
-    W.ws = nullptr;
-    // large (dense-form) workspaces: the fastest of several placements (nx_common.hpp alloc_placed_workspace)
-    const hipError_t e = nx::alloc_placed_workspace<uint64_t>(slots, 14, st, &W.ws, &g_place);
-    if (e != hipSuccess) return e;
-    W.threads = slots;
-    W.stamp = 0;
-    return hipSuccess;
-}
-}  // namespace
-
-// Place and zero the encoder's table workspace on `stream` for batches of up to max_chunks chunks
-// now, so a server sets it up at start-up, before its own buffers take the memory the placement
-// choice draws candidates from.  Optional: nx_snappy_encode_batch allocates on demand.
+// Place and zero the device's encoder table workspace for batches of up to max_chunks chunks now, so
+// a server sets it up at start-up, before its own buffers take the memory the placement choice draws
+// candidates from.  Kept until nx_workspaces_trim.  Optional: the standalone batch
+// API grows it on demand; batchers and handles hold their own share from creation.
 extern "C" int32_t nx_snappy_encoder_reserve(uint32_t max_chunks, void* stream) {
     int dev = 0, cus = 256;
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     if (max_chunks <= (uint32_t)cus) return NX_OK;  // the LDS form needs no workspace
-    const hipStream_t st = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    NX_HIP_CHECK(ensure_ws(g_ws[{dev, st}], ws_slots(max_chunks, cus), st));
+    const int32_t r = nx::ws_hold(nx::WsKind::SnappyEnc, dev, max_chunks, (hipStream_t)stream);
+    if (r != NX_OK) return r;
+    {
+        nx::SharedWs& W = nx::shared_ws(nx::WsKind::SnappyEnc, dev);
+        std::lock_guard<std::mutex> lk(W.mu);
+        W.kept = true;
+    }
+    nx::ws_unhold(nx::WsKind::SnappyEnc, dev);
     return NX_OK;
 }
 
@@ -731,28 +704,28 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
         NX_HIP_CHECK(hipGetLastError());
         return NX_OK;
     }
-    const bool spread = n <= kSpreadMaxChunks;
-    const size_t slots = ws_slots(n, cus);
     const size_t per = 16384u * sizeof(uint64_t);
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    Workspace& W = g_ws[{dev, st}];
-    NX_HIP_CHECK(ensure_ws(W, slots, st));
+    nx::WsLease lease(nx::WsKind::SnappyEnc, dev, st);
+    NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::SnappyEnc, n, cus)));
+    nx::SharedWs& W = lease.ws();
+    const nx::LaneGrid g = nx::ws_grid(nx::WsKind::SnappyEnc, n, cus, W.slots);
+    uint64_t* ws = static_cast<uint64_t*>(W.p);
     // Each launch gives a table slot at most kMaxStamp - 1 chunks (one stamp each).
-    const size_t per_launch = slots * (kMaxStamp - 1);
+    const size_t per_launch = g.slots * (kMaxStamp - 1);
     for (size_t base = 0; base < n; base += per_launch) {
         const uint32_t m = (uint32_t)std::min<size_t>(per_launch, n - base);
-        const uint32_t iters = (uint32_t)((m + slots - 1) / slots);
+        const uint32_t iters = (uint32_t)((m + g.slots - 1) / g.slots);
         if (W.stamp + iters >= kMaxStamp) {
-            NX_HIP_CHECK(hipMemsetAsync(W.ws, 0, W.threads * per, st));
+            NX_HIP_CHECK(hipMemsetAsync(ws, 0, W.slots * per, st));
             W.stamp = 0;
         }
-        if (spread) {
-            const size_t waves = std::min<size_t>(slots, m);
+        if (g.spread) {
+            const size_t waves = std::min<size_t>(g.slots, m);
             hipLaunchKernelGGL((nx::enc::k_snappy_encode<true, true>), dim3((unsigned)waves), dim3(64), 0, st, in, in_off + base,
-                               in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp);
+                               in_len + base, out, out_off + base, out_len + base, status + base, m, ws, W.stamp);
         } else {
-            hipLaunchKernelGGL((nx::enc::k_snappy_encode<true, false>), dim3((unsigned)(slots / kEncBlock)), dim3(kEncBlock), 0, st, in,
-                               in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, W.ws, W.stamp);
+            hipLaunchKernelGGL((nx::enc::k_snappy_encode<true, false>), dim3((unsigned)(g.slots / kEncBlock)), dim3(kEncBlock), 0, st, in,
+                               in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, ws, W.stamp);
         }
         NX_HIP_CHECK(hipGetLastError());
         W.stamp += iters;
@@ -764,9 +737,12 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
 // and the index kept; *n = 0 when no workspace has been placed yet.  Diagnostics only.
 extern "C" int32_t nx_snappy_encode_placement(float* probe_ms, int32_t cap, int32_t* n, int32_t* pick) {
     if (!n || !pick || (cap > 0 && !probe_ms)) return NX_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    *n = g_place.n;
-    *pick = g_place.pick;
-    for (int32_t k = 0; k < g_place.n && k < cap; ++k) probe_ms[k] = g_place.ms[k];
+    int dev = 0;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    nx::SharedWs& W = nx::shared_ws(nx::WsKind::SnappyEnc, dev);
+    std::lock_guard<std::mutex> lk(W.mu);
+    *n = W.place.n;
+    *pick = W.place.pick;
+    for (int32_t k = 0; k < W.place.n && k < cap; ++k) probe_ms[k] = W.place.ms[k];
     return NX_OK;
 }

@@ -1,0 +1,152 @@
+// workspace.hip — storage, growth and ownership of the shared device workspaces (workspace.hpp).
+#include <algorithm>
+#include "workspace.hpp"
+
+namespace nx {
+namespace {
+constexpr int kMaxDevices = 64;
+SharedWs g_ws[(int)WsKind::Count][kMaxDevices];
+thread_local bool t_no_grow = false;
+
+// Free W (waits for its last use first: nothing may still read or write it).
+hipError_t ws_drop(SharedWs& W) {
+    hipError_t e = hipSuccess;
+    if (W.p) {
+        if (W.used) e = hipEventSynchronize(W.ev);
+        const hipError_t f = hipFree(W.p);
+        if (e == hipSuccess) e = f;
+    }
+    W.p = nullptr;
+    W.slots = 0;
+    W.stamp = 0;
+    W.used = false;
+    return e;
+}
+
+hipError_t ws_mark(SharedWs& W, hipStream_t st) {
+    if (!W.ev) {
+        const hipError_t e = hipEventCreateWithFlags(&W.ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    W.used = true;
+    return hipEventRecord(W.ev, st);
+}
+
+// Reallocate W with at least `slots` slots (caller holds W.mu).  Blocking: set-up only.
+hipError_t ws_grow(WsKind k, SharedWs& W, size_t slots, hipStream_t st) {
+    if (W.p && W.slots >= slots) return hipSuccess;
+    hipError_t e = ws_drop(W);
+    if (e != hipSuccess) return e;
+    void* p = nullptr;
+    if (k == WsKind::DecRecords) {
+        e = hipMalloc(&p, slots * kDecSlotBytes);  // records are written before they are read: no zeroing
+    } else {
+        const WsSpec& s = kWsSpec[(int)k];
+        if (s.entry_bytes == 8) {
+            uint64_t* q = nullptr;
+            e = alloc_placed_workspace<uint64_t>(slots, s.lg, st, &q, &W.place);
+            p = q;
+        } else {
+            uint32_t* q = nullptr;
+            e = alloc_placed_workspace<uint32_t>(slots, s.lg, st, &q, &W.place);
+            p = q;
+        }
+    }
+    if (e != hipSuccess) return e;
+    W.p = p;
+    W.slots = slots;
+    W.stamp = 0;
+    return ws_mark(W, st);  // users on other streams wait for the zeroing
+}
+}  // namespace
+
+SharedWs& shared_ws(WsKind k, int dev) { return g_ws[(int)k][dev < 0 || dev >= kMaxDevices ? 0 : dev]; }
+
+size_t ws_want(WsKind k, uint32_t n, int cus) {
+    if (k == WsKind::DecRecords) return std::min<uint32_t>(n, kDecMaxFrames);
+    return lane_grid(n, cus, kWsSpec[(int)k].waves_per_cu).slots;
+}
+
+LaneGrid ws_grid(WsKind k, uint32_t n, int cus, size_t have) {
+    const unsigned wpcu = kWsSpec[(int)k].waves_per_cu;
+    LaneGrid g = lane_grid(n, cus, wpcu);
+    if (g.slots <= have) return g;
+    if (!g.spread && have >= kSpreadMaxChunks) {
+        g.slots = have / 256 * 256;
+        g.grid = (unsigned)(g.slots / 256);
+        return g;
+    }
+    g.spread = true;
+    g.block = 64;
+    g.slots = std::min<size_t>(std::min<size_t>(have, (size_t)cus * wpcu), n);
+    g.grid = (unsigned)g.slots;
+    return g;
+}
+
+NoGrowScope::NoGrowScope() : prev(t_no_grow) { t_no_grow = true; }
+NoGrowScope::~NoGrowScope() { t_no_grow = prev; }
+bool ws_no_grow() { return t_no_grow; }
+
+WsLease::WsLease(WsKind k, int dev, hipStream_t st) : k_(k), W_(shared_ws(k, dev)), lk_(W_.mu), st_(st) {}
+
+WsLease::~WsLease() {
+    if (acquired_) (void)ws_mark(W_, st_);  // the next user waits for this batch's launches
+}
+
+hipError_t WsLease::acquire(size_t want) {
+    if (!W_.p || (!t_no_grow && W_.slots < want)) {
+        const hipError_t e = ws_grow(k_, W_, std::max(want, W_.slots), st_);
+        if (e != hipSuccess) return e;
+        W_.kept = true;
+    }
+    acquired_ = true;
+    return W_.used ? hipStreamWaitEvent(st_, W_.ev, 0) : hipSuccess;
+}
+
+int32_t ws_hold(WsKind k, int dev, uint32_t units, hipStream_t st) {
+    int cus = 256;
+    NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    SharedWs& W = shared_ws(k, dev);
+    std::lock_guard<std::mutex> lk(W.mu);
+    NX_HIP_CHECK(ws_grow(k, W, std::max(ws_want(k, units, cus), W.slots), st));
+    W.owners += 1;
+    return NX_OK;
+}
+
+void ws_unhold(WsKind k, int dev) {
+    SharedWs& W = shared_ws(k, dev);
+    std::lock_guard<std::mutex> lk(W.mu);
+    if (W.owners > 0) W.owners -= 1;
+    if (W.owners == 0 && !W.kept) (void)ws_drop(W);
+}
+
+}  // namespace nx
+
+// Free, on the current device, every workspace no batcher or handle holds (those grown by the
+// standalone batch API or nx_snappy_encoder_reserve included); held ones stay, and are freed when
+// their last owner is.  Blocks until their last launches complete.
+extern "C" int32_t nx_workspaces_trim(void) {
+    int dev = 0;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    int32_t r = NX_OK;
+    for (int k = 0; k < (int)nx::WsKind::Count; ++k) {
+        nx::SharedWs& W = nx::shared_ws((nx::WsKind)k, dev);
+        std::lock_guard<std::mutex> lk(W.mu);
+        W.kept = false;
+        if (W.owners == 0 && nx::ws_drop(W) != hipSuccess) r = NX_ERR_HIP;
+    }
+    return r;
+}
+
+// Bytes of the workspace of `kind` (NX_WS_* in netty_amd.h) on the current device and its owners.
+extern "C" int32_t nx_workspace_info(int32_t kind, uint64_t* bytes, int32_t* owners) {
+    if (kind < 0 || kind >= (int32_t)nx::WsKind::Count || !bytes || !owners) return NX_ERR_INVALID_ARG;
+    int dev = 0;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    nx::SharedWs& W = nx::shared_ws((nx::WsKind)kind, dev);
+    std::lock_guard<std::mutex> lk(W.mu);
+    const nx::WsSpec& s = nx::kWsSpec[kind];
+    *bytes = kind == (int32_t)nx::WsKind::DecRecords ? W.slots * nx::kDecSlotBytes : W.slots * ((size_t)s.entry_bytes << s.lg);
+    *owners = W.owners;
+    return NX_OK;
+}

@@ -1,0 +1,85 @@
+// workspace.hpp — the device workspaces of the batch kernels (the encoders' per-lane hash tables,
+// the decoder's per-frame record slots): one per device and kind, shared by every stream.
+//
+// Launches that use a workspace are ordered on the device: a batch waits (hipStreamWaitEvent) for
+// the event the previous batch recorded after its launches, so the host never blocks and any number
+// of streams (the batcher's four, every handle's own) share one allocation.  A workspace grows only
+// where growth is allowed: in the standalone batch entry points (nx_*_batch called directly) and at
+// set-up (nx_snappy_encoder_reserve, nx_batcher_new and the handle constructors, which hold it).
+// Batches submitted by a batcher or a handle run inside a NoGrowScope: they use the slots the owner
+// reserved and cap their grid to them, so a flush never allocates, frees or probes.  The last owner
+// to let go frees it unless the standalone API grew it (then nx_workspaces_trim does).
+#pragma once
+#include <mutex>
+#include "nx_common.hpp"
+
+namespace nx {
+
+enum class WsKind : int { SnappyEnc = 0, Lz4Enc, FastLzEnc, LzfEnc, DecRecords, Count };
+
+// Table geometry per encoder kind (entry bytes, log2 entries per table, waves per CU of its launch);
+// each codec static_asserts its own constants against this.
+struct WsSpec {
+    uint32_t entry_bytes;
+    uint32_t lg;
+    unsigned waves_per_cu;
+};
+constexpr WsSpec kWsSpec[] = {{8, 14, 16}, {4, 13, 16}, {4, 13, 8}, {4, 14, 8}, {0, 0, 0}};
+constexpr size_t kDecSlotBytes = 16384u * 4u + 8u;  // records of one frame + its count and length
+constexpr uint32_t kDecMaxFrames = 262144;           // frames per parse/expand launch pair
+
+struct SharedWs {
+    std::mutex mu;
+    void* p = nullptr;
+    size_t slots = 0;    // tables (lanes or waves) or frames
+    uint32_t stamp = 0;  // encoders: last stamp used
+    hipEvent_t ev = nullptr;
+    bool used = false;   // ev has been recorded
+    int owners = 0;      // batchers and handles holding it
+    bool kept = false;   // grown by the standalone API or a reserve: kept until nx_workspaces_trim
+    PlacementReport place;
+};
+
+SharedWs& shared_ws(WsKind k, int dev);
+// slots a batch of n units asks for: the encoders' lane_grid slots, the decoder's frames per launch
+size_t ws_want(WsKind k, uint32_t n, int cus);
+// The lane-per-chunk grid for n chunks over at most `have` table slots: the dense form while it has
+// at least kSpreadMaxChunks lanes (a dense wave does the work of ~16 spread waves), else one chunk
+// per wave on up to cus * waves_per_cu waves.
+LaneGrid ws_grid(WsKind k, uint32_t n, int cus, size_t have);
+
+struct NoGrowScope {
+    NoGrowScope();
+    ~NoGrowScope();
+    bool prev;
+};
+bool ws_no_grow();
+
+// One batch's use of a workspace: holds its lock from acquire() to destruction.
+class WsLease {
+  public:
+    WsLease(WsKind k, int dev, hipStream_t st);
+    ~WsLease();
+    // Grow to `want` slots when growth is allowed (blocking, set-up only), allocate if there is no
+    // workspace yet, then order the stream after the previous user's launches.
+    hipError_t acquire(size_t want);
+    SharedWs& ws() { return W_; }
+
+  private:
+    WsKind k_;
+    SharedWs& W_;
+    std::unique_lock<std::mutex> lk_;
+    hipStream_t st_;
+    bool acquired_ = false;
+};
+
+// Owners: hold at creation (grows to `units` now), unhold at destruction (the last one frees).
+int32_t ws_hold(WsKind k, int dev, uint32_t units, hipStream_t st);
+void ws_unhold(WsKind k, int dev);
+
+// Owner sizes: a handle encodes a message of up to 1024 slices without waiting on another slot; a
+// batcher flush of up to 16384 slices / frames runs at full grid.
+constexpr uint32_t kHandleHoldUnits = 1024;
+constexpr uint32_t kBatcherHoldUnits = 16384;
+
+}  // namespace nx

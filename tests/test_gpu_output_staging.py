@@ -158,7 +158,10 @@ def test_encoder_workspace_placement_report(dev, B, oracle):
     the index kept, which must be the fastest."""
     import ctypes
     from netty_amd import _lib
-    s = torch.cuda.Stream(dev)  # a fresh stream gets its own workspace, placed now
+    import gc
+    gc.collect()
+    B.workspaces_trim()  # the device's workspace (unless a live handle holds one) is placed anew
+    s = torch.cuda.Stream(dev)
     chunks = [b"placement" * 7] * N_DENSE
     inp, off, ln = B.pack(chunks, dev, align=1)
     out, ooff = B.out_slots([B.snappy_max_compressed_length(len(c)) for c in chunks], dev)

@@ -1,0 +1,145 @@
+"""GPU tests of the shared device workspaces (csrc/workspace.hpp, include/netty_amd.h NX_WS_*): one
+encoder table workspace and one decoder record workspace per device, shared by every stream, held by
+batchers and handles from creation, never grown inside a flush, freed with their last owner.
+
+The reference allocates its tables per call (Snappy.java:187-211); these tests pin the resource
+behaviour of the GPU replacement, and that a batch capped to a held workspace (a grid narrower than
+the batch) still yields the oracle's bytes."""
+import gc
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def nx():
+    import netty_amd
+    return netty_amd
+
+
+@pytest.fixture(scope="module")
+def B():
+    from netty_amd import batch
+    return batch
+
+
+def _free_bytes():
+    torch.cuda.synchronize()
+    return torch.cuda.mem_get_info()[0]
+
+
+def _collect(B):
+    gc.collect()  # handles of earlier tests release their share in __del__
+    B.workspaces_trim()
+
+
+def test_handles_hold_and_release(nx, B):
+    _collect(B)
+    makers = {
+        B.WS_SNAPPY_ENC: lambda: nx.SnappyFrameEncoder(),
+        B.WS_DEC_RECORDS: lambda: nx.SnappyFrameDecoder(True),
+        B.WS_LZ4_ENC: lambda: nx.Lz4FrameEncoder(),
+        B.WS_FASTLZ_ENC: lambda: nx.FastLzFrameEncoder(),
+        B.WS_LZF_ENC: lambda: nx.LzfEncoder(),
+    }
+    for kind, mk in makers.items():
+        b0, o0 = B.workspace_info(kind)
+        h1, h2 = mk(), mk()
+        b1, o1 = B.workspace_info(kind)
+        assert o1 == o0 + 2 and b1 > 0 and b1 >= b0, kind
+        h1.close()
+        assert B.workspace_info(kind) == (b1, o0 + 1), kind  # the second holder keeps it
+        h2.close()
+        b2, o2 = B.workspace_info(kind)
+        assert o2 == o0, kind
+        if o0 == 0:
+            assert b2 == 0, kind  # the last owner frees it
+
+
+def test_standalone_growth_kept_until_trim(nx, B):
+    _collect(B)
+    _, owners = B.workspace_info(B.WS_SNAPPY_ENC)
+    if owners:
+        pytest.skip("a live handle of another test holds the workspace")
+    dev = torch.device("cuda:0")
+    chunks = [b"standalone %d " % i * 9 for i in range(2000)]
+    inp, off, ln = B.pack(chunks, dev, align=1)
+    out, ooff = B.out_slots([B.snappy_max_compressed_length(len(c)) for c in chunks], dev)
+    olen, st = B.snappy_encode(inp, off, ln, out, ooff)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    b1, o1 = B.workspace_info(B.WS_SNAPPY_ENC)
+    assert b1 > 0 and o1 == 0  # grown on demand, kept for the next standalone call
+    B.workspaces_trim()
+    assert B.workspace_info(B.WS_SNAPPY_ENC) == (0, 0)
+
+
+def test_handle_message_beyond_its_reservation(nx, B, oracle):
+    """A handle holds 1024 table slots; a 1100-slice message runs on that grid (some waves encode two
+    slices in turn) without growing it, and its bytes equal the oracle's."""
+    _collect(B)
+    e = nx.SnappyFrameEncoder()
+    held, _ = B.workspace_info(B.WS_SNAPPY_ENC)
+    msg = b"".join(oracle.textgen_chunk(900 + i, 32767) for i in range(1100))
+    got = e.encode(msg)
+    want, _ = oracle.snappy_frame_encode(msg)
+    assert got == want
+    assert B.workspace_info(B.WS_SNAPPY_ENC)[0] == held
+    e.close()
+
+
+def test_batcher_large_flushes_on_all_streams_one_workspace(nx, B, oracle):
+    """Eight flushes of 16 500 encoder slices each (two on each of the batcher's four streams, all in
+    flight together) and two 16 500-chunk decoder jobs: the workspaces reserved at nx_batcher_new are
+    the only ones (no growth during the flushes, device memory grows by less than one workspace),
+    every job's bytes equal the oracle's, and nx_batcher_free returns the memory."""
+    _collect(B)
+    enc = nx.SnappyFrameEncoder()
+    dec = nx.SnappyFrameDecoder(True)
+    free0 = _free_bytes()
+    e0, eo0 = B.workspace_info(B.WS_SNAPPY_ENC)
+    d0, do0 = B.workspace_info(B.WS_DEC_RECORDS)
+    b = nx.Batcher()
+    e1, eo1 = B.workspace_info(B.WS_SNAPPY_ENC)
+    d1, do1 = B.workspace_info(B.WS_DEC_RECORDS)
+    assert (eo1, do1) == (eo0 + 1, do0 + 1)
+    assert e1 >= e0 and d1 >= d0
+    free1 = _free_bytes()
+
+    n = 16500
+    msgs = [oracle.textgen_chunk(70000 + i, 19 + (i * 37) % 300) for i in range(n)]
+    stream = bytearray()
+    for i, m in enumerate(msgs):
+        stream += oracle.snappy_frame_encode(m, started=i > 0)[0]
+    stream = bytes(stream)
+    tickets = []
+    for f in range(8):
+        ts = [b.submit_encode(enc, m) for m in msgs]
+        td = b.submit_decode(dec, stream) if f in (0, 5) else None
+        b.flush()
+        tickets.append((ts, td))
+    assert b.stats()["flushes"] == 8
+    for f, (ts, td) in enumerate(tickets):
+        for j, (t, m) in enumerate(zip(ts, msgs)):
+            b.wait(t)
+            want = oracle.snappy_frame_encode(m, started=f > 0 or j > 0)[0]
+            assert b.result(t) == [want], (f, j)
+        if td is not None:
+            b.wait(td)
+            assert b.result(td) == msgs, f
+    assert B.workspace_info(B.WS_SNAPPY_ENC) == (e1, eo1)  # never grown inside a flush
+    assert B.workspace_info(B.WS_DEC_RECORDS) == (d1, do1)
+    free2 = _free_bytes()
+    assert free1 - free2 < max(e1, 64 * MiB), (free1 - free2) / MiB
+    b.close()
+    enc.close()
+    dec.close()
+    _, eo3 = B.workspace_info(B.WS_SNAPPY_ENC)
+    _, do3 = B.workspace_info(B.WS_DEC_RECORDS)
+    assert (eo3, do3) == (eo0 - 1, do0 - 1)  # the batcher's and the two handles' shares returned
+    free3 = _free_bytes()
+    assert free3 >= free0 - 64 * MiB, (free0 - free3) / MiB
