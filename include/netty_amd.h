@@ -102,13 +102,6 @@ int32_t nx_snappy_decode_batch_fused(const uint8_t* in, const uint64_t* in_off, 
                                      const uint32_t* expected_masked_crc, uint32_t* crc_out,
                                      uint32_t n, void* stream);
 
-/* Same contract as nx_snappy_decode_batch, reference-structured variant: one lane runs the serial
- * state machine per chunk (cross-check / baseline for the wave-cooperative kernel). */
-int32_t nx_snappy_decode_batch_naive(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
-                                     uint32_t* out_len, uint32_t* consumed, int32_t* status,
-                                     const uint32_t* expected_masked_crc, uint32_t* crc_out,
-                                     uint32_t n, void* stream);
 
 /* Replaces the chunk walk of SnappyFrameDecoder.decode (SnappyFrameDecoder.java:85-231) as
  * ByteToMessageDecoder.callDecode runs it over a cumulation (ByteToMessageDecoder.java:464-517),

@@ -35,7 +35,6 @@ _SIGS = {
     "nx_lzf_max_compressed_length": (sz, [sz]),
     "nx_snappy_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_snappy_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
-    "nx_snappy_decode_batch_naive": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_snappy_decode_batch_fused": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_crc32c_masked_batch": (i32, [vp, vp, vp, vp, u32, vp]),
     "nx_snappy_frame_scan_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, vp]),

@@ -65,22 +65,20 @@ def snappy_encode(inp, in_off, in_len, out, out_off, out_len=None, status=None):
 
 
 def snappy_decode(inp, in_off, in_len, out, out_off, out_cap=None, expected_crc=None, want_crc=False, consumed=False,
-                  naive=False, out_len=None, status=None, variant="auto"):
+                  out_len=None, status=None, variant="auto", fn=None):
     """Snappy.decode per chunk (+ fused masked-CRC32C verify).  Returns dict of tensors.
 
-    variant: "auto" (parse/expand kernel pair), "fused" (single-kernel wave decoder) or "naive"
-    (lane-per-chunk reference-structured kernel); all three have the same contract."""
+    variant: "auto" (parse/expand kernel pair) or "fused" (single-kernel wave decoder), with the same
+    contract; fn: another entry point of that contract (the tests' lane-per-chunk cross-check kernel)."""
     n = in_len.numel()
     dev = inp.device
     out_len = torch.empty(n, dtype=torch.int32, device=dev) if out_len is None else out_len
     status = torch.empty(n, dtype=torch.int32, device=dev) if status is None else status
     cons = torch.empty(n, dtype=torch.int32, device=dev) if consumed else None
     crc = torch.empty(n, dtype=torch.int32, device=dev) if want_crc else None
-    if naive:
-        variant = "naive"
     lib = _lib.load()
-    fn = {"auto": lib.nx_snappy_decode_batch, "fused": lib.nx_snappy_decode_batch_fused,
-          "naive": lib.nx_snappy_decode_batch_naive}[variant]
+    if fn is None:
+        fn = {"auto": lib.nx_snappy_decode_batch, "fused": lib.nx_snappy_decode_batch_fused}[variant]
     _chk(fn(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(cons),
             _ptr(status), _ptr(expected_crc), _ptr(crc), n, _stream()), "nx_snappy_decode_batch")
     return {"out_len": out_len, "status": status, "consumed": cons, "crc": crc}

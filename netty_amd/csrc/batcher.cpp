@@ -26,9 +26,14 @@
 //
 // Results are applied in submission order per decoder: a failing chunk marks the decoder corrupted
 // (:227-230) and the jobs submitted after it on that decoder deliver nothing (Java skips all later
-// input, :86-89).  Limitation of the asynchronous path: a validating decoder whose compressed chunk
-// decodes fewer bytes than its length (the leftover is re-parsed as a chunk header in Java, :206-212)
-// fails that job with NX_ERR_FRAME_CORRUPT; the synchronous nx_snappy_frame_decoder_decode is exact.
+// input, :86-89).  A validating decoder's compressed chunk that decodes fewer bytes than its length
+// leaves the rest to be parsed again as a chunk header (:206-212); that is known only at apply().  So a
+// validating decoder keeps the bytes its unapplied jobs walked (and any partial chunk after them, which
+// it carries into the next submit instead of leaving it in the caller's cumulation), and apply() walks
+// them again from the leftover: the job continues in the collecting batch (launched by the next
+// poll/wait) with the messages it has so far, and the decoder's jobs walked before that deliver
+// nothing (their bytes are in the continuation).  Messages and errors equal the synchronous
+// nx_snappy_frame_decoder_decode's, in the same order; they may arrive on an earlier ticket.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
@@ -253,6 +258,11 @@ struct Job {
     int32_t status = NX_OK;
     std::vector<nx_msg> msgs;
     std::string err;
+    // decode, validating decoders: the walked bytes start at stream position s_base (acts[].data is
+    // relative to it), under the decoder's re-walk epoch; `walked` = s_base is in dec->outstanding
+    uint64_t s_base = 0, epoch = 0;
+    bool walked = false;
+    std::deque<std::vector<uint8_t>> owned;  // messages delivered before a re-walk moved the job to a later batch
 };
 
 struct Batch {
@@ -363,14 +373,15 @@ struct nx_batcher {
     uint64_t launches = 0, chunks = 0, flushes = 0;
     uint64_t applied = 0;     // batches applied, in flush order (Batch::seq < applied)
     size_t flush_bytes = 0;   // auto-flush threshold on a batch's input bytes (0 = only explicit flushes)
+    std::vector<std::pair<Job*, Batch*>> cont;  // re-walked jobs to queue again (found by apply())
+    bool kick = false;        // the collecting batch holds a re-walked job: launch it at the next poll/wait
 };
 
 namespace {
 
 bool advance(nx_batcher* b, uint64_t upto, bool block);
 
-Batch* fresh_batch(nx_batcher* b) {
-    advance(b, ~0ull, false);  // apply every completed batch (in flush order), even if its jobs were released unpolled
+Batch* reuse_or_new_batch(nx_batcher* b) {
     for (Batch* x : b->all) {
         if (!x->inflight && x->live == 0 && x != b->cur) {
             x->reset();
@@ -386,9 +397,175 @@ Batch* fresh_batch(nx_batcher* b) {
     return x;
 }
 
+Batch* fresh_batch(nx_batcher* b) {
+    advance(b, ~0ull, false);  // apply every completed batch (in flush order), even if its jobs were released unpolled
+    return reuse_or_new_batch(b);
+}
+
 Batch* collecting(nx_batcher* b) {
-    if (!b->cur) b->cur = fresh_batch(b);
+    if (!b->cur) {
+        Batch* x = fresh_batch(b);
+        if (!b->cur) b->cur = x;  // advance() may have opened one for re-walked jobs
+    }
     return b->cur;
+}
+
+// Drop the stream bytes no unapplied job of a validating decoder can re-walk any more.
+void trim_hist(nx_snappy_frame_decoder* d) {
+    if (d->corrupted) {  // (:86-89): nothing is parsed again
+        d->hist.clear();
+        d->hist.shrink_to_fit();
+        d->hist_base = d->parse_pos;
+        return;
+    }
+    const uint64_t keep = d->outstanding.empty() ? d->parse_pos : *d->outstanding.begin();
+    if (keep > d->hist_base) {
+        d->hist.erase(d->hist.begin(), d->hist.begin() + (ptrdiff_t)(keep - d->hist_base));
+        d->hist_base = keep;
+    }
+}
+
+void unwalk(Job* j) {  // the job no longer needs its walked bytes kept
+    if (!j->walked) return;
+    nx_snappy_frame_decoder* d = j->dec;
+    auto it = d->outstanding.find(j->s_base);
+    if (it != d->outstanding.end()) d->outstanding.erase(it);
+    j->walked = false;
+}
+
+// Queue decoder job j's walked actions into batch bt.  Payloads are copied from S (host bytes the
+// walk ran over), or, with dS (the device address of S in registered memory), gathered from there at
+// flush.  On failure the batch's arrays go back to their sizes at entry (its other jobs stay valid).
+int32_t enqueue_dec(Batch* bt, Job* j, const uint8_t* S, size_t walked, const uint8_t* dS) {
+    const size_t n_act = bt->dact.size(), n_dc = bt->dc_off.size(), n_du = bt->du_off.size(), n_dir = bt->direct.size();
+    const uint64_t dir_used = bt->direct_used;
+    auto fail = [&](int32_t code) -> int32_t {
+        bt->dact.resize(n_act);
+        bt->dact_direct.resize(n_act);
+        bt->dc_off.resize(n_dc);
+        bt->dc_len.resize(n_dc);
+        bt->dc_crc.resize(n_dc);
+        bt->dc_direct.resize(n_dc);
+        bt->du_off.resize(n_du);
+        bt->du_len.resize(n_du);
+        bt->du_direct.resize(n_du);
+        bt->direct.resize(n_dir);
+        bt->direct_used = dir_used;
+        return code;
+    };
+    uint64_t rbase = 0;
+    if (dS && walked) {
+        rbase = (bt->direct_used + 15) & ~15ull;
+        bt->direct.push_back({S, dS, walked, rbase});
+        bt->direct_used = rbase + walked;
+    }
+    DecJob J{};
+    J.a0 = (uint32_t)bt->dact.size();
+    J.validate = j->dec->validate ? 1u : 0u;
+    size_t out_need = 0;
+    for (const SnappyAction& a : j->acts) {
+        if (a.kind != SAct::Uncomp && a.kind != SAct::Comp) continue;
+        uint64_t off = 0;
+        if (dS) {
+            off = rbase + a.data;
+        } else {
+            uint8_t* st = bt->stage(a.dlen, &off);
+            if (!st) return fail(NX_ERR_HIP);
+            memcpy(st, S + a.data, a.dlen);
+        }
+        const uint8_t dir = dS ? 1 : 0;
+        bt->dact_direct.push_back(dir);
+        DecAct A{off, a.dlen, 0, 0, a.crc};
+        if (a.kind == SAct::Comp) {
+            A.kind = 2;
+            A.chunk = (uint32_t)bt->dc_off.size();
+            bt->dc_off.push_back(off);
+            bt->dc_len.push_back(a.dlen);
+            bt->dc_crc.push_back(a.crc);
+            bt->dc_direct.push_back(dir);
+            if (j->dec->validate) bt->dc_validate = true;
+            out_need += nx::bt::snappy_decoded_bound(a.dlen);
+        } else {
+            A.kind = 1;
+            A.chunk = (uint32_t)bt->du_off.size();
+            bt->du_off.push_back(off);
+            bt->du_len.push_back(a.dlen);
+            bt->du_direct.push_back(dir);
+            out_need += a.dlen;
+        }
+        bt->dact.push_back(A);
+    }
+    J.na = (uint32_t)bt->dact.size() - J.a0;
+    if (!bt->reserve_out(out_need + 16, &J.out_off)) return fail(NX_ERR_HIP);
+    j->index = (uint32_t)bt->djob.size();
+    bt->djob.push_back(J);
+    bt->jobs.push_back(j);
+    return NX_OK;
+}
+
+// The header walk of SnappyFrameDecoder.decode over S[0..n) from the decoder's state (:85-231); a
+// header-level error ends it and is kept on the job, applied in order (the decoder turns corrupted then).
+size_t walk(nx_snappy_frame_decoder* d, Job* j, const uint8_t* S, size_t n, bool& started, uint64_t& skip) {
+    size_t p = 0;
+    j->acts.clear();
+    j->has_parse_err = false;
+    j->parse_err.clear();
+    while (p < n && nx::fr::snappy_parse_one(S, n, p, started, skip, d->validate, j->acts)) {
+    }
+    if (!j->acts.empty() && j->acts.back().kind == SAct::Error) {
+        j->has_parse_err = true;
+        j->parse_err = j->acts.back().err;
+        p = j->acts.back().end;
+        j->acts.pop_back();
+    }
+    return p;
+}
+
+bool has_gpu_work(const Job* j) {
+    for (const SnappyAction& a : j->acts)
+        if (a.kind == SAct::Uncomp || a.kind == SAct::Comp) return true;
+    return false;
+}
+
+// Job j's compressed chunk decoded fewer bytes than its length, in validating mode: Java leaves the
+// rest in the cumulation and parses it as the next chunk header (SnappyFrameDecoder.java:206-212).
+// Walk the decoder's stream again from q (the first unread byte): every byte handed over so far, so
+// the walks of the decoder's later, not yet applied jobs are void (new epoch; they deliver nothing and
+// their bytes are covered here).  Returns true when j has GPU work again: it is queued into the
+// collecting batch by queue_continuations() and completes there.
+bool rewalk(nx_batcher* b, Batch* bt, Job* j, uint64_t q) {
+    nx_snappy_frame_decoder* d = j->dec;
+    d->epoch += 1;
+    d->parse_failed = false;
+    bool started = true;  // a compressed chunk was accepted (:180-183)
+    uint64_t skip = 0;
+    const uint8_t* S = d->hist.data() + (q - d->hist_base);
+    const size_t n = (size_t)(d->hist_base + d->hist.size() - q);
+    const size_t p = walk(d, j, S, n, started, skip);
+    d->started = started;
+    d->skip = skip;
+    d->parse_pos = q + p;
+    if (j->has_parse_err) d->parse_failed = true;
+    j->s_base = q;
+    j->epoch = d->epoch;
+    if (!has_gpu_work(j)) {
+        if (j->has_parse_err) {
+            j->status = NX_ERR_FRAME_CORRUPT;
+            j->err = j->parse_err;
+            d->corrupted = true;  // (:227-230)
+        }
+        return false;
+    }
+    // the messages so far live in bt's arena, which may be reused before j completes elsewhere
+    for (nx_msg& m : j->msgs) {
+        j->owned.emplace_back(m.data, m.data + m.len);
+        m.data = j->owned.back().data();
+    }
+    d->outstanding.insert(q);
+    j->walked = true;
+    j->applied = false;
+    b->cont.push_back({j, bt});
+    return true;
 }
 
 // Launch everything `bt` collected (batcher lock held).
@@ -530,7 +707,11 @@ int32_t fail_batch(nx_batcher* b, Batch* bt, int32_t code) {
         j->status = code;
         j->err = "GPU batch launch failed";
         j->msgs.clear();
-        if (j->kind == 1 && j->dec) j->dec->corrupted = true;
+        if (j->kind == 1 && j->dec) {
+            unwalk(j);
+            j->dec->corrupted = true;
+            trim_hist(j->dec);
+        }
     }
     bt->inflight = false;
     bt->done = true;
@@ -543,7 +724,7 @@ int32_t launch(nx_batcher* b, Batch* bt) {
 }
 
 // The batch is complete: turn the result records into each job's messages, in submission order.
-void apply(Batch* bt) {
+void apply(nx_batcher* b, Batch* bt) {
     const int64_t* res_len = reinterpret_cast<const int64_t*>(bt->out.h + bt->res_enc);
     const DecRes* dres = reinterpret_cast<const DecRes*>(bt->out.h + bt->res_dec);
     char buf[160];
@@ -562,10 +743,16 @@ void apply(Batch* bt) {
         }
         nx_snappy_frame_decoder* d = j->dec;
         j->applied = true;
-        if (d->corrupted) continue;  // an earlier job of this decoder failed: Java skips later input (:86-89)
+        unwalk(j);
+        // an earlier job of this decoder failed: Java skips later input (:86-89); or a re-walk after an
+        // earlier job's leftover covered this job's bytes
+        if (d->corrupted || (d->validate && j->epoch != d->epoch)) {
+            trim_hist(d);
+            continue;
+        }
         const DecJob& J = bt->djob[j->index];
         uint32_t a = J.a0;
-        bool failed = false;
+        bool failed = false, moved = false;
         for (const SnappyAction& act : j->acts) {
             if (act.kind != SAct::Uncomp && act.kind != SAct::Comp) {
                 if (act.kind == SAct::Stream) d->started = true;
@@ -586,21 +773,65 @@ void apply(Batch* bt) {
                 break;
             }
             j->msgs.push_back({bt->out.h + R.off, (size_t)R.len});
-            if (A.kind == 2 && J.validate && R.cons < A.len) {  // validating-mode leftover (:206-212): see header
-                j->status = NX_ERR_FRAME_CORRUPT;
-                j->err = "asynchronous validating decode: compressed chunk shorter than its length (use the synchronous decoder)";
-                failed = true;
+            if (A.kind == 2 && J.validate && R.cons < A.len) {  // validating-mode leftover (:206-212)
+                moved = rewalk(b, bt, j, j->s_base + act.data + R.cons);
                 break;
             }
         }
-        if (!failed && j->has_parse_err) {
+        if (!failed && !moved && j->has_parse_err) {
             j->status = NX_ERR_FRAME_CORRUPT;
             j->err = j->parse_err;
             failed = true;
         }
         if (failed) d->corrupted = true;  // (:227-230)
+        trim_hist(d);
     }
     bt->done = true;
+}
+
+// Queue the jobs apply() re-walked into the collecting batch (after every job already in it: those of
+// the same decoder were walked before the re-walk and deliver nothing).  The next poll()/wait() launches it.
+void queue_continuations(nx_batcher* b) {
+    for (auto& [j, from] : b->cont) {
+        Batch* to = b->cur ? b->cur : reuse_or_new_batch(b);
+        nx_snappy_frame_decoder* d = j->dec;
+        for (size_t k = 0; k < from->jobs.size(); ++k)
+            if (from->jobs[k] == j) {
+                from->jobs.erase(from->jobs.begin() + (ptrdiff_t)k);
+                break;
+            }
+        auto it = b->tickets.find(j->ticket);
+        const bool live = it != b->tickets.end();
+        if (!to || enqueue_dec(to, j, d->hist.data() + (j->s_base - d->hist_base), 0, nullptr) != NX_OK) {
+            // cannot queue it: the job fails as a launch failure would (result() reports it)
+            unwalk(j);
+            j->applied = true;
+            j->status = NX_ERR_HIP;
+            j->err = "GPU batch launch failed";
+            d->corrupted = true;
+            trim_hist(d);
+            from->jobs.push_back(j);  // stays owned by its batch
+            continue;
+        }
+        b->cur = to;
+        if (live) {
+            if (from->live) from->live -= 1;
+            to->live += 1;
+            it->second.first = to;
+        }
+        b->kick = true;
+    }
+    b->cont.clear();
+}
+
+// Launch a collecting batch that holds re-walked jobs (their tickets are already out).
+void kick(nx_batcher* b) {
+    if (!b->kick) return;
+    b->kick = false;
+    Batch* bt = b->cur;
+    if (!bt || bt->jobs.empty()) return;
+    b->cur = nullptr;
+    (void)launch(b, bt);  // a failed launch completes the batch's jobs with the error
 }
 
 // Apply completed batches in flush order up to (and including) sequence number `upto`; false if one
@@ -613,9 +844,10 @@ bool advance(nx_batcher* b, uint64_t upto, bool block) {
         if (!bt) return false;  // unreachable: every launched batch stays in flight until applied
         const hipError_t e = block ? hipEventSynchronize(bt->ev) : hipEventQuery(bt->ev);
         if (e != hipSuccess) return false;
-        apply(bt);
+        apply(b, bt);
         bt->inflight = false;
         b->applied += 1;
+        if (!b->cont.empty()) queue_continuations(b);
     }
     return true;
 }
@@ -779,97 +1011,64 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
     j->ticket = b->next_ticket++;
     j->kind = 1;
     j->dec = d;
-    size_t p = 0;
-    if (d->corrupted || d->parse_failed) {  // (:86-89): an earlier input failed
+    size_t p = 0;  // bytes of `in` consumed
+    // the chunk-header walk runs now, so the decoder's started/skip state advances in call order; it
+    // is committed below, once the job is queued
+    bool started = d->started;
+    uint64_t skip = d->skip;
+    const uint8_t* S = in;  // the walked bytes: a validating decoder's carried bytes, then `in`
+    size_t carried = 0, walked = 0;
+    std::vector<uint8_t> joined;
+    const bool skipping = d->corrupted || d->parse_failed;  // (:86-89): an earlier input failed
+    if (skipping) {
         p = n;
     } else {
-        // the chunk-header walk runs now, so the decoder's started/skip state advances in call order
-        bool started = d->started;
-        uint64_t skip = d->skip;
-        while (p < n && nx::fr::snappy_parse_one(in, n, p, started, skip, d->validate, j->acts)) {
+        if (d->validate) {
+            carried = (size_t)(d->hist_base + d->hist.size() - d->parse_pos);
+            if (carried) {
+                joined.reserve(carried + n);
+                joined.assign(d->hist.end() - (ptrdiff_t)carried, d->hist.end());
+                joined.insert(joined.end(), in, in + n);
+                S = joined.data();
+            }
         }
-        if (!j->acts.empty() && j->acts.back().kind == SAct::Error) {
-            j->has_parse_err = true;
-            j->parse_err = j->acts.back().err;
-            p = j->acts.back().end;
-            j->acts.pop_back();
+        walked = walk(d, j, S, carried + n, started, skip);
+        p = walked > carried ? walked - carried : 0;
+    }
+    // registered cumulation: the consumed bytes are gathered from the mapped pages at flush (the
+    // caller keeps them valid until the job completes); else every payload is copied now
+    const uint8_t* dS = nullptr;
+    if (registered && walked && !carried) {
+        dS = registered_device_ptr(in, walked);
+        if (!dS) {  // not inside an nx_host_register'd range
+            delete j;
+            return NX_ERR_INVALID_ARG;
         }
+    }
+    if (enqueue_dec(bt, j, S, walked, dS) != NX_OK) {
+        delete j;
+        return NX_ERR_HIP;
+    }
+    *consumed = p;
+    if (!skipping) {
         d->started = started;
         d->skip = skip;
         // later submits skip their input (:227-230); the decoder turns corrupted when this job is
         // applied, after the jobs submitted before it have delivered their messages
         if (j->has_parse_err) d->parse_failed = true;
     }
-    *consumed = p;
-    // on a failure below the batch's arrays go back to their sizes at entry (other jobs stay valid)
-    const size_t n_act = bt->dact.size(), n_dc = bt->dc_off.size(), n_du = bt->du_off.size(), n_dir = bt->direct.size();
-    const uint64_t dir_used = bt->direct_used;
-    auto fail = [&](int32_t code) -> int64_t {
-        bt->dact.resize(n_act);
-        bt->dact_direct.resize(n_act);
-        bt->dc_off.resize(n_dc);
-        bt->dc_len.resize(n_dc);
-        bt->dc_crc.resize(n_dc);
-        bt->dc_direct.resize(n_dc);
-        bt->du_off.resize(n_du);
-        bt->du_len.resize(n_du);
-        bt->du_direct.resize(n_du);
-        bt->direct.resize(n_dir);
-        bt->direct_used = dir_used;
-        delete j;
-        return code;
-    };
-    // registered cumulation: the consumed bytes are gathered from the mapped pages at flush (the
-    // caller keeps them valid until the job completes); else every payload is copied now
-    uint64_t rbase = 0;
-    if (registered && p) {
-        const uint8_t* dsrc = registered_device_ptr(in, p);
-        if (!dsrc) return fail(NX_ERR_INVALID_ARG);  // not inside an nx_host_register'd range
-        rbase = (bt->direct_used + 15) & ~15ull;
-        bt->direct.push_back({in, dsrc, p, rbase});
-        bt->direct_used = rbase + p;
-    }
-    DecJob J{};
-    J.a0 = (uint32_t)bt->dact.size();
-    J.validate = d->validate ? 1u : 0u;
-    size_t out_need = 0;
-    for (const SnappyAction& a : j->acts) {
-        if (a.kind != SAct::Uncomp && a.kind != SAct::Comp) continue;
-        uint64_t off = 0;
-        if (registered) {
-            off = rbase + a.data;
-        } else {
-            uint8_t* st = bt->stage(a.dlen, &off);
-            if (!st) return fail(NX_ERR_HIP);
-            memcpy(st, in + a.data, a.dlen);
+    if (d->validate && !d->corrupted) {
+        // every consumed byte is kept until no unapplied job can re-walk it (a leftover, :206-212);
+        // skipped input too, since a re-walk may find that the failure was not reached after all
+        d->hist.insert(d->hist.end(), in, in + p);
+        if (!skipping) {
+            j->s_base = d->parse_pos;
+            j->epoch = d->epoch;
+            j->walked = true;
+            d->outstanding.insert(j->s_base);
+            d->parse_pos += walked;
         }
-        const uint8_t dir = registered ? 1 : 0;
-        bt->dact_direct.push_back(dir);
-        DecAct A{off, a.dlen, 0, 0, a.crc};
-        if (a.kind == SAct::Comp) {
-            A.kind = 2;
-            A.chunk = (uint32_t)bt->dc_off.size();
-            bt->dc_off.push_back(off);
-            bt->dc_len.push_back(a.dlen);
-            bt->dc_crc.push_back(a.crc);
-            bt->dc_direct.push_back(dir);
-            if (d->validate) bt->dc_validate = true;
-            out_need += nx::bt::snappy_decoded_bound(a.dlen);
-        } else {
-            A.kind = 1;
-            A.chunk = (uint32_t)bt->du_off.size();
-            bt->du_off.push_back(off);
-            bt->du_len.push_back(a.dlen);
-            bt->du_direct.push_back(dir);
-            out_need += a.dlen;
-        }
-        bt->dact.push_back(A);
     }
-    J.na = (uint32_t)bt->dact.size() - J.a0;
-    if (!bt->reserve_out(out_need + 16, &J.out_off)) return fail(NX_ERR_HIP);
-    j->index = (uint32_t)bt->djob.size();
-    bt->djob.push_back(J);
-    bt->jobs.push_back(j);
     bt->live += 1;
     b->tickets[j->ticket] = {bt, j};
     (void)maybe_autoflush(b, bt);  // a failed launch completes the job with the error (result())
@@ -890,6 +1089,7 @@ extern "C" int64_t nx_snappy_frame_decoder_submit_registered(nx_snappy_frame_dec
 extern "C" int32_t nx_batcher_flush(nx_batcher* b) {
     if (!b) return NX_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(b->mu);
+    b->kick = false;
     Batch* bt = b->cur;
     if (!bt || bt->jobs.empty()) return NX_OK;
     b->cur = nullptr;
@@ -901,26 +1101,35 @@ extern "C" int32_t nx_batcher_poll(nx_batcher* b, int64_t ticket) {
     std::lock_guard<std::mutex> lk(b->mu);
     auto it = b->tickets.find((uint64_t)ticket);
     if (it == b->tickets.end()) return NX_ERR_INVALID_ARG;
-    return poll_batch(b, it->second.first, false) ? 1 : 0;
+    Job* j = it->second.second;
+    (void)poll_batch(b, it->second.first, false);
+    kick(b);
+    return j->applied ? 1 : 0;  // a re-walked job continues in a later batch
 }
 
 extern "C" int32_t nx_batcher_wait(nx_batcher* b, int64_t ticket) {
     if (!b) return NX_ERR_INVALID_ARG;
-    Batch* bt;
-    {
-        std::lock_guard<std::mutex> lk(b->mu);
-        auto it = b->tickets.find((uint64_t)ticket);
-        if (it == b->tickets.end()) return NX_ERR_INVALID_ARG;
-        bt = it->second.first;
-        if (bt == b->cur) {  // not flushed yet: flush now
-            b->cur = nullptr;
-            (void)launch(b, bt);  // a failed launch completes the batch's jobs with the error
+    for (;;) {  // more than one pass only when a re-walk moved the job to a later batch
+        Batch* bt;
+        Job* j;
+        {
+            std::lock_guard<std::mutex> lk(b->mu);
+            auto it = b->tickets.find((uint64_t)ticket);
+            if (it == b->tickets.end()) return NX_ERR_INVALID_ARG;
+            bt = it->second.first;
+            j = it->second.second;
+            if (bt == b->cur) {  // not flushed yet: flush now
+                b->cur = nullptr;
+                (void)launch(b, bt);  // a failed launch completes the batch's jobs with the error
+            }
+            if (j->applied) return NX_OK;
         }
-        if (bt->done) return NX_OK;
+        if (hipEventSynchronize(bt->ev) != hipSuccess) return NX_ERR_HIP;
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (!poll_batch(b, bt, true)) return NX_ERR_HIP;
+        kick(b);
+        if (j->applied) return NX_OK;
     }
-    if (hipEventSynchronize(bt->ev) != hipSuccess) return NX_ERR_HIP;
-    std::lock_guard<std::mutex> lk(b->mu);
-    return poll_batch(b, bt, true) ? NX_OK : NX_ERR_HIP;
 }
 
 extern "C" int32_t nx_batcher_result(nx_batcher* b, int64_t ticket, const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <set>
 #include <string>
 #include <vector>
 #include "../../include/netty_amd.h"
@@ -95,4 +96,14 @@ struct nx_snappy_frame_decoder {
     bool parse_failed = false;  // batcher: a submitted input failed its header walk (applied later, in order)
     uint64_t skip = 0;  // numBytesToSkip
     nx::h::MsgList ml;
+    // Batcher, validating decoders only.  A compressed chunk that decodes fewer bytes than its length
+    // leaves the rest to be parsed again as the next chunk header (SnappyFrameDecoder.java:206-212),
+    // which is only known once the chunk is decoded.  So the handed-over byte stream is kept from the
+    // first byte a not-yet-applied job walked (absolute positions in the decoder's stream): a leftover
+    // found at apply() re-walks it from there.
+    std::vector<uint8_t> hist;         // stream bytes [hist_base, hist_base + hist.size())
+    uint64_t hist_base = 0;
+    uint64_t parse_pos = 0;            // the header walk has reached here; [parse_pos, end) is carried into the next submit
+    uint64_t epoch = 0;                // bumped by each re-walk: jobs walked under an older epoch deliver nothing
+    std::multiset<uint64_t> outstanding;  // walk starts of jobs submitted and not yet applied
 };

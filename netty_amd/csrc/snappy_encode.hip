@@ -541,8 +541,8 @@ done:
     return w.pos();
 }
 
-// Launch bound 6 blocks of 256 per CU keeps the kernel under 80 VGPRs (no spills) at the 16 waves/CU
-// the host launches.
+// __launch_bounds__(256, 4): at least 4 blocks of 256 (16 waves) per CU, the residency the host
+// launches for, so the kernel stays within 128 VGPRs per lane.
 //
 // SPREAD = false: lane t encodes chunks t, t + lanes, ... (throughput form, every lane of a wave busy).
 // SPREAD = true: one chunk per WAVE, lane 0 only (small batches: lanes of different chunks never share

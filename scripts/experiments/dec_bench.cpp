@@ -1,9 +1,9 @@
 // Standalone timing harness for the Snappy decode kernels (experiments only).  N text chunks of
 // 64 KiB (include/netty_amd_textgen.h) are encoded with libnetty_amd's nx_snappy_encode_batch, then
-// decoded R times with the k_parse / k_expand of DEC_SRC (compiled into this binary, variants by
-// -D flags); per-kernel ms (HIP events) and the identity check are printed.
+// decoded R times with the k_parse / k_expand of DEC_SRC (default: the product source; an A/B copy
+// with -D flags for variants), compiled into this binary; per-kernel ms (HIP events) and the identity check are printed.
 #ifndef DEC_SRC
-#define DEC_SRC "snappy_decode_exp.hip"
+#define DEC_SRC "../../netty_amd/csrc/snappy_decode.hip"
 #endif
 #include DEC_SRC
 #include "../../include/netty_amd.h"
@@ -12,7 +12,7 @@
 #include <string.h>
 #include <vector>
 int main(int argc, char** argv) {
-    using namespace nx::decx;
+    using namespace nx::dec;
     int N = argc > 1 ? atoi(argv[1]) : 65536, R = argc > 2 ? atoi(argv[2]) : 3, crc = argc > 3 ? atoi(argv[3]) : 1;
     const int L = 65536;
     static nx_textgen_tables tg;

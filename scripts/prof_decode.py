@@ -21,7 +21,7 @@ ts = []
 for _ in range(R):
     a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
     a.record()
-    r = B.snappy_decode(enc, eoff, elen, dec, off, expected_crc=crc, variant=os.environ.get("NX_VARIANT", "naive" if os.environ.get("NX_NAIVE") == "1" else "auto"))
+    r = B.snappy_decode(enc, eoff, elen, dec, off, expected_crc=crc, variant=os.environ.get("NX_VARIANT", "auto"))
     b.record()
     torch.cuda.synchronize()
     ts.append(a.elapsed_time(b))

@@ -24,3 +24,18 @@ def oracle():
     from oracle import pyoracle
     pyoracle.build()
     return pyoracle
+
+
+@pytest.fixture(scope="session")
+def naive_decode():
+    """The test-only lane-per-chunk Snappy decoder (tests/native/libnx_test_naive.so, built by
+    __graft_entry__.build()), with nx_snappy_decode_batch's contract: a cross-check of the product
+    decoder, never shipped in libnetty_amd.so."""
+    import ctypes as C
+    from netty_amd import _lib
+    _lib.load()  # libnetty_amd.so first (the test library links against it)
+    L = C.CDLL(os.path.join(ROOT, "tests", "native", "libnx_test_naive.so"))
+    f = L.nx_snappy_decode_batch_naive
+    f.restype = C.c_int32
+    f.argtypes = [C.c_void_p] * 11 + [C.c_uint32, C.c_void_p]
+    return f

@@ -2,9 +2,10 @@
 //
 // Executes Snappy.decode's state machine (Snappy.java:315-650) once per complete chunk, as
 // SnappyFrameDecoder drives it (SnappyFrameDecoder.java:194-224), one chunk per lane, output
-// straight to HBM.  Kept as the structural baseline and as a second GPU implementation the
-// optimized wave-cooperative decoder (snappy_decode.hip) is cross-checked against.
-#include "nx_common.hpp"
+// straight to HBM.  TEST-ONLY (tests/native/libnx_test_naive.so, not part of libnetty_amd.so): a
+// second GPU implementation the product decoder (snappy_decode.hip) is cross-checked against, with
+// nx_snappy_decode_batch's contract.
+#include "../../netty_amd/csrc/nx_common.hpp"
 
 namespace nx {
 

@@ -244,3 +244,103 @@ def test_batcher_rejected_encoder_submit_keeps_stream_identifier(nx, oracle):
     b.flush()
     b.wait(t)
     assert b.result(t) == [oracle.snappy_frame_encode(data)[0]]
+
+
+# ---- validating-mode leftovers (SnappyFrameDecoder.java:206-212): a compressed chunk that decodes fewer
+# bytes than its length leaves the rest in the cumulation, parsed again as the next chunk header
+STREAM_ID = b"\xff\x06\x00\x00sNaPpY"
+EMPTY_CRC = 0xA282EAD8  # mask(crc32c of no bytes)
+
+
+def _chunk(kind, payload, crc):
+    n = len(payload) + 4
+    return bytes([kind, n & 255, (n >> 8) & 255, n >> 16]) + crc.to_bytes(4, "little") + payload
+
+
+def leftover_streams(oracle):
+    """Streams whose compressed chunks hide further chunks in their unread tails, with the messages the
+    reference delivers (worked out from Snappy.decode, Snappy.java:315-393)."""
+    x = oracle.textgen_chunk(21, 3000)
+    y = oracle.textgen_chunk(22, 40)
+    z = oracle.textgen_chunk(23, 60000)
+    comp = lambda d: _chunk(0, oracle.snappy_encode(d), oracle.snappy_checksum(d))  # noqa: E731
+    unc = lambda d: _chunk(1, d, oracle.snappy_checksum(d))  # noqa: E731
+    # preamble 0: decode() returns at once (:324-327), one empty message, the rest is the next header
+    zero = lambda rest: _chunk(0, b"\x00" + rest, EMPTY_CRC)  # noqa: E731
+    # a 60-byte literal tag with fewer bytes behind it: NOT_ENOUGH_INPUT, the reader rewinds to just
+    # after the tag (decodeLiteral :454-494); the message is what was decoded before it
+    trunc = lambda d, rest: _chunk(0, oracle.snappy_encode(d) + bytes([59 << 2]) + rest, oracle.snappy_checksum(d))  # noqa: E731
+    tail = comp(z)
+    # (stream, messages when validating, messages without validation: readSlice drops the tail, :215)
+    return [
+        (STREAM_ID + zero(comp(x)) + tail, [b"", x, z], [b"", z]),
+        (STREAM_ID + zero(zero(unc(y))) + comp(y) + tail, [b"", b"", y, y, z], [b"", y, z]),
+        (STREAM_ID + trunc(x, unc(y)) + tail, [x, y, z], [x, z]),
+        (STREAM_ID + comp(y) + trunc(y, zero(b"")) + zero(b"") + tail, [y, y, b"", b"", z], [y, y, b"", z]),
+    ]
+
+
+def test_sync_decoder_validating_leftover(nx, oracle):
+    """The synchronous handle re-parses a leftover as the next chunk header, as the reference does."""
+    for stream, want, plain in leftover_streams(oracle):
+        d = nx.SnappyFrameDecoder(True)
+        assert d.channel_read(stream) == want
+        assert d.readable_bytes() == 0
+        assert nx.SnappyFrameDecoder(False).channel_read(stream) == plain
+
+
+@pytest.mark.parametrize("reads", [1, 3, 7])
+@pytest.mark.parametrize("flush_every", [0, 1, 2])
+def test_batcher_validating_leftover_equals_sync(nx, oracle, reads, flush_every):
+    """The batcher re-walks a validating decoder's stream from the leftover at apply() time: over any
+    split of the stream into reads and any flush pattern, every channel receives the synchronous
+    decoder's messages in the same order (possibly on an earlier ticket)."""
+    rng = random.Random(reads * 10 + flush_every)
+    streams = leftover_streams(oracle)
+    b = nx.Batcher()
+    chans = []
+    for stream, want, _ in streams * 2:
+        cuts = sorted(rng.randrange(0, len(stream) + 1) for _ in range(reads - 1))
+        parts = [stream[a:c] for a, c in zip([0] + cuts, cuts + [len(stream)])]
+        chans.append((nx.SnappyFrameDecoder(True), parts, want, []))
+    for r in range(reads):
+        for d, parts, _, tickets in chans:
+            tickets.append(b.submit_decode(d, parts[r]))
+        if flush_every and r % flush_every == 0:
+            b.flush()
+    b.flush()
+    for d, parts, want, tickets in chans:
+        got = []
+        for t in tickets:
+            b.wait(t)
+            got += b.result(t)
+        assert got == want
+        s = nx.SnappyFrameDecoder(True)
+        sync = []
+        for p in parts:
+            sync += s.channel_read(p)
+        assert sync == want
+
+
+def test_batcher_validating_leftover_then_error(nx, oracle):
+    """A header error inside a leftover fails the continuing job with the reference message, after its
+    earlier messages; later input on the decoder is skipped (:86-89)."""
+    x = oracle.textgen_chunk(31, 500)
+    bad = bytes([0x02, 0x01, 0x00, 0x00, 0x00])
+    stream = STREAM_ID + _chunk(0, oracle.snappy_encode(x), oracle.snappy_checksum(x)) + _chunk(0, b"\x00" + bad, EMPTY_CRC)
+    later = _chunk(1, b"abcd", oracle.snappy_checksum(b"abcd"))
+    b = nx.Batcher()
+    d = nx.SnappyFrameDecoder(True)
+    t1 = b.submit_decode(d, stream)
+    t2 = b.submit_decode(d, later)
+    b.flush()
+    b.wait(t1)
+    b.wait(t2)
+    with pytest.raises(nx.DecompressionException, match="Found reserved unskippable chunk type: 0x2") as ei:
+        b.result(t1)
+    assert ei.value.decoded == [x, b""]
+    assert b.result(t2) == []
+    s = nx.SnappyFrameDecoder(True)
+    with pytest.raises(nx.DecompressionException, match="Found reserved unskippable chunk type: 0x2") as ei:
+        s.channel_read(stream)
+    assert ei.value.decoded == [x, b""]

@@ -68,13 +68,14 @@ def test_snappy_encode_parity(dev, B, oracle, kat, in_align, out_align):
 
 
 @pytest.mark.parametrize("variant,align", [("auto", 16), ("auto", 1), ("fused", 16), ("fused", 1), ("naive", 16)])
-def test_snappy_decode_parity(dev, B, oracle, kat, variant, align):
+def test_snappy_decode_parity(dev, B, oracle, kat, naive_decode, variant, align):
     chunks = _corpus(oracle, kat)
     enc = [oracle.snappy_encode(c) for c in chunks]
     inp, off, ln = B.pack(enc, dev, align=align)
     out, ooff = B.out_slots([65536] * len(enc), dev)
     crcs = torch.tensor([oracle.snappy_checksum(c) for c in chunks], dtype=torch.int64).to(torch.int32).to(dev)
-    r = B.snappy_decode(inp, off, ln, out, ooff, expected_crc=crcs, want_crc=True, consumed=True, variant=variant)
+    r = B.snappy_decode(inp, off, ln, out, ooff, expected_crc=crcs, want_crc=True, consumed=True,
+                        variant="auto" if variant == "naive" else variant, fn=naive_decode if variant == "naive" else None)
     torch.cuda.synchronize()
     st, olen, cons = r["status"].cpu().tolist(), r["out_len"].cpu().tolist(), r["consumed"].cpu().tolist()
     crc = [x & 0xFFFFFFFF for x in r["crc"].cpu().tolist()]
@@ -112,11 +113,12 @@ def _crafted_streams(oracle, kat):
 
 
 @pytest.mark.parametrize("variant", ["auto", "fused", "naive"])
-def test_snappy_decode_edge_cases(dev, B, oracle, kat, variant):
+def test_snappy_decode_edge_cases(dev, B, oracle, kat, naive_decode, variant):
     cases = _crafted_streams(oracle, kat)
     inp, off, ln = B.pack(cases, dev)
     out, ooff = B.out_slots([65536] * len(cases), dev)
-    r = B.snappy_decode(inp, off, ln, out, ooff, consumed=True, variant=variant)
+    r = B.snappy_decode(inp, off, ln, out, ooff, consumed=True, variant="auto" if variant == "naive" else variant,
+                        fn=naive_decode if variant == "naive" else None)
     torch.cuda.synchronize()
     st, olen, cons = r["status"].cpu().tolist(), r["out_len"].cpu().tolist(), r["consumed"].cpu().tolist()
     outh, ooff_h = out.cpu().numpy().tobytes(), ooff.cpu().tolist()
