@@ -9,6 +9,7 @@
 // The readU16 quirk (FastLz.java:552-557: an ABSOLUTE index compared against readableBytes())
 // is reproduced through the per-chunk u16_limit = readableBytes() - inOffset of the Java call.
 #include "nx_common.hpp"
+#include "records.hpp"
 
 namespace nx {
 namespace flz {
@@ -338,20 +339,25 @@ __global__ void __launch_bounds__(256) k_compress(const uint8_t* __restrict__ in
     }
 }
 
-__global__ void __launch_bounds__(256) k_decompress(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                                                    const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ in_avail,
-                                                    uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
-                                                    const uint32_t* __restrict__ out_lim, int32_t* __restrict__ result, uint32_t n) {
+// After the record path (records.hpp): blocks it left with kNeedSerial run the lane-serial decoder
+// (Java's return value or status); the others return the length the parse produced.
+__global__ void __launch_bounds__(256) k_decompress_finish(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                           const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ in_avail,
+                                                           uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                                           const uint32_t* __restrict__ out_lim, int32_t* __restrict__ result,
+                                                           const uint32_t* __restrict__ olen, uint32_t n) {
     // output through 64-byte LDS units (nx_common.hpp ByteStageT; 17 KiB per block keeps 8 blocks/CU)
     __shared__ __attribute__((aligned(16))) uint8_t stages[256 * 68];
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t nthreads = gridDim.x * blockDim.x;
-    for (uint32_t c = tid; c < n; c += nthreads) {
-        const uint32_t il = in_len[c];
-        const uint32_t av = in_avail ? in_avail[c] : il;
-        ByteStageT<64> o(&stages[threadIdx.x * 68], out + out_off[c]);
-        result[c] = decompress(in + in_off[c], (int32_t)il, (int32_t)av, o, (int32_t)out_lim[c]);
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    if (result[c] != nx::dec::kNeedSerial) {
+        result[c] = (int32_t)olen[c];
+        return;
     }
+    const uint32_t il = in_len[c];
+    const uint32_t av = in_avail ? in_avail[c] : il;
+    ByteStageT<64> o(&stages[threadIdx.x * 68], out + out_off[c]);
+    result[c] = decompress(in + in_off[c], (int32_t)il, (int32_t)av, o, (int32_t)out_lim[c]);
 }
 
 // Adler32 (java.util.zip.Adler32): one wave per chunk, lanes take 16-byte slots of 1 KiB blocks.
@@ -455,17 +461,35 @@ extern "C" int32_t nx_fastlz_compress_batch(const uint8_t* in, const uint64_t* i
     return NX_OK;
 }
 
+namespace {
+struct FlzDecCtx {
+    const uint8_t* in;
+    const uint64_t* in_off;
+    const uint32_t* in_len;
+    const uint32_t* in_avail;
+    uint8_t* out;
+    const uint64_t* out_off;
+    const uint32_t* lim;
+    int32_t* result;
+};
+hipError_t flz_dec_after(uint32_t base, uint32_t m, const uint32_t* olen, void* ctx, hipStream_t st) {
+    const FlzDecCtx& x = *static_cast<const FlzDecCtx*>(ctx);
+    hipLaunchKernelGGL(nx::flz::k_decompress_finish, dim3((m + 255) / 256), dim3(256), 0, st, x.in, x.in_off + base, x.in_len + base,
+                       x.in_avail ? x.in_avail + base : nullptr, x.out, x.out_off + base, x.lim + base, x.result + base, olen, m);
+    return hipGetLastError();
+}
+}  // namespace
+
+// Blocks go through the record expander (snappy_decode.hip k_parse_fastlz + k_expand); the few it
+// does not take (malformed, reads past the block) through the lane-serial decompress().
 extern "C" int32_t nx_fastlz_decompress_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                               const uint32_t* in_avail, uint8_t* out, const uint64_t* out_off,
                                               const uint32_t* out_len_limit, int32_t* result, uint32_t n, void* stream) {
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len_limit || !result) return NX_ERR_INVALID_ARG;
-    unsigned grid = (n + 255) / 256;
-    if (grid > 8192) grid = 8192;
-    hipLaunchKernelGGL(nx::flz::k_decompress, dim3(grid), dim3(256), 0, (hipStream_t)stream, in, in_off, in_len, in_avail, out,
-                       out_off, out_len_limit, result, n);
-    NX_HIP_CHECK(hipGetLastError());
-    return NX_OK;
+    FlzDecCtx ctx{in, in_off, in_len, in_avail, out, out_off, out_len_limit, result};
+    return nx::dec::decode_records(nx::dec::RecCodec::FastLz, in, in_off, in_len, in_avail, out_len_limit, out, out_off, result, n,
+                                   (hipStream_t)stream, flz_dec_after, &ctx);
 }
 
 extern "C" int32_t nx_adler32_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t* out, uint32_t n,

@@ -429,7 +429,7 @@ struct nx_fastlz_frame_decoder {
 
 extern "C" nx_fastlz_frame_decoder* nx_fastlz_frame_decoder_new(int32_t validate) {
     auto* d = new nx_fastlz_frame_decoder();
-    if (!d->g.ok) {
+    if (!d->g.hold(nx::WsKind::DecRecords)) {  // FastLZ blocks decode through the record expander
         delete d;
         return nullptr;
     }
@@ -730,7 +730,7 @@ struct nx_lzf_decoder {
 };
 extern "C" nx_lzf_decoder* nx_lzf_decoder_new(void) {
     auto* d = new nx_lzf_decoder();
-    if (!d->g.ok) {
+    if (!d->g.hold(nx::WsKind::DecRecords)) {  // LZF blocks decode through the record expander
         delete d;
         return nullptr;
     }

@@ -9,6 +9,7 @@
 // of bytes [p-1, p+2], 3-byte candidate check, MAX_OFF 8192, MAX_REF 264, matchEnd-2/-1 inserts —
 // byte for byte (PARITY UNPINNED vs the library itself: no reference bytes exist offline).
 #include "nx_common.hpp"
+#include "records.hpp"
 
 namespace nx {
 namespace lzf {
@@ -191,18 +192,18 @@ __global__ void __launch_bounds__(256) k_encode(const uint8_t* __restrict__ in, 
     }
 }
 
-__global__ void __launch_bounds__(256) k_decode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                                                const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
-                                                const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_len,
-                                                int32_t* __restrict__ status, uint32_t n) {
+// After the record path (records.hpp): blocks it left with kNeedSerial run the lane-serial decoder,
+// which reports the status; the others decoded exactly out_len bytes (NX_OK, already set).
+__global__ void __launch_bounds__(256) k_decode_finish(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                       const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                       const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_len,
+                                                       int32_t* __restrict__ status, uint32_t n) {
     // output through 64-byte LDS units (nx_common.hpp ByteStageT; 17 KiB per block keeps 8 blocks/CU)
     __shared__ __attribute__((aligned(16))) uint8_t stages[256 * 68];
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t nthreads = gridDim.x * blockDim.x;
-    for (uint32_t c = tid; c < n; c += nthreads) {
-        ByteStageT<64> o(&stages[threadIdx.x * 68], out + out_off[c]);
-        status[c] = decode_chunk(in + in_off[c], (int32_t)in_len[c], o, (int32_t)out_len[c]);
-    }
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n || status[c] != nx::dec::kNeedSerial) return;
+    ByteStageT<64> o(&stages[threadIdx.x * 68], out + out_off[c]);
+    status[c] = decode_chunk(in + in_off[c], (int32_t)in_len[c], o, (int32_t)out_len[c]);
 }
 
 }  // namespace lzf
@@ -243,15 +244,32 @@ extern "C" int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off
     return NX_OK;
 }
 
+namespace {
+struct LzfDecCtx {
+    const uint8_t* in;
+    const uint64_t* in_off;
+    const uint32_t* in_len;
+    uint8_t* out;
+    const uint64_t* out_off;
+    const uint32_t* out_len;
+    int32_t* status;
+};
+hipError_t lzf_dec_after(uint32_t base, uint32_t m, const uint32_t*, void* ctx, hipStream_t st) {
+    const LzfDecCtx& x = *static_cast<const LzfDecCtx*>(ctx);
+    hipLaunchKernelGGL(nx::lzf::k_decode_finish, dim3((m + 255) / 256), dim3(256), 0, st, x.in, x.in_off + base, x.in_len + base, x.out,
+                       x.out_off + base, x.out_len + base, x.status + base, m);
+    return hipGetLastError();
+}
+}  // namespace
+
+// Blocks go through the record expander (snappy_decode.hip k_parse_lzf + k_expand); corrupt ones
+// through the lane-serial decode_chunk(), which reports them.
 extern "C" int32_t nx_lzf_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                        const uint64_t* out_off, const uint32_t* out_len, int32_t* status, uint32_t n,
                                        void* stream) {
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
-    unsigned grid = (n + 255) / 256;
-    if (grid > 8192) grid = 8192;
-    hipLaunchKernelGGL(nx::lzf::k_decode, dim3(grid), dim3(256), 0, (hipStream_t)stream, in, in_off, in_len, out, out_off, out_len,
-                       status, n);
-    NX_HIP_CHECK(hipGetLastError());
-    return NX_OK;
+    LzfDecCtx ctx{in, in_off, in_len, out, out_off, out_len, status};
+    return nx::dec::decode_records(nx::dec::RecCodec::Lzf, in, in_off, in_len, nullptr, out_len, out, out_off, status, n,
+                                   (hipStream_t)stream, lzf_dec_after, &ctx);
 }

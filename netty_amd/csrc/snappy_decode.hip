@@ -46,6 +46,7 @@
 #include <mutex>
 #include "nx_common.hpp"
 #include "workspace.hpp"
+#include "records.hpp"
 
 namespace nx {
 namespace dec {
@@ -1117,6 +1118,186 @@ __global__ void __launch_bounds__(256) k_lz4_serial(const uint8_t* __restrict__ 
     status[c] = st;
 }
 
+// =====================================================================================
+// FastLZ and LZF blocks through the same record expander (configs[3]; records.hpp)
+// =====================================================================================
+// A copy of `len` bytes at distance `dist` splits into 64-byte records exactly (its bytes repeat at
+// the distance); a literal run of FastLZ / LZF is at most 32 bytes, one record.
+__device__ __forceinline__ bool put_copy(RecWriter& rw, uint32_t len, uint32_t dist) {
+    bool fit = true;
+    for (uint32_t k = 0; k < len && fit; k += 64u) {
+        const uint32_t m = len - k < 64u ? len - k : 64u;
+        fit = rw.put(0x80000000u | ((m - 1u) << 25) | dist);
+    }
+    return fit;
+}
+
+// FastLz.decompress (FastLz.java:409-543; the lane-serial form is fastlz.hip decompress()).  Block
+// byte 0 carries the level (bits 7..5) and the first literal-run control (bits 4..0); then runs of
+// ctrl+1 literal bytes (ctrl < 32) and back-references of (ctrl >> 5) + 2 (+ extension bytes) bytes
+// at distance ((ctrl & 31) << 8) + code + 1, level 2 with a 16-bit far distance (+ MAX_DISTANCE)
+// after a 255 code.  Every check of the Java method that can fail sends the block to the serial path
+// (kNeedSerial), as does any read at or past in_len (Java reads those through readU16-era indices
+// up to the array's readable bytes, fastlz.hip FIN).
+__global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                              const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ avail_a,
+                                                              const uint32_t* __restrict__ lim_a, uint32_t* __restrict__ rec,
+                                                              uint32_t* __restrict__ nrec, uint32_t* __restrict__ out_len,
+                                                              int32_t* __restrict__ status, uint32_t n) {
+    __shared__ uint32_t wins[kParseBlock * kWinDw + 4];
+    __shared__ __attribute__((aligned(16))) uint32_t recq[kParseBlock * kQDw];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint32_t in_len = in_len_a[c];
+    const uint32_t lim = lim_a[c];
+    // record fields, and a block whose readable bytes end inside it (in_avail): the serial path decides
+    if (in_len < 1u || in_len >= (1u << 24) || lim >= (1u << 24) || (avail_a && avail_a[c] < in_len)) {
+        status[c] = kNeedSerial;
+        return;
+    }
+    BurstWin win;
+    win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
+    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
+    const uint32_t b0 = win_byte(win, 0);
+    const uint32_t level = (b0 >> 5) + 1u;  // (in[0] >> 5) + 1 on the signed byte: 5..8 for b0 >= 0x80
+    bool ok = level == 1u || level == 2u;
+    uint32_t ip = 1, op = 0, ctrl = b0 & 31u;
+    bool loop = ok;
+    while (loop) {
+        if (ctrl >= 32u) {
+            uint32_t len = (ctrl >> 5) - 1u;
+            const uint32_t ofs = (ctrl & 31u) << 8;
+            uint32_t dist;  // op - ref + 1 of the Java loop
+            if (len == 6u) {
+                uint32_t code = 255u;
+                do {
+                    if (ip >= in_len) {
+                        ok = false;
+                        break;
+                    }
+                    code = win_byte(win, ip++);
+                    len += code;
+                } while (level == 2u && code == 255u);
+                if (!ok) break;
+            }
+            if (ip >= in_len) {
+                ok = false;
+                break;
+            }
+            const uint32_t code = win_byte(win, ip++);
+            dist = ofs + code + 1u;
+            if (level == 2u && code == 255u && ofs == (31u << 8)) {
+                if (ip + 1u >= in_len) {
+                    ok = false;
+                    break;
+                }
+                dist = ((win_byte(win, ip) << 8) | win_byte(win, ip + 1u)) + 8191u + 1u;  // MAX_DISTANCE
+                ip += 2u;
+            }
+            // Java: op + len + 3 > outLength -> 0; ref - 1 < 0 -> 0 (ref = op - dist + 1)
+            if (op + len + 3u > lim || dist > op) {
+                ok = false;
+                break;
+            }
+            if (ip < in_len) ctrl = win_byte(win, ip++);
+            else loop = false;
+            if (!put_copy(rw, len + 3u, dist)) {
+                ok = false;
+                break;
+            }
+            op += len + 3u;
+        } else {
+            const uint32_t k = ctrl + 1u;
+            if (op + k > lim || ip + k > in_len || !rw.put(((k - 1u) << 25) | ip)) {
+                ok = false;
+                break;
+            }
+            ip += k;
+            op += k;
+            loop = ip < in_len;
+            if (loop) ctrl = win_byte(win, ip++);
+        }
+    }
+    if (!ok) {
+        status[c] = kNeedSerial;
+        return;
+    }
+    rw.finish();
+    nrec[c] = rw.n;
+    out_len[c] = op;
+    status[c] = NX_OK;
+}
+
+// ChunkDecoder.decodeChunk (compress-lzf 1.0.3, as LzfDecoder.java:205 calls it; lane-serial form:
+// lzf.hip decode_chunk): runs of ctrl+1 literal bytes (ctrl < 32) and back-references of
+// (ctrl >> 5) + 2 (+ an extension byte when the length field is 7) bytes at distance
+// ((ctrl & 31) << 8) + next byte + 1, until exactly lim bytes are produced.  Any corrupt block goes to
+// the serial path (kNeedSerial), which reports it.
+__global__ void __launch_bounds__(kParseBlock) k_parse_lzf(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                           const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ lim_a,
+                                                           uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
+                                                           uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t n) {
+    __shared__ uint32_t wins[kParseBlock * kWinDw + 4];
+    __shared__ __attribute__((aligned(16))) uint32_t recq[kParseBlock * kQDw];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint32_t in_len = in_len_a[c];
+    const uint32_t lim = lim_a[c];
+    if (in_len >= (1u << 24) || lim >= (1u << 24)) {
+        status[c] = kNeedSerial;
+        return;
+    }
+    BurstWin win;
+    win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
+    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
+    uint32_t ip = 0, op = 0;
+    bool ok = true;
+    do {
+        if (ip >= in_len) {
+            ok = false;
+            break;
+        }
+        const uint32_t ctrl = win_byte(win, ip++);
+        if (ctrl < 32u) {
+            const uint32_t k = ctrl + 1u;
+            if (ip + k > in_len || op + k > lim || !rw.put(((k - 1u) << 25) | ip)) {
+                ok = false;
+                break;
+            }
+            ip += k;
+            op += k;
+            continue;
+        }
+        uint32_t len = ctrl >> 5;
+        if (len == 7u) {
+            if (ip >= in_len) {
+                ok = false;
+                break;
+            }
+            len += win_byte(win, ip++);
+        }
+        if (ip >= in_len) {
+            ok = false;
+            break;
+        }
+        const uint32_t dist = ((ctrl & 31u) << 8) + win_byte(win, ip++) + 1u;
+        len += 2u;
+        if (dist > op || op + len > lim || !put_copy(rw, len, dist)) {
+            ok = false;
+            break;
+        }
+        op += len;
+    } while (op < lim);
+    if (!ok) {
+        status[c] = kNeedSerial;
+        return;
+    }
+    rw.finish();
+    nrec[c] = rw.n;
+    out_len[c] = op;
+    status[c] = NX_OK;
+}
+
 }  // namespace dec
 }  // namespace nx
 
@@ -1262,6 +1443,42 @@ extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off
         hipLaunchKernelGGL(k_lz4_serial, dim3((m + 255) / 256), dim3(256), 0, st, in, in_off + base, in_len + base, out_len + base,
                            out, out_off + base, status + base, m);
         NX_HIP_CHECK(hipGetLastError());
+    }
+    return NX_OK;
+}
+
+// FastLZ / LZF blocks: codec parse -> k_expand -> the codec's finish kernel (records.hpp).
+int32_t nx::dec::decode_records(RecCodec codec, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* avail,
+                                const uint32_t* lim,
+                                uint8_t* out, const uint64_t* out_off, int32_t* status, uint32_t n, hipStream_t st, RecAfter after,
+                                void* ctx) {
+    static_assert(kNeedSerial == kNeedFused, "one marker for the serial fallback");
+    if (n == 0) return NX_OK;
+    if (nx::crc_tables_init() != NX_OK) return NX_ERR_HIP;
+    int dev = 0, cus = 256;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const size_t lds = kTabBytes + kWaves * sizeof(WaveLds);
+    NX_HIP_CHECK(wave_kernel_attrs(lds));
+    unsigned blocks_per_cu = (unsigned)(160 * 1024 / lds);
+    if (blocks_per_cu < 1) blocks_per_cu = 1;
+    nx::WsLease lease(nx::WsKind::DecRecords, dev, st);
+    NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::DecRecords, n, cus)));
+    const DecSlots W = dec_slots(lease.ws());
+    const uint32_t sb = n < W.frames ? n : W.frames;
+    for (uint32_t base = 0; base < n; base += sb) {
+        const uint32_t m = n - base < sb ? n - base : sb;
+        const dim3 pg((m + kParseBlock - 1) / kParseBlock), pb(kParseBlock);
+        if (codec == RecCodec::FastLz)
+            hipLaunchKernelGGL(k_parse_fastlz, pg, pb, 0, st, in, in_off + base, in_len + base, avail ? avail + base : nullptr,
+                               lim + base, W.rec, W.nrec, W.olen, status + base, m);
+        else
+            hipLaunchKernelGGL(k_parse_lzf, pg, pb, 0, st, in, in_off + base, in_len + base, lim + base, W.rec, W.nrec, W.olen,
+                               status + base, m);
+        NX_HIP_CHECK(hipGetLastError());
+        NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W.rec, W.nrec, W.olen, status + base, nullptr,
+                                   nullptr, m, cus, lds, blocks_per_cu, st));
+        NX_HIP_CHECK(after(base, m, W.olen, ctx, st));
     }
     return NX_OK;
 }

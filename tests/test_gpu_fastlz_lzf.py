@@ -111,3 +111,76 @@ def test_lzf_encode_decode_parity(dev, B, oracle):
         assert st2[k] == 0
         assert h2[oo2[k]:oo2[k] + ulens[k]] == chunks[i]
     assert st2[-1] == -30
+
+
+def _fastlz_many_matches(level, n_matches):
+    """A level-1/2 block of one literal then n_matches 3-byte back-references at distance 1: more
+    records than a record slot holds (16384), so the record path hands it to the lane-serial kernel."""
+    return bytes([(level - 1) << 5, ord("a")]) + bytes([1 << 5, 0]) * n_matches
+
+
+def test_fastlz_decompress_record_path_edges(dev, B, oracle):
+    """Blocks the record expander takes and the ones it leaves to the lane-serial kernel (malformed,
+    truncated at many points, more records than a slot, reads past the block): results and bytes equal
+    FastLz.decompress's (FastLz.java:409-543) as the oracle restates it."""
+    chunks = _mixed(oracle, 16, 11)
+    blocks, lims = [], []
+    for i, c in enumerate(chunks):
+        lv = 1 + (i % 2)
+        z = oracle.fastlz_compress(c, lv)
+        blocks.append(z)
+        lims.append(len(c))
+        for cut in range(1, len(z), max(len(z) // 7, 1)):  # truncated blocks
+            blocks.append(z[:cut])
+            lims.append(len(c))
+        blocks.append(z)  # output limit one byte short
+        lims.append(max(len(c) - 1, 0))
+    for lv in (1, 2):
+        blocks.append(_fastlz_many_matches(lv, 21000))
+        lims.append(1 + 3 * 21000)
+        blocks.append(_fastlz_many_matches(lv, 5000))  # within a slot
+        lims.append(1 + 3 * 5000)
+    blocks.append(bytes([0x00, 0x41, 0x20, 0x05]))  # distance beyond the output
+    lims.append(64)
+    blocks.append(bytes([0x40]))  # bad level
+    lims.append(8)
+    inp, off, ln = B.pack(blocks, dev)
+    out, ooff = B.out_slots([max(x, 1) for x in lims], dev)
+    lim = torch.tensor(lims, dtype=torch.int32, device=dev)
+    res = B.fastlz_decompress(inp, off, ln, out, ooff, lim).cpu().tolist()
+    h, oo = out.cpu().numpy().tobytes(), ooff.cpu().tolist()
+    for i, z in enumerate(blocks):
+        wr, wout = oracle.fastlz_decompress(z, lims[i])
+        assert res[i] == wr, (i, len(z), lims[i], res[i], wr)
+        if wr > 0:
+            assert h[oo[i]:oo[i] + wr] == wout, i
+
+
+def test_lzf_decode_record_path_edges(dev, B, oracle):
+    """LZF bodies through the record expander and the serial fallback: corrupt and truncated bodies
+    report NX_ERR_LZF_CORRUPT, more-records-than-a-slot bodies decode through the serial kernel."""
+    chunks = _mixed(oracle, 16, 13)
+    bodies, ulens = [], []
+    for c in chunks:
+        if len(c) < 16:
+            continue
+        body = oracle.lzf_compress_body(c)
+        bodies.append(body)
+        ulens.append(len(c))
+        for cut in range(1, len(body), max(len(body) // 5, 1)):
+            bodies.append(body[:cut])
+            ulens.append(len(c))
+    many = bytes([0, ord("a")]) + bytes([0x20, 0]) * 21000  # 21001 records: the serial path
+    bodies.append(many)
+    ulens.append(1 + 3 * 21000)
+    inp, off, ln = B.pack(bodies, dev)
+    out, ooff = B.out_slots(ulens, dev)
+    ul = torch.tensor(ulens, dtype=torch.int32, device=dev)
+    st = B.lzf_decode(inp, off, ln, out, ooff, ul).cpu().tolist()
+    h, oo = out.cpu().numpy().tobytes(), ooff.cpu().tolist()
+    for k, body in enumerate(bodies):
+        wst, wout = oracle.lzf_decode_chunk(body, ulens[k])
+        assert st[k] == wst, (k, st[k], wst)
+        if wst == 0:
+            assert h[oo[k]:oo[k] + ulens[k]] == wout, k
+    assert st[-1] == 0 and h[oo[-1]:oo[-1] + 4] == b"aaaa"
