@@ -1137,8 +1137,14 @@ __device__ __forceinline__ bool put_copy(RecWriter& rw, uint32_t len, uint32_t d
 // ctrl+1 literal bytes (ctrl < 32) and back-references of (ctrl >> 5) + 2 (+ extension bytes) bytes
 // at distance ((ctrl & 31) << 8) + code + 1, level 2 with a 16-bit far distance (+ MAX_DISTANCE)
 // after a 255 code.  Every check of the Java method that can fail sends the block to the serial path
-// (kNeedSerial), as does any read at or past in_len (Java reads those through readU16-era indices
-// up to the array's readable bytes, fastlz.hip FIN).
+// (kNeedSerial), as does any read at or past in_len (Java reads those through the array's readable
+// bytes, fastlz.hip FIN).
+//
+// Burst form, as k_parse: the lanes whose next control byte is not in their LDS window reload it
+// together (one wait for the wave), then each lane decodes tokens from an 8-byte register view of
+// its window until it runs out.  A token's header is at most 5 bytes (control, length extension,
+// code, two far-distance bytes), inside what BurstWin::has guarantees; only a level-2 length
+// extension that continues past a 255 byte takes the byte-at-a-time slow path.
 __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                               const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ avail_a,
                                                               const uint32_t* __restrict__ lim_a, uint32_t* __restrict__ rec,
@@ -1158,65 +1164,87 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
     BurstWin win;
     win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
     RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
-    const uint32_t b0 = win_byte(win, 0);
+    win.load(0);
+    const uint32_t b0 = (uint32_t)win.get8(0) & 0xFFu;
     const uint32_t level = (b0 >> 5) + 1u;  // (in[0] >> 5) + 1 on the signed byte: 5..8 for b0 >= 0x80
-    bool ok = level == 1u || level == 2u;
-    uint32_t ip = 1, op = 0, ctrl = b0 & 31u;
-    bool loop = ok;
-    while (loop) {
-        if (ctrl >= 32u) {
-            uint32_t len = (ctrl >> 5) - 1u;
-            const uint32_t ofs = (ctrl & 31u) << 8;
-            uint32_t dist;  // op - ref + 1 of the Java loop
-            if (len == 6u) {
-                uint32_t code = 255u;
-                do {
-                    if (ip >= in_len) {
-                        ok = false;
-                        break;
-                    }
-                    code = win_byte(win, ip++);
-                    len += code;
-                } while (level == 2u && code == 255u);
-                if (!ok) break;
-            }
-            if (ip >= in_len) {
-                ok = false;
-                break;
-            }
-            const uint32_t code = win_byte(win, ip++);
-            dist = ofs + code + 1u;
-            if (level == 2u && code == 255u && ofs == (31u << 8)) {
-                if (ip + 1u >= in_len) {
+    const uint32_t k0 = (b0 & 31u) + 1u;    // the first literal run
+    bool ok = (level == 1u || level == 2u) && k0 <= lim && 1u + k0 <= in_len && rw.put(((k0 - 1u) << 25) | 1u);
+    uint32_t ip = 1u + k0, op = k0;  // ip: the next control byte
+    bool run = ok && ip < in_len;
+    for (;;) {
+        if (!__any(run)) break;
+        if (run && !win.has(ip)) win.load(ip);  // burst reload: one wait for the whole wave
+        while (run && win.has(ip)) {
+            const uint64_t v = win.get8(ip);
+            const uint32_t ctrl = (uint32_t)v & 0xFFu;
+            uint32_t adv, len, dist;
+            bool put_ok;
+            if (ctrl < 32u) {  // literal run
+                const uint32_t k = ctrl + 1u;
+                if (op + k > lim || ip + 1u + k > in_len) {
                     ok = false;
                     break;
                 }
-                dist = ((win_byte(win, ip) << 8) | win_byte(win, ip + 1u)) + 8191u + 1u;  // MAX_DISTANCE
-                ip += 2u;
+                put_ok = rw.put(((k - 1u) << 25) | (ip + 1u));
+                adv = 1u + k;
+                len = k;
+            } else {
+                len = (ctrl >> 5) - 1u;
+                const uint32_t ofs = (ctrl & 31u) << 8;
+                uint32_t p = 1u;  // header bytes used so far
+                if (len == 6u && level == 2u && ((uint32_t)(v >> 8) & 0xFFu) == 255u) {
+                    // slow path: a level-2 extension run of 255s (matches of 264+ bytes)
+                    uint32_t code = 255u;
+                    while (code == 255u) {
+                        if (ip + p >= in_len) break;
+                        code = win_byte(win, ip + p);
+                        ++p;
+                        len += code;
+                    }
+                    if (code == 255u || ip + p + 2u >= in_len + 0u) {
+                        // ran off the block (or too close to its end for the code/far bytes): serial
+                        ok = false;
+                        break;
+                    }
+                    const uint32_t cd = win_byte(win, ip + p);
+                    ++p;
+                    dist = ofs + cd + 1u;
+                    if (cd == 255u && ofs == (31u << 8)) {
+                        dist = ((win_byte(win, ip + p) << 8) | win_byte(win, ip + p + 1u)) + 8192u;  // + MAX_DISTANCE + 1
+                        p += 2u;
+                    }
+                } else {
+                    if (len == 6u) {
+                        len += (uint32_t)(v >> 8) & 0xFFu;
+                        p = 2u;
+                    }
+                    const uint32_t code = (uint32_t)(v >> (8u * p)) & 0xFFu;
+                    ++p;
+                    dist = ofs + code + 1u;
+                    if (level == 2u && code == 255u && ofs == (31u << 8)) {
+                        const uint32_t hi = (uint32_t)(v >> (8u * p)) & 0xFFu, lo = (uint32_t)(v >> (8u * p + 8u)) & 0xFFu;
+                        dist = ((hi << 8) | lo) + 8192u;  // + MAX_DISTANCE + 1
+                        p += 2u;
+                    }
+                }
+                // every header byte inside the block; Java: op + len + 3 > outLength -> 0, ref - 1 < 0 -> 0
+                if (ip + p > in_len || op + len + 3u > lim || dist > op) {
+                    ok = false;
+                    break;
+                }
+                len += 3u;
+                put_ok = put_copy(rw, len, dist);
+                adv = p;
             }
-            // Java: op + len + 3 > outLength -> 0; ref - 1 < 0 -> 0 (ref = op - dist + 1)
-            if (op + len + 3u > lim || dist > op) {
+            if (!put_ok) {
                 ok = false;
                 break;
             }
-            if (ip < in_len) ctrl = win_byte(win, ip++);
-            else loop = false;
-            if (!put_copy(rw, len + 3u, dist)) {
-                ok = false;
-                break;
-            }
-            op += len + 3u;
-        } else {
-            const uint32_t k = ctrl + 1u;
-            if (op + k > lim || ip + k > in_len || !rw.put(((k - 1u) << 25) | ip)) {
-                ok = false;
-                break;
-            }
-            ip += k;
-            op += k;
-            loop = ip < in_len;
-            if (loop) ctrl = win_byte(win, ip++);
+            ip += adv;
+            op += len;
+            run = ip < in_len;  // Java: a control byte follows while ip < inLength
         }
+        if (!ok) run = false;
     }
     if (!ok) {
         status[c] = kNeedSerial;
@@ -1232,7 +1260,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
 // lzf.hip decode_chunk): runs of ctrl+1 literal bytes (ctrl < 32) and back-references of
 // (ctrl >> 5) + 2 (+ an extension byte when the length field is 7) bytes at distance
 // ((ctrl & 31) << 8) + next byte + 1, until exactly lim bytes are produced.  Any corrupt block goes to
-// the serial path (kNeedSerial), which reports it.
+// the serial path (kNeedSerial), which reports it.  Burst form as k_parse_fastlz (headers <= 3 bytes).
 __global__ void __launch_bounds__(kParseBlock) k_parse_lzf(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                            const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ lim_a,
                                                            uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
@@ -1243,7 +1271,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lzf(const uint8_t* __rest
     if (c >= n) return;
     const uint32_t in_len = in_len_a[c];
     const uint32_t lim = lim_a[c];
-    if (in_len >= (1u << 24) || lim >= (1u << 24)) {
+    if (in_len == 0u || lim == 0u || in_len >= (1u << 24) || lim >= (1u << 24)) {  // (lim 0 or no input: always corrupt)
         status[c] = kNeedSerial;
         return;
     }
@@ -1251,43 +1279,32 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lzf(const uint8_t* __rest
     win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
     RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
     uint32_t ip = 0, op = 0;
-    bool ok = true;
-    do {
-        if (ip >= in_len) {
-            ok = false;
-            break;
-        }
-        const uint32_t ctrl = win_byte(win, ip++);
-        if (ctrl < 32u) {
+    bool ok = true, run = true;  // run: op < lim, and the next control byte at ip < in_len
+    for (;;) {
+        if (!__any(run)) break;
+        if (run && !win.has(ip)) win.load(ip);
+        while (run && win.has(ip)) {
+            const uint64_t v = win.get8(ip);
+            const uint32_t ctrl = (uint32_t)v & 0xFFu, b1 = (uint32_t)(v >> 8) & 0xFFu, b2 = (uint32_t)(v >> 16) & 0xFFu;
+            const bool lit = ctrl < 32u;
+            const bool ext = (ctrl >> 5) == 7u;
             const uint32_t k = ctrl + 1u;
-            if (ip + k > in_len || op + k > lim || !rw.put(((k - 1u) << 25) | ip)) {
+            const uint32_t hdr = lit ? 1u : (ext ? 3u : 2u);
+            const uint32_t len = lit ? k : (ctrl >> 5) + (ext ? b1 : 0u) + 2u;
+            const uint32_t dist = ((ctrl & 31u) << 8) + (ext ? b2 : b1) + 1u;
+            const bool bad = lit ? (ip + 1u + k > in_len || op + k > lim) : (ip + hdr > in_len || dist > op || op + len > lim);
+            if (bad || !(lit ? rw.put(((k - 1u) << 25) | (ip + 1u)) : put_copy(rw, len, dist))) {
                 ok = false;
                 break;
             }
-            ip += k;
-            op += k;
-            continue;
+            ip += lit ? 1u + k : hdr;
+            op += len;
+            run = op < lim;
+            if (run && ip >= in_len) ok = false;  // more output wanted, no control byte left
+            run = run && ok;
         }
-        uint32_t len = ctrl >> 5;
-        if (len == 7u) {
-            if (ip >= in_len) {
-                ok = false;
-                break;
-            }
-            len += win_byte(win, ip++);
-        }
-        if (ip >= in_len) {
-            ok = false;
-            break;
-        }
-        const uint32_t dist = ((ctrl & 31u) << 8) + win_byte(win, ip++) + 1u;
-        len += 2u;
-        if (dist > op || op + len > lim || !put_copy(rw, len, dist)) {
-            ok = false;
-            break;
-        }
-        op += len;
-    } while (op < lim);
+        if (!ok) run = false;
+    }
     if (!ok) {
         status[c] = kNeedSerial;
         return;
