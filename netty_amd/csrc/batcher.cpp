@@ -263,6 +263,10 @@ struct Job {
     uint64_t s_base = 0, epoch = 0;
     bool walked = false;
     std::deque<std::vector<uint8_t>> owned;  // messages delivered before a re-walk moved the job to a later batch
+    Job() = default;
+    Job(const Job&) = delete;
+    Job& operator=(const Job&) = delete;
+    ~Job() { nx_decoder_unref(dec); }  // a decoder job holds a reference to its handle (handles.hpp)
 };
 
 struct Batch {
@@ -1041,14 +1045,17 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
     if (registered && walked && !carried) {
         dS = registered_device_ptr(in, walked);
         if (!dS) {  // not inside an nx_host_register'd range
+            j->dec = nullptr;
             delete j;
             return NX_ERR_INVALID_ARG;
         }
     }
     if (enqueue_dec(bt, j, S, walked, dS) != NX_OK) {
+        j->dec = nullptr;  // no reference taken yet
         delete j;
         return NX_ERR_HIP;
     }
+    d->refs.fetch_add(1);  // released with the job (~Job)
     *consumed = p;
     if (!skipping) {
         d->started = started;

@@ -168,7 +168,7 @@ extern "C" nx_snappy_frame_decoder* nx_snappy_frame_decoder_new(int32_t validate
     d->validate = validate != 0;
     return d;
 }
-extern "C" void nx_snappy_frame_decoder_free(nx_snappy_frame_decoder* d) { delete d; }
+extern "C" void nx_snappy_frame_decoder_free(nx_snappy_frame_decoder* d) { nx_decoder_unref(d); }
 
 using nx::fr::SAct;
 using nx::fr::SnappyAction;

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include <set>
 #include <string>
 #include <vector>
@@ -106,4 +107,12 @@ struct nx_snappy_frame_decoder {
     uint64_t parse_pos = 0;            // the header walk has reached here; [parse_pos, end) is carried into the next submit
     uint64_t epoch = 0;                // bumped by each re-walk: jobs walked under an older epoch deliver nothing
     std::multiset<uint64_t> outstanding;  // walk starts of jobs submitted and not yet applied
+    // the owner's reference plus one per batcher job: nx_snappy_frame_decoder_free drops the owner's,
+    // and the handle is deleted when the last job referring to it is deleted (a handler removed while
+    // its jobs are in flight)
+    std::atomic<int> refs{1};
 };
+
+inline void nx_decoder_unref(nx_snappy_frame_decoder* d) {
+    if (d && d->refs.fetch_sub(1) == 1) delete d;
+}

@@ -676,10 +676,13 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
 // tags instead of one per tag for whichever lane happens to cross a block.
 constexpr int kParseBlock = 256;
 constexpr int kWinDw = 17;
-struct BurstWin {
+template <uint32_t NB>  // window of NB 16-byte blocks; LDS stride 4 * NB + 1 dwords (conflict-free)
+struct BurstWinT {
+    static constexpr uint32_t kBytes = 16u * NB;
+    static constexpr int kStride = 4 * (int)NB + 1;
     const uint8_t* origin;  // chunk start rounded down to 16 bytes
     uint32_t pad, end;      // chunk start - origin; chunk end, origin-relative
-    uint32_t base;          // window = origin-relative [base, base + 64)
+    uint32_t base;          // window = origin-relative [base, base + kBytes)
     uint32_t* w;            // this lane's LDS window
     __device__ __forceinline__ void init(const uint8_t* in, uint32_t length, uint32_t* lds) {
         origin = reinterpret_cast<const uint8_t*>((uintptr_t)in & ~(uintptr_t)15);
@@ -691,12 +694,12 @@ struct BurstWin {
     // are the (up to) 5 header bytes at chunk position p in the window?
     __device__ __forceinline__ bool has(uint32_t p) const {
         const uint32_t q = p + pad;
-        return q >= base && (q + 5u <= base + 64u || base + 64u >= end);
+        return q >= base && (q + 5u <= base + kBytes || base + kBytes >= end);
     }
     __device__ __forceinline__ void load(uint32_t p) {
         base = (p + pad) & ~15u;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
+        for (uint32_t k = 0; k < NB; ++k) {
             if (base + 16u * k < end) {
                 const uint4 x = *reinterpret_cast<const uint4*>(origin + base + 16u * k);
                 w[4 * k] = x.x;
@@ -714,6 +717,8 @@ struct BurstWin {
         return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
     }
 };
+using BurstWin = BurstWinT<4>;
+static_assert(BurstWin::kStride == kWinDw, "k_parse window stride");
 
 // Record writer: a lane's records gather 16 at a time in its LDS queue row and leave as one 64-byte
 // run (four back-to-back 16-byte stores), so the record slot is written in half-lines the L2 merges
@@ -943,11 +948,27 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
 // produces the bytes.  Checks (each NX_ERR_LZ4_MALFORMED, oracle/netty_oracle.c orc_lz4_decompress):
 // reading past the block, an offset of 0 or beyond the bytes produced, output past want, and a block
 // that ends with the output short of want.
-__device__ __forceinline__ uint32_t win_byte(BurstWin& win, uint32_t p) {
+
+// A copy of `len` bytes at distance `dist` splits into 64-byte records exactly (its bytes repeat at
+// the distance); a literal run of FastLZ / LZF is at most 32 bytes, one record.
+__device__ __forceinline__ bool put_copy(RecWriter& rw, uint32_t len, uint32_t dist) {
+    bool fit = true;
+    for (uint32_t k = 0; k < len && fit; k += 64u) {
+        const uint32_t m = len - k < 64u ? len - k : 64u;
+        fit = rw.put(0x80000000u | ((m - 1u) << 25) | dist);
+    }
+    return fit;
+}
+
+template <class Win>
+__device__ __forceinline__ uint32_t win_byte(Win& win, uint32_t p) {
     if (!win.has(p)) win.load(p);
     return (uint32_t)win.get8(p) & 0xFFu;
 }
 
+// One lane per block, byte at a time through the lane's LDS window (win_byte).  A burst form (one
+// header per step from an 8-byte view, wave-wide reloads, as k_parse) measured slower on configs[3]'s
+// mixed blocks: 35.5 vs 21.1 ms per 262 144 blocks (half of them random: one 64 KiB literal run).
 __global__ void __launch_bounds__(kParseBlock) k_parse_lz4(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                            const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ want_a,
                                                            uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
@@ -1121,17 +1142,10 @@ __global__ void __launch_bounds__(256) k_lz4_serial(const uint8_t* __restrict__ 
 // =====================================================================================
 // FastLZ and LZF blocks through the same record expander (configs[3]; records.hpp)
 // =====================================================================================
-// A copy of `len` bytes at distance `dist` splits into 64-byte records exactly (its bytes repeat at
-// the distance); a literal run of FastLZ / LZF is at most 32 bytes, one record.
-__device__ __forceinline__ bool put_copy(RecWriter& rw, uint32_t len, uint32_t dist) {
-    bool fit = true;
-    for (uint32_t k = 0; k < len && fit; k += 64u) {
-        const uint32_t m = len - k < 64u ? len - k : 64u;
-        fit = rw.put(0x80000000u | ((m - 1u) << 25) | dist);
-    }
-    return fit;
-}
 
+#ifndef FLZ_WIN_BLOCKS
+#define FLZ_WIN_BLOCKS 4
+#endif
 // FastLz.decompress (FastLz.java:409-543; the lane-serial form is fastlz.hip decompress()).  Block
 // byte 0 carries the level (bits 7..5) and the first literal-run control (bits 4..0); then runs of
 // ctrl+1 literal bytes (ctrl < 32) and back-references of (ctrl >> 5) + 2 (+ extension bytes) bytes
@@ -1150,7 +1164,8 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
                                                               const uint32_t* __restrict__ lim_a, uint32_t* __restrict__ rec,
                                                               uint32_t* __restrict__ nrec, uint32_t* __restrict__ out_len,
                                                               int32_t* __restrict__ status, uint32_t n) {
-    __shared__ uint32_t wins[kParseBlock * kWinDw + 4];
+    using Win = BurstWinT<FLZ_WIN_BLOCKS>;
+    __shared__ uint32_t wins[kParseBlock * Win::kStride + 4];
     __shared__ __attribute__((aligned(16))) uint32_t recq[kParseBlock * kQDw];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
@@ -1161,8 +1176,8 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
         status[c] = kNeedSerial;
         return;
     }
-    BurstWin win;
-    win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
+    Win win;
+    win.init(in + in_off[c], in_len, &wins[threadIdx.x * Win::kStride]);
     RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
     win.load(0);
     const uint32_t b0 = (uint32_t)win.get8(0) & 0xFFu;
@@ -1256,6 +1271,9 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
     status[c] = NX_OK;
 }
 
+#ifndef LZF_WIN_BLOCKS
+#define LZF_WIN_BLOCKS 8  // 128-byte windows: 13.3 -> 12.3 ms per 131072 text blocks (literal runs of up to 33 bytes)
+#endif
 // ChunkDecoder.decodeChunk (compress-lzf 1.0.3, as LzfDecoder.java:205 calls it; lane-serial form:
 // lzf.hip decode_chunk): runs of ctrl+1 literal bytes (ctrl < 32) and back-references of
 // (ctrl >> 5) + 2 (+ an extension byte when the length field is 7) bytes at distance
@@ -1265,7 +1283,8 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lzf(const uint8_t* __rest
                                                            const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ lim_a,
                                                            uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
                                                            uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t n) {
-    __shared__ uint32_t wins[kParseBlock * kWinDw + 4];
+    using Win = BurstWinT<LZF_WIN_BLOCKS>;
+    __shared__ uint32_t wins[kParseBlock * Win::kStride + 4];
     __shared__ __attribute__((aligned(16))) uint32_t recq[kParseBlock * kQDw];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
@@ -1275,8 +1294,8 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lzf(const uint8_t* __rest
         status[c] = kNeedSerial;
         return;
     }
-    BurstWin win;
-    win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
+    Win win;
+    win.init(in + in_off[c], in_len, &wins[threadIdx.x * Win::kStride]);
     RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
     uint32_t ip = 0, op = 0;
     bool ok = true, run = true;  // run: op < lim, and the next control byte at ip < in_len

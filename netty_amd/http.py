@@ -11,14 +11,24 @@ codec itself stays Netty's: message objects, header parsing, chunked transfer.
   (HttpContentCompressor.java:295-365), the Accept-Encoding q-value negotiation that picks "snappy".
   ``new_content_encoder`` is the snappy encoder factory (:232-233, :470-474).
 
+- ``SnappyHttpBodyEncoder`` / ``SnappyHttpBodyDecoder`` are the NON-BLOCKING snappy body path over the
+  cross-channel batcher: HttpContentEncoder / HttpContentDecoder run their
+  codec through an EmbeddedChannel synchronously (HttpContentEncoder.java:336-343,
+  HttpContentDecoder.java:165-175), so a GPU codec there would have to block the event loop.  These
+  handlers instead submit each body content as a batcher job and release messages strictly in
+  arrival order once their jobs complete (poll() never blocks), with the header rewriting those two
+  classes do for a coded body.
+
 Reference paths are relative to /root/reference/codec-http/src/main/java/io/netty/handler/codec/http/.
 """
 from __future__ import annotations
 
+import collections
 import re
 import struct
+from dataclasses import dataclass, field
 
-from .handlers import EmbeddedChannel, SnappyFrameDecoder, SnappyFrameEncoder
+from .handlers import Batcher, EmbeddedChannel, SnappyFrameDecoder, SnappyFrameEncoder
 
 SNAPPY = "snappy"  # HttpHeaderValues.SNAPPY (HttpHeaderValues.java:124-126)
 
@@ -123,3 +133,131 @@ class HttpContentCompressor:
         if enc == SNAPPY:
             return enc, EmbeddedChannel(SnappyFrameEncoder())
         return enc, None
+
+
+# ------------------------------------------------------------------ non-blocking snappy body path
+@dataclass
+class HttpMessage:
+    """The head of a request or response (headers by lower-case name)."""
+    headers: dict = field(default_factory=dict)
+
+
+@dataclass
+class HttpContent:
+    content: bytes = b""
+
+
+@dataclass
+class LastHttpContent(HttpContent):
+    trailers: dict = field(default_factory=dict)
+
+
+class _Ordered:
+    """A channel's messages in arrival order: ready ones, or batcher tickets still running."""
+
+    def __init__(self, batcher: Batcher):
+        self.b = batcher
+        self.q = collections.deque()  # [ticket or None, message or builder]
+
+    def push_ready(self, msg):
+        self.q.append([None, msg])
+
+    def push_job(self, ticket, build):
+        self.q.append([ticket, build])
+
+    def poll(self) -> list:
+        """Messages whose turn has come (a running job stops the release; never blocks)."""
+        out = []
+        while self.q:
+            t, m = self.q[0]
+            if t is not None:
+                if not self.b.poll(t):
+                    break
+                m = m(self.b.result(t))
+            self.q.popleft()
+            out.extend(m if isinstance(m, list) else [m])
+        return out
+
+
+class SnappyHttpBodyEncoder:
+    """Outbound, for a response whose coding HttpContentCompressor negotiated as snappy
+    (determineEncoding :295-365; SnappyEncoderFactory :470-474 makes one SnappyFrameEncoder per
+    response).  Header rewriting as HttpContentEncoder.encode does for a coded body
+    (HttpContentEncoder.java:181-196): Content-Encoding set, Content-Length removed, chunked transfer.
+    Each content's bytes become one batcher job; the framed bytes replace the content when it is done."""
+
+    def __init__(self, batcher: Batcher):
+        self.b = batcher
+        self.o = _Ordered(batcher)
+        self.enc = None
+
+    def write(self, msg, encoding: str | None = None):
+        """encoding: the negotiated coding for a response head (None = pass the body through)."""
+        if isinstance(msg, HttpMessage):
+            if encoding == SNAPPY:
+                h = dict(msg.headers)
+                h["content-encoding"] = SNAPPY
+                h.pop("content-length", None)
+                h["transfer-encoding"] = "chunked"
+                msg = HttpMessage(h)
+                self.enc = SnappyFrameEncoder()
+            self.o.push_ready(msg)
+            return
+        if self.enc is None:  # an identity body
+            self.o.push_ready(msg)
+            return
+        t = self.b.submit_encode(self.enc, msg.content)
+        # fetchEncoderOutput (:352-366) drops an empty buffer: an empty content yields no chunk
+        framed = lambda r: [HttpContent(x) for x in r if x]  # noqa: E731
+        if isinstance(msg, LastHttpContent):
+            trailers = msg.trailers
+            self.enc = None  # finishEncode: SnappyFrameEncoder adds nothing at the end of the body (:345-350)
+            self.o.push_job(t, lambda r: framed(r) + [LastHttpContent(b"", trailers)])  # encodeContent (:271-290)
+        else:
+            self.o.push_job(t, framed)
+
+    def poll(self) -> list:
+        return self.o.poll()
+
+
+class SnappyHttpBodyDecoder:
+    """Inbound, ahead of HttpContentDecompressor: a message whose Content-Encoding is snappy
+    (newContentDecoder :124-130, ASCII case-insensitive) is decoded here, with HttpContentDecoder's
+    header rewriting (HttpContentDecoder.java:89-137: the trimmed Content-Encoding picks the decoder,
+    Content-Length is removed for chunked transfer, the identity target coding removes
+    Content-Encoding); every other message passes through in order.  One DefaultHttpContent per
+    non-empty decoded chunk, as ByteBufForwarder (:286-294) fires them, then the last content with the
+    trailers (:174-187)."""
+
+    def __init__(self, batcher: Batcher, validate_checksums: bool = False):
+        self.b = batcher
+        self.o = _Ordered(batcher)
+        self.dec = None
+        self.validate = validate_checksums
+
+    def read(self, msg):
+        if isinstance(msg, HttpMessage):
+            ce = msg.headers.get("content-encoding", "")
+            if _ascii_eq_ignore_case(ce.strip(), SNAPPY):
+                h = dict(msg.headers)
+                if "content-length" in h:
+                    del h["content-length"]
+                    h["transfer-encoding"] = "chunked"
+                h.pop("content-encoding", None)
+                msg = HttpMessage(h)
+                self.dec = SnappyFrameDecoder(self.validate)
+            self.o.push_ready(msg)
+            return
+        if self.dec is None:
+            self.o.push_ready(msg)
+            return
+        t = self.b.submit_decode(self.dec, msg.content)
+        if isinstance(msg, LastHttpContent):
+            trailers = msg.trailers
+            self.dec = None
+            self.o.push_job(t, lambda r: [HttpContent(x) for x in r if x] + [LastHttpContent(b"", trailers)])
+        else:
+            self.o.push_job(t, lambda r: [HttpContent(x) for x in r if x])
+
+    def poll(self) -> list:
+        return self.o.poll()

@@ -23,6 +23,9 @@ fi
 if [[ $STAGE == all || $STAGE == bench ]]; then
   run timeout -k 10 600 python bench.py --total-chunks "$CHUNKS" --weak-chunks 0 --steps 3 --warmup 1 --cpu-seconds 6 > "$OUT/bench.log" 2>&1 || exit 1
 fi
+if [[ $STAGE == full ]]; then  # the driver's default bench line (configs[4], 100 GiB at N=1)
+  run timeout -k 10 900 python bench.py > "$OUT/bench_full.log" 2>&1 || exit 1
+fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
   export TMPDIR=/tmp
   cd /tmp && run timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \

@@ -344,3 +344,29 @@ def test_batcher_validating_leftover_then_error(nx, oracle):
     with pytest.raises(nx.DecompressionException, match="Found reserved unskippable chunk type: 0x2") as ei:
         s.channel_read(stream)
     assert ei.value.decoded == [x, b""]
+
+
+def test_batcher_decoder_freed_with_jobs_in_flight(nx, oracle):
+    """A handler removed while its jobs are queued (nx_snappy_frame_decoder_free before the flush):
+    the jobs keep the handle alive and still deliver their messages (validating and not)."""
+    data = oracle.textgen_chunk(41, 150000)
+    f, _ = oracle.snappy_frame_encode(data)
+    b = nx.Batcher()
+    tickets = []
+    for validate in (False, True):
+        d = nx.SnappyFrameDecoder(validate)
+        tickets.append(b.submit_decode(d, f[:len(f) // 2]))
+        tickets.append(b.submit_decode(d, f[len(f) // 2:]))
+        d.close()  # the owner's reference goes; the two jobs hold theirs
+    b.flush()
+    got = []
+    for t in tickets:
+        b.wait(t)
+        got.append(b"".join(b.result(t)))
+    assert got[0] + got[1] == data and got[2] + got[3] == data
+    # the batches are reused afterwards (their jobs, and with them the last references, are deleted)
+    d2 = nx.SnappyFrameDecoder(True)
+    t = b.submit_decode(d2, f)
+    b.flush()
+    b.wait(t)
+    assert b"".join(b.result(t)) == data

@@ -60,3 +60,86 @@ def test_snappy_content_decoder_and_encoder():
     while (m := dec.read_inbound()) is not None:
         got += m
     assert got == body
+
+
+def _drain(handler, want_lasts, limit_s=60.0):
+    """poll() until `want_lasts` LastHttpContent messages came out (poll never blocks)."""
+    import time
+    out, t0 = [], time.time()
+    while sum(isinstance(m, http.LastHttpContent) for m in out) < want_lasts:
+        out += handler.poll()
+        assert time.time() - t0 < limit_s, "batcher jobs did not complete"
+    return out
+
+
+@pytest.mark.gpu
+def test_nonblocking_snappy_http_bodies(oracle):
+    """The non-blocking HTTP snappy path: per channel, a snappy response of
+    several contents, an identity response and a second snappy response, all encoded by ONE batcher
+    flush for every channel; each channel's messages come out in order, the framed bodies equal
+    SnappyFrameEncoder's bytes (one encoder per response), and the decoder side restores the bodies
+    with HttpContentDecoder's header rewriting."""
+    import random
+    from netty_amd.handlers import Batcher
+    rng = random.Random(5)
+    b = Batcher()
+    chans = []
+    for ch in range(6):
+        parts = [oracle.textgen_chunk(ch * 10 + k, rng.randrange(0, 90000)) for k in range(3)] + [b""]
+        plain = [b"identity body " * (ch + 1)]
+        parts2 = [oracle.textgen_chunk(ch * 10 + 7, 5000)]
+        enc = http.SnappyHttpBodyEncoder(b)
+        enc.write(http.HttpMessage({"content-length": str(sum(map(len, parts)))}), encoding="snappy")
+        for p in parts[:-1]:
+            enc.write(http.HttpContent(p))
+        enc.write(http.LastHttpContent(parts[-1], {"x-trailer": str(ch)}))
+        enc.write(http.HttpMessage({"content-length": str(len(plain[0]))}))  # identity: passes through
+        enc.write(http.LastHttpContent(plain[0]))
+        enc.write(http.HttpMessage({}), encoding="snappy")
+        enc.write(http.LastHttpContent(parts2[0]))
+        chans.append((enc, parts, plain, parts2))
+    b.flush()
+    for enc, parts, plain, parts2 in chans:
+        out = _drain(enc, 3)
+        head = out[0]
+        assert head.headers == {"content-encoding": "snappy", "transfer-encoding": "chunked"}
+        want, started = [], False
+        for p in parts:
+            if p:
+                want.append(oracle.snappy_frame_encode(p, started=started)[0])
+                started = True
+        i = 1
+        got = []
+        while not isinstance(out[i], http.LastHttpContent):
+            got.append(out[i].content)
+            i += 1
+        assert got == want
+        assert out[i].trailers == {"x-trailer": str(chans.index((enc, parts, plain, parts2)))}
+        assert out[i + 1].headers == {"content-length": str(len(plain[0]))}
+        assert out[i + 2] == http.LastHttpContent(plain[0])
+        assert out[i + 3].headers["content-encoding"] == "snappy"
+        assert out[i + 4].content == oracle.snappy_frame_encode(parts2[0])[0]
+        assert isinstance(out[i + 5], http.LastHttpContent) and len(out) == i + 6
+        # inbound: the framed body re-chunked at random points, Content-Encoding in another case
+        body = b"".join(got)
+        cuts = sorted(rng.randrange(0, len(body) + 1) for _ in range(4))
+        pieces = [body[a:c] for a, c in zip([0] + cuts, cuts + [len(body)])]
+        dec = http.SnappyHttpBodyDecoder(b, validate_checksums=True)
+        dec.read(http.HttpMessage({"content-encoding": " Snappy ", "content-length": str(len(body))}))
+        for p in pieces[:-1]:
+            dec.read(http.HttpContent(p))
+        dec.read(http.LastHttpContent(pieces[-1], {"t": "1"}))
+        dec.read(http.HttpMessage({"content-length": "3"}))
+        dec.read(http.LastHttpContent(b"abc"))
+        b.flush()
+        din = _drain(dec, 2)
+        assert din[0].headers == {"transfer-encoding": "chunked"}
+        k = 1
+        dec_body = b""
+        while not isinstance(din[k], http.LastHttpContent):
+            assert din[k].content  # empty chunks are not forwarded (ByteBufForwarder)
+            dec_body += din[k].content
+            k += 1
+        assert dec_body == b"".join(parts)
+        assert din[k] == http.LastHttpContent(b"", {"t": "1"})
+        assert din[k + 1].headers == {"content-length": "3"} and din[k + 2] == http.LastHttpContent(b"abc")
