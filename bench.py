@@ -352,12 +352,14 @@ def roofline(algo_bytes, ms, n_chunks, kernels, traffic, copy_gbs):
 
 
 ENC_KERNELS = ["nx::enc::k_snappy_encode"]
-# Snappy.encode's dependent memory requests per 64 KiB chunk of the bench corpus: table probes (one
-# exchange of a random 64-bit slot each; profiles/r01/encoder_experiments.md) and first reads of a
-# candidate's input — with the wide table entries (exact word + 3 following bytes) only matches of
-# 7+ bytes read the candidate (scripts/experiments/sim_window.py's match-length census: 4 275 of
-# 7 723 matches per chunk; 9 709 with the round-1 32-bit entries)
+# Snappy.encode's random table traffic per 64 KiB chunk of the bench corpus: table probes (one
+# exchange of a random 64-bit slot each), inserts (one store after each match, :187-188) and first
+# reads of a candidate's input (with the wide table entries — exact word + 3 following bytes — only
+# matches of 7+ bytes read the candidate).  Pinned by tests/test_bench_census.py to the oracle's
+# census (oracle/netty_oracle.c orc_snappy_encode_census) over chunks spread across configs[4]: the
+# bench itself runs no oracle code outside its cpu_baseline leg.
 ENC_PROBES_PER_CHUNK = 16546
+ENC_INSERTS_PER_CHUNK = 7724
 ENC_CANDIDATE_LOADS_PER_CHUNK = 4275
 
 
@@ -473,7 +475,9 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
         got = ENC_PROBES_PER_CHUNK * n / (t_enc / 1e3)
         r_enc["random_access"] = {
             "note": "the encoder's bound: serial chains of random table exchanges + candidate loads per lane",
-            "probes_per_chunk": ENC_PROBES_PER_CHUNK, "candidate_loads_per_chunk": ENC_CANDIDATE_LOADS_PER_CHUNK,
+            "probes_per_chunk": ENC_PROBES_PER_CHUNK, "inserts_per_chunk": ENC_INSERTS_PER_CHUNK,
+            "candidate_loads_per_chunk": ENC_CANDIDATE_LOADS_PER_CHUNK,
+            "census_source": "tests/test_bench_census.py (oracle census of configs[4] chunks, within 1 %)",
             "achieved_probes_per_s": round(got / 1e9, 3) * 1e9,
             "ceiling_probes_per_s": round(ceil / 1e9, 3) * 1e9 if ceil else None,
             "frac": round(got / ceil, 4) if ceil else None,

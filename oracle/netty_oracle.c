@@ -134,8 +134,11 @@ static size_t encode_copy(uint8_t* out, size_t op, int32_t offset, int32_t lengt
 
 size_t orc_snappy_max_compressed_length(size_t n) { return 32 + n + n / 6; }
 
-/* Snappy.encode (:82-165) with in.readerIndex() == 0 (baseIndex = 0) */
-size_t orc_snappy_encode(const uint8_t* in, int32_t length, uint8_t* out) {
+/* Snappy.encode (:82-165) with in.readerIndex() == 0 (baseIndex = 0).  census (nullable, test-only):
+ * [0] += table probes (a read + write of one slot: the probe loop :164-173 and the lookup after each
+ * match :189-191), [1] += inserts (:187-188), [2] += matches, [3] += matches of 7+ bytes (the GPU's
+ * wide table entries hold a candidate's first 7 bytes, so only these read the candidate's input). */
+static size_t snappy_encode_impl(const uint8_t* in, int32_t length, uint8_t* out, uint64_t* census) {
     size_t op = 0;
     /* preamble: LE base-128 varint (:84-92); `length >>> i*7` */
     for (int i = 0;; i++) {
@@ -170,6 +173,7 @@ size_t orc_snappy_encode(const uint8_t* in, int32_t length, uint8_t* out) {
                 nextHash = snappy_hash(in, nextIndex, shift);
                 candidate = baseIndex + table[hash];
                 table[hash] = (uint16_t)(inIndex - baseIndex);
+                if (census) census[0]++;
             } while (be32(in + inIndex) != be32(in + candidate));
 
             op = encode_literal(in + nextEmit, out, op, inIndex - nextEmit);
@@ -178,6 +182,10 @@ size_t orc_snappy_encode(const uint8_t* in, int32_t length, uint8_t* out) {
             do {
                 int32_t base = inIndex;
                 int32_t matched = 4 + find_matching_length(in, candidate + 4, inIndex + 4, length);
+                if (census) {
+                    census[2]++;
+                    census[3] += matched >= 7;
+                }
                 inIndex += matched;
                 int32_t offset = base - candidate;
                 op = encode_copy(out, op, offset, matched);
@@ -189,6 +197,10 @@ size_t orc_snappy_encode(const uint8_t* in, int32_t length, uint8_t* out) {
                 uint32_t currentHash = snappy_hash(in, insertTail + 1, shift);
                 candidate = baseIndex + table[currentHash];
                 table[currentHash] = (uint16_t)(inIndex - baseIndex);
+                if (census) {
+                    census[0]++;
+                    census[1]++;
+                }
             } while (be32(in + insertTail + 1) == be32(in + candidate));
 
             nextHash = snappy_hash(in, insertTail + 2, shift);
@@ -199,6 +211,12 @@ done_outer:
     if (nextEmit < length) op = encode_literal(in + nextEmit, out, op, length - nextEmit);
     free(table);
     return op;
+}
+
+size_t orc_snappy_encode(const uint8_t* in, int32_t length, uint8_t* out) { return snappy_encode_impl(in, length, out, NULL); }
+
+size_t orc_snappy_encode_census(const uint8_t* in, int32_t length, uint8_t* out, uint64_t* census) {
+    return snappy_encode_impl(in, length, out, census);
 }
 
 /* =====================================================================================

@@ -28,6 +28,9 @@ uint32_t orc_snappy_checksum(const uint8_t* p, size_t n);
 size_t orc_snappy_max_compressed_length(size_t n);
 /* encode(in, out, length) with in.readerIndex()==0 (the framing encoder's readSlice). Returns bytes written. */
 size_t orc_snappy_encode(const uint8_t* in, int32_t length, uint8_t* out);
+/* orc_snappy_encode plus a census of its table traffic (test-only; netty_oracle.c snappy_encode_impl):
+ * census[0..3] += probes, inserts, matches, matches of 7+ bytes. */
+size_t orc_snappy_encode_census(const uint8_t* in, int32_t length, uint8_t* out, uint64_t* census);
 /* One-shot decode of a complete chunk payload, as SnappyFrameDecoder drives Snappy.decode.
  * out_cap = output ByteBuf max capacity (65536 in the frame decoder).
  * Returns status (NX_OK or NX_ERR_*); *out_len = bytes produced (partial on silent truncation);

@@ -45,6 +45,8 @@ def lib():
         L.orc_snappy_max_compressed_length.argtypes = [C.c_size_t]
         L.orc_snappy_encode.restype = C.c_size_t
         L.orc_snappy_encode.argtypes = [C.c_char_p, C.c_int32, C.c_void_p]
+        L.orc_snappy_encode_census.restype = C.c_size_t
+        L.orc_snappy_encode_census.argtypes = [C.c_char_p, C.c_int32, C.c_void_p, C.POINTER(C.c_uint64)]
         L.orc_snappy_decode.restype = C.c_int32
         L.orc_snappy_decode.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                         C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
@@ -117,6 +119,15 @@ def snappy_encode(data: bytes) -> bytes:
     out = _buf(L.orc_snappy_max_compressed_length(len(data)))
     n = L.orc_snappy_encode(bytes(data), len(data), out)
     return bytes(out[:n])
+
+
+def snappy_encode_census(data: bytes):
+    """(encoded bytes, {probes, inserts, matches, matches_7plus}) of Snappy.encode's table traffic."""
+    L = lib()
+    out = _buf(L.orc_snappy_max_compressed_length(len(data)))
+    c = (C.c_uint64 * 4)()
+    n = L.orc_snappy_encode_census(bytes(data), len(data), out, c)
+    return bytes(out[:n]), dict(zip(("probes", "inserts", "matches", "matches_7plus"), list(c)))
 
 
 def snappy_decode(data: bytes, out_cap: int = 1 << 31):
