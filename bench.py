@@ -366,8 +366,9 @@ ENC_CANDIDATE_LOADS_PER_CHUNK = 4275
 def probe_ceiling(torch, dev, lanes=262144, steps=16384):
     """The random-access ceiling of the encoder's request pattern on this GPU (netty_amd/tools/
     probe_ceiling.hip: per lane a serial chain of 64-bit table exchanges + the encoder's share of
-    dependent input loads over its own regions, at the encoder's resident lane count).  Returns
-    probes/s or None."""
+    dependent input loads over its own regions, with and without the encoder's share of insert
+    stores, at the encoder's resident lane count).  Returns {"with_inserts", "no_inserts"} probes/s,
+    or None."""
     import ctypes
     path = os.path.join(ROOT, "netty_amd", "libnx_probe_ceiling.so")
     if not os.path.exists(path):
@@ -375,27 +376,30 @@ def probe_ceiling(torch, dev, lanes=262144, steps=16384):
     lib = ctypes.CDLL(path)
     lib.nx_probe_ceiling.restype = ctypes.c_int32
     lib.nx_probe_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
-                                     ctypes.c_uint32, ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
     # The rate depends on where the table lands; the encoder's workspace is the best of
     # several placements (snappy_encode.hip alloc_workspace), so the ceiling is too: the fastest of up
     # to three tables held at once (each drawn while the others stay allocated).
     inp = torch.empty(lanes * 16384, dtype=torch.int32, device=dev)
     sink = torch.empty(lanes, dtype=torch.int32, device=dev)
-    permille = round(1000 * ENC_CANDIDATE_LOADS_PER_CHUNK / ENC_PROBES_PER_CHUNK)
-    tabs, best = [], None
+    loads = round(1000 * ENC_CANDIDATE_LOADS_PER_CHUNK / ENC_PROBES_PER_CHUNK)
+    inserts = round(1000 * ENC_INSERTS_PER_CHUNK / ENC_PROBES_PER_CHUNK)
+    tabs, best = [], {}
     for k in range(3):
         if k and torch.cuda.mem_get_info(dev)[0] < lanes * 16384 * 8 + (8 << 30):
             break
         tabs.append(torch.empty(lanes * 16384, dtype=torch.int64, device=dev))
-        ms = ctypes.c_float(0.0)
-        rc = lib.nx_probe_ceiling(tabs[-1].data_ptr(), inp.data_ptr(), sink.data_ptr(), lanes, steps, permille, ctypes.byref(ms),
-                                  ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
-        if rc == 0 and ms.value > 0:
-            rate = lanes * steps / (ms.value / 1e3)
-            best = rate if best is None else max(best, rate)
+        for key, ins in (("no_inserts", 0), ("with_inserts", inserts)):
+            ms = ctypes.c_float(0.0)
+            rc = lib.nx_probe_ceiling(tabs[-1].data_ptr(), inp.data_ptr(), sink.data_ptr(), lanes, steps, loads, ins,
+                                      ctypes.byref(ms), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+            if rc == 0 and ms.value > 0:
+                best[key] = max(best.get(key, 0.0), lanes * steps / (ms.value / 1e3))
     del tabs, inp, sink
     torch.cuda.empty_cache()
-    return best
+    return best or None
+
+
 def encoder_placement():
     """Probe times of the candidate placements the encoder's workspace was chosen from."""
     import ctypes
@@ -412,9 +416,9 @@ def encoder_placement():
 DEC_KERNELS = ["nx::dec::k_parse", "nx::dec::k_expand"]
 
 
-def timed_legs(torch, leg, steps, warmup, sync, S, dev):
+def timed_legs(torch, leg, steps, warmup, sync, S, dev, cdev=None):
     """W untimed steps, then exactly K steps bracketed by barrier + device synchronize on both sides;
-    the job's time is the max over ranks."""
+    the job's time is the max over ranks (reduced on cdev, default dev)."""
     dsync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     for _ in range(warmup):
         leg.step(False)
@@ -427,7 +431,7 @@ def timed_legs(torch, leg, steps, warmup, sync, S, dev):
     dsync()
     sync()
     t1 = time.perf_counter()
-    return S.max_over_ranks(t1 - t0, device=dev)
+    return S.max_over_ranks(t1 - t0, device=dev if cdev is None else cdev)
 
 
 def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg_factory=None, emit=print):
@@ -445,9 +449,12 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
+    # the device of the few collective tensors: the GPU under RCCL; the host under gloo (the CPU tests,
+    # and the GPU test that runs two ranks' GPU legs on one device)
+    cdev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if gpu:
+        if gpu and backend == "nccl":
             dist.init_process_group(backend, rank=rank, world_size=world, device_id=dev)
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
@@ -460,10 +467,10 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
     lo, hi = S.shard_range(args.total_chunks, rank, world)
     n = hi - lo
     leg = SnappyRoundTrip(torch, dev, lo, n, args.sub_chunks) if gpu else leg_factory(lo, n)
-    elapsed = timed_legs(torch, leg, args.steps, args.warmup, sync, S, dev)
+    elapsed = timed_legs(torch, leg, args.steps, args.warmup, sync, S, dev, cdev)
     ok, crc_detect = leg.verify(rank)
     comp_bytes = leg.comp_bytes()
-    my_off, total_comp, totals_all = S.exchange_offsets(comp_bytes, device=dev)
+    my_off, total_comp, totals_all = S.exchange_offsets(comp_bytes, device=cdev)
     t_crc, t_enc, t_dec = leg.kernel_ms_per_step(args.steps)
     U, C_ = n * CHUNK, comp_bytes
     copy_gbs = copy_rate_gbs(torch, leg.src[:min(n, leg.sub) * CHUNK], leg.dec) if gpu else None
@@ -471,17 +478,22 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
     r_dec = roofline(C_ + U, t_dec, n, DEC_KERNELS, traffic, copy_gbs)  # decode: C_in + U_out per chunk
     r_enc = roofline(U + C_, t_enc, n, ENC_KERNELS, traffic, copy_gbs)  # encode: U_in + C_out per chunk
     if gpu and t_enc and not args.no_probe_ceiling:
-        ceil = probe_ceiling(torch, dev)
+        ceil = probe_ceiling(torch, dev) or {}
         got = ENC_PROBES_PER_CHUNK * n / (t_enc / 1e3)
+        cw, cn = ceil.get("with_inserts"), ceil.get("no_inserts")
         r_enc["random_access"] = {
-            "note": "the encoder's bound: serial chains of random table exchanges + candidate loads per lane",
+            "note": "the encoder's bound: serial chains of random table exchanges + insert stores + candidate loads per lane",
             "probes_per_chunk": ENC_PROBES_PER_CHUNK, "inserts_per_chunk": ENC_INSERTS_PER_CHUNK,
             "candidate_loads_per_chunk": ENC_CANDIDATE_LOADS_PER_CHUNK,
             "census_source": "tests/test_bench_census.py (oracle census of configs[4] chunks, within 1 %)",
             "achieved_probes_per_s": round(got / 1e9, 3) * 1e9,
-            "ceiling_probes_per_s": round(ceil / 1e9, 3) * 1e9 if ceil else None,
-            "frac": round(got / ceil, 4) if ceil else None,
-            "ceiling_source": "netty_amd/tools/probe_ceiling.hip, same request mix without compute, 262144 lanes, timed live, fastest of up to 3 table placements (as the encoder chooses its workspace)"}
+            "ceiling_probes_per_s": round(cw / 1e9, 3) * 1e9 if cw else None,
+            "frac": round(got / cw, 4) if cw else None,
+            "ceiling_no_inserts_probes_per_s": round(cn / 1e9, 3) * 1e9 if cn else None,
+            "frac_no_inserts": round(got / cn, 4) if cn else None,
+            "ceiling_source": "netty_amd/tools/probe_ceiling.hip, the same request mix without compute (exchanges, "
+                              "insert stores and candidate loads in the census proportions; and without the stores), "
+                              "262144 lanes, timed live, fastest of up to 3 table placements (as the encoder chooses its workspace)"}
     if gpu:
         r_enc["workspace_placement"] = encoder_placement()
     dominant = r_enc if t_enc >= t_dec else r_dec
@@ -508,7 +520,7 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
         "compressed_bytes_per_rank": totals_all,
         "crc_corruption_subset_detected": crc_detect,
     }
-    ok = S.all_true(ok, device=dev)
+    ok = S.all_true(ok, device=cdev)
     line["verified"] = ok
     if gpu and rank == 0:
         line["device"] = device_info(torch, dev)
@@ -516,9 +528,9 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
         del leg
         torch.cuda.empty_cache()
         wk = SnappyRoundTrip(torch, dev, rank * args.weak_chunks, args.weak_chunks, args.sub_chunks)
-        wel = timed_legs(torch, wk, args.weak_steps, 1 if args.warmup else 0, sync, S, dev)
+        wel = timed_legs(torch, wk, args.weak_steps, 1 if args.warmup else 0, sync, S, dev, cdev)
         wok, _ = wk.verify(rank)
-        wok = S.all_true(wok, device=dev)
+        wok = S.all_true(wok, device=cdev)
         _, we, wd = wk.kernel_ms_per_step(args.weak_steps)
         line["weak_1m_per_gpu"] = {
             "workload": "configs[1]+configs[2]: the same step over chunks_per_gpu chunks on every GPU (weak scaling)",
