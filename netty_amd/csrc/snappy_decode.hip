@@ -394,12 +394,10 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
                 const uint32_t m0 = n0 - xo * ((n0 * inv) >> 16);
                 const uint32_t q = tstart - xo;
                 uint32_t ad[4];
+                uint32_t mi = m0;  // (n0 + i) mod xo, stepped: m0 < xo, so one wrap test per byte
 #pragma unroll
                 for (uint32_t i = 0; i < 4; ++i) {
-                    uint32_t mi = m0 + i;
-                    mi -= mi >= xo ? xo : 0u;
-                    mi -= mi >= xo ? xo : 0u;
-                    mi -= mi >= xo ? xo : 0u;
+                    if (i) mi = mi + 1u == xo ? 0u : mi + 1u;
                     ad[i] = (q + mi) & (kRing - 1);
                 }
                 ova = ad[0] | (ad[1] << 16);
@@ -908,10 +906,14 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
         uint32_t rnext = (uint32_t)lane < N ? R[lane] : 0u;
         for (uint32_t b = 0; b < N; b += 64u) {
             const uint32_t r = rnext;
-            rnext = b + 64u + (uint32_t)lane < N ? R[b + 64u + lane] : 0u;  // prefetch the next batch
             const bool valid = b + (uint32_t)lane < N;
             const bool isc = (r >> 31) != 0u;
             const uint32_t len = valid ? ((r >> 25) & 63u) + 1u : 0u;
+            // Issue the next batch's prefetch only after this batch's records are in use: vmcnt counts
+            // in order, so a wait for `r` placed after the new load also waited for the new load
+            // (a memory latency per batch; 57.8 -> 57.0 ms per 262 144 frames).
+            asm volatile("" ::"v"(len) : "memory");
+            rnext = b + 64u + (uint32_t)lane < N ? R[b + 64u + lane] : 0u;  // prefetch the next batch
             const uint32_t x = r & 0x1FFFFFFu;
             const uint32_t incl = incl_scan(len);
             const uint32_t ostart = O + incl - len;
