@@ -370,3 +370,44 @@ def test_batcher_decoder_freed_with_jobs_in_flight(nx, oracle):
     b.flush()
     b.wait(t)
     assert b"".join(b.result(t)) == data
+
+
+def test_batcher_validating_leftover_registered_autoflush(nx, oracle):
+    """Leftover re-walks with registered cumulations and auto-flushes across the batcher's four streams:
+    each read's cumulation is placed in a registered arena (bytes [0, consumed) stay valid until the job
+    completes, the unconsumed tail is resubmitted with the next read, as ByteToMessageDecoder's
+    cumulation), many jobs per decoder are in flight at once, small batches launch on their own, and
+    every channel still receives the synchronous decoder's messages in order."""
+    streams = [(s, w) for s, w, _ in leftover_streams(oracle)] * 3
+    rng = random.Random(77)
+    arena_size = 8 * sum(len(s) for s, _ in streams) + 4096
+    arena = (C.c_uint8 * arena_size)()
+    base = C.addressof(arena)
+    nx.Batcher.register(base, arena_size)
+    try:
+        b = nx.Batcher(flush_bytes=48 << 10)
+        chans = []
+        for s, w in streams:
+            cuts = sorted(rng.randrange(0, len(s) + 1) for _ in range(3))
+            parts = [s[a:c] for a, c in zip([0] + cuts, cuts + [len(s)])]
+            chans.append([nx.SnappyFrameDecoder(True), parts, w, [], bytearray()])
+        pos = 0
+        for r in range(4):
+            for ch in chans:
+                d, parts, _, tickets, cum = ch
+                cum += parts[r]
+                C.memmove(base + pos, bytes(cum), len(cum))
+                t, consumed = b.submit_decode_registered(d, base + pos, len(cum))
+                tickets.append(t)
+                pos += (len(cum) + 15) & ~15
+                del cum[:consumed]
+        b.flush()
+        for d, parts, want, tickets, cum in chans:
+            got = []
+            for t in tickets:
+                b.wait(t)
+                got += b.result(t)
+            assert got == want
+        assert b.stats()["flushes"] > 1
+    finally:
+        nx.Batcher.unregister(base)
