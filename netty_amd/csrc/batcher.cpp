@@ -262,7 +262,8 @@ struct Job {
     // relative to it), under the decoder's re-walk epoch; `walked` = s_base is in dec->outstanding
     uint64_t s_base = 0, epoch = 0;
     bool walked = false;
-    std::deque<std::vector<uint8_t>> owned;  // messages delivered before a re-walk moved the job to a later batch
+    std::vector<std::vector<uint8_t>> owned;  // messages delivered before a re-walk moved the job (a moved
+                                              // vector keeps its buffer; a deque would allocate per Job)
     Job() = default;
     Job(const Job&) = delete;
     Job& operator=(const Job&) = delete;
@@ -414,19 +415,13 @@ Batch* collecting(nx_batcher* b) {
     return b->cur;
 }
 
-// Drop the stream bytes no unapplied job of a validating decoder can re-walk any more.
+// Drop the stream segments no unapplied job of a validating decoder can re-walk any more.
 void trim_hist(nx_snappy_frame_decoder* d) {
     if (d->corrupted) {  // (:86-89): nothing is parsed again
-        d->hist.clear();
-        d->hist.shrink_to_fit();
-        d->hist_base = d->parse_pos;
+        d->hist.clear(d->parse_pos);
         return;
     }
-    const uint64_t keep = d->outstanding.empty() ? d->parse_pos : *d->outstanding.begin();
-    if (keep > d->hist_base) {
-        d->hist.erase(d->hist.begin(), d->hist.begin() + (ptrdiff_t)(keep - d->hist_base));
-        d->hist_base = keep;
-    }
+    d->hist.drop_before(d->outstanding.empty() ? d->parse_pos : *d->outstanding.begin());
 }
 
 void unwalk(Job* j) {  // the job no longer needs its walked bytes kept
@@ -440,7 +435,7 @@ void unwalk(Job* j) {  // the job no longer needs its walked bytes kept
 // Queue decoder job j's walked actions into batch bt.  Payloads are copied from S (host bytes the
 // walk ran over), or, with dS (the device address of S in registered memory), gathered from there at
 // flush.  On failure the batch's arrays go back to their sizes at entry (its other jobs stay valid).
-int32_t enqueue_dec(Batch* bt, Job* j, const uint8_t* S, size_t walked, const uint8_t* dS) {
+int32_t enqueue_dec(Batch* bt, Job* j, const uint8_t* S, size_t walked, const uint8_t* dS, int64_t staged = -1) {
     const size_t n_act = bt->dact.size(), n_dc = bt->dc_off.size(), n_du = bt->du_off.size(), n_dir = bt->direct.size();
     const uint64_t dir_used = bt->direct_used;
     auto fail = [&](int32_t code) -> int32_t {
@@ -472,6 +467,8 @@ int32_t enqueue_dec(Batch* bt, Job* j, const uint8_t* S, size_t walked, const ui
         uint64_t off = 0;
         if (dS) {
             off = rbase + a.data;
+        } else if (staged >= 0) {  // the walked bytes are already in the staging arena at `staged`
+            off = (uint64_t)staged + a.data;
         } else {
             uint8_t* st = bt->stage(a.dlen, &off);
             if (!st) return fail(NX_ERR_HIP);
@@ -543,8 +540,8 @@ bool rewalk(nx_batcher* b, Batch* bt, Job* j, uint64_t q) {
     d->parse_failed = false;
     bool started = true;  // a compressed chunk was accepted (:180-183)
     uint64_t skip = 0;
-    const uint8_t* S = d->hist.data() + (q - d->hist_base);
-    const size_t n = (size_t)(d->hist_base + d->hist.size() - q);
+    const uint8_t* S = d->hist.own_from(q);
+    const size_t n = (size_t)(d->hist.end - q);
     const size_t p = walk(d, j, S, n, started, skip);
     d->started = started;
     d->skip = skip;
@@ -806,7 +803,8 @@ void queue_continuations(nx_batcher* b) {
             }
         auto it = b->tickets.find(j->ticket);
         const bool live = it != b->tickets.end();
-        if (!to || enqueue_dec(to, j, d->hist.data() + (j->s_base - d->hist_base), 0, nullptr) != NX_OK) {
+        const uint8_t* S = d->hist.at(j->s_base);  // the owned segment rewalk() made, from s_base on
+        if (!to || !S || enqueue_dec(to, j, S, 0, nullptr) != NX_OK) {
             // cannot queue it: the job fails as a launch failure would (result() reports it)
             unwalk(j);
             j->applied = true;
@@ -887,8 +885,8 @@ extern "C" nx_batcher* nx_batcher_new(void) {
     // One Snappy table workspace and one record workspace for the whole batcher, whichever of its
     // streams a flush lands on (a flush waits on the device for the previous flush's kernels).
     b->held_enc = hipGetDevice(&b->dev) == hipSuccess &&
-                  nx::ws_hold(nx::WsKind::SnappyEnc, b->dev, nx::kBatcherHoldUnits, b->s[0]) == NX_OK;
-    b->held_dec = b->held_enc && nx::ws_hold(nx::WsKind::DecRecords, b->dev, nx::kBatcherHoldUnits, b->s[0]) == NX_OK;
+                  nx::ws_hold(nx::WsKind::SnappyEnc, b->dev, nx::kBatcherEncHoldUnits, b->s[0]) == NX_OK;
+    b->held_dec = b->held_enc && nx::ws_hold(nx::WsKind::DecRecords, b->dev, nx::kBatcherDecHoldUnits, b->s[0]) == NX_OK;
     if (!b->held_dec) {
         nx_batcher_free(b);
         return nullptr;
@@ -1028,10 +1026,10 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
         p = n;
     } else {
         if (d->validate) {
-            carried = (size_t)(d->hist_base + d->hist.size() - d->parse_pos);
+            carried = (size_t)(d->hist.end - d->parse_pos);
             if (carried) {
                 joined.reserve(carried + n);
-                joined.assign(d->hist.end() - (ptrdiff_t)carried, d->hist.end());
+                d->hist.copy_from(d->parse_pos, joined);
                 joined.insert(joined.end(), in, in + n);
                 S = joined.data();
             }
@@ -1050,7 +1048,21 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
             return NX_ERR_INVALID_ARG;
         }
     }
-    if (enqueue_dec(bt, j, S, walked, dS) != NX_OK) {
+    // a validating decoder stages the walked bytes whole (headers too): the payloads are slices of
+    // that copy, and its history references it instead of copying the bytes a second time
+    int64_t staged = -1;
+    if (d->validate && !dS && walked) {
+        uint64_t off = 0;
+        uint8_t* st = bt->stage(walked, &off);
+        if (!st) {
+            j->dec = nullptr;
+            delete j;
+            return NX_ERR_HIP;
+        }
+        memcpy(st, S, walked);
+        staged = (int64_t)off;
+    }
+    if (enqueue_dec(bt, j, S, walked, dS, staged) != NX_OK) {
         j->dec = nullptr;  // no reference taken yet
         delete j;
         return NX_ERR_HIP;
@@ -1067,7 +1079,12 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
     if (d->validate && !d->corrupted) {
         // every consumed byte is kept until no unapplied job can re-walk it (a leftover, :206-212);
         // skipped input too, since a re-walk may find that the failure was not reached after all
-        d->hist.insert(d->hist.end(), in, in + p);
+        // a registered cumulation stays valid until this job completes, and so does the job's copy in
+        // the staging arena: referenced, not copied
+        if (staged >= 0)
+            d->hist.append_staged(&bt->staging.h, (uint64_t)staged + carried, p);
+        else
+            d->hist.append(in, p, !registered);
         if (!skipping) {
             j->s_base = d->parse_pos;
             j->epoch = d->epoch;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <atomic>
+#include <deque>
 #include <set>
 #include <string>
 #include <vector>
@@ -80,6 +81,78 @@ struct MsgList {
 
 inline constexpr uint8_t kStreamStart[10] = {0xff, 0x06, 0x00, 0x00, 0x73, 0x4e, 0x61, 0x50, 0x70, 0x59};
 
+// A validating batcher decoder's handed-over stream bytes, as segments in stream order: a reference to
+// a registered cumulation or to the job's copy in its batch's staging arena (both valid while the job
+// that consumed them is unapplied, which is as long as a re-walk can need them; a staging arena may
+// be reallocated while its batch collects, so that reference is the arena's pointer + offset), or an
+// owned copy.
+struct StreamHist {
+    struct Seg {
+        uint64_t pos;
+        const uint8_t* p;
+        size_t n;
+        std::vector<uint8_t> own;
+        uint8_t* const* base = nullptr;  // staging reference: bytes at *base + off
+        uint64_t off = 0;
+        const uint8_t* data() const { return base ? *base + off : p; }
+    };
+    std::deque<Seg> segs;
+    uint64_t end = 0;  // stream position after the last byte handed over
+    void append(const uint8_t* p, size_t n, bool copy) {
+        if (!n) return;
+        Seg s{end, p, n, {}};
+        if (copy) {
+            s.own.assign(p, p + n);
+            s.p = s.own.data();
+        }
+        segs.push_back(std::move(s));
+        end += n;
+    }
+    void append_staged(uint8_t* const* base, uint64_t off, size_t n) {
+        if (!n) return;
+        Seg s{end, nullptr, n, {}, base, off};
+        segs.push_back(std::move(s));
+        end += n;
+    }
+    // [a, end) into `out` (appended)
+    void copy_from(uint64_t a, std::vector<uint8_t>& out) const {
+        for (const Seg& s : segs) {
+            if (s.pos + s.n <= a) continue;
+            const size_t o = a > s.pos ? (size_t)(a - s.pos) : 0;
+            out.insert(out.end(), s.data() + o, s.data() + s.n);
+        }
+    }
+    // Make [a, end) one owned, contiguous segment and return its bytes (a re-walk: what it leaves
+    // carried outlives the jobs whose registered memory it was in).
+    const uint8_t* own_from(uint64_t a) {
+        std::vector<uint8_t> v;
+        copy_from(a, v);
+        while (!segs.empty() && segs.back().pos >= a) segs.pop_back();
+        if (!segs.empty() && segs.back().pos + segs.back().n > a) {  // split the segment holding a
+            Seg& s = segs.back();
+            s.n = (size_t)(a - s.pos);
+            if (!s.own.empty()) s.own.resize(s.n);  // (p stays valid: shrinking keeps the buffer)
+        }
+        Seg t{a, nullptr, v.size(), std::move(v)};
+        t.p = t.own.data();
+        segs.push_back(std::move(t));
+        return segs.back().p;
+    }
+    // bytes at stream position a, contiguous to the end of its segment
+    const uint8_t* at(uint64_t a) const {
+        for (const Seg& s : segs)
+            if (a >= s.pos && a < s.pos + s.n) return s.data() + (a - s.pos);
+        return nullptr;
+    }
+    void drop_before(uint64_t a) {  // whole segments that end at or below a
+        while (!segs.empty() && segs.front().pos + segs.front().n <= a) segs.pop_front();
+    }
+    void clear(uint64_t at_pos) {
+        segs.clear();
+        end = at_pos;
+    }
+};
+
 }  // namespace h
 }  // namespace nx
 
@@ -102,8 +175,7 @@ struct nx_snappy_frame_decoder {
     // which is only known once the chunk is decoded.  So the handed-over byte stream is kept from the
     // first byte a not-yet-applied job walked (absolute positions in the decoder's stream): a leftover
     // found at apply() re-walks it from there.
-    std::vector<uint8_t> hist;         // stream bytes [hist_base, hist_base + hist.size())
-    uint64_t hist_base = 0;
+    nx::h::StreamHist hist;            // stream bytes from the first an unapplied job walked to hist.end
     uint64_t parse_pos = 0;            // the header walk has reached here; [parse_pos, end) is carried into the next submit
     uint64_t epoch = 0;                // bumped by each re-walk: jobs walked under an older epoch deliver nothing
     std::multiset<uint64_t> outstanding;  // walk starts of jobs submitted and not yet applied

@@ -81,5 +81,12 @@ void ws_unhold(WsKind k, int dev);
 // batcher flush of up to 16384 slices / frames runs at full grid.
 constexpr uint32_t kHandleHoldUnits = 1024;
 constexpr uint32_t kBatcherHoldUnits = 16384;
+// A batcher's reservations.  Snappy tables in the DENSE form for 65 536 lanes (8 GiB): a flush of more
+// than kSpreadMaxChunks slices runs lane-per-chunk on 256 blocks, one per CU (the table request rate
+// saturates from ~32 K lanes; 16 640 lanes were only 65 blocks, and a reservation below
+// kSpreadMaxChunks lanes runs one chunk per wave on 4 096 waves).  Records for 65 536 frames (4 GiB), so
+// k_parse's lane-per-frame launch of a sub-batch fills every CU as well.
+constexpr uint32_t kBatcherEncHoldUnits = 65536;
+constexpr uint32_t kBatcherDecHoldUnits = 65536;
 
 }  // namespace nx
