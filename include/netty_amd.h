@@ -354,7 +354,10 @@ int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx_batcher* b
  * caller discards now (the chunk payloads are copied).  Result: the decoded messages in order, then
  * (status < 0) the first failure's message; a failed job marks the decoder corrupted (:227-230).
  * The decoder may be freed (nx_snappy_frame_decoder_free, a handler removed) while its jobs are in
- * flight: each job holds a reference to it until the job's batch is reused or the batcher is freed. */
+ * flight: each job holds a reference to it until the job's batch is reused or the batcher is freed.
+ * A validating decoder whose compressed chunk decodes short (a leftover, SnappyFrameDecoder.java:
+ * 206-212) walks its stream again at apply time: the messages of bytes that later jobs had consumed
+ * arrive on the earlier job's ticket, so read every ticket of a decoder before releasing it. */
 int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
                                        size_t* consumed);
 /* The same for a cumulation in registered memory (a pooled direct buffer the socket read into): the

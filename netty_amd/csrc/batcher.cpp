@@ -793,14 +793,19 @@ void apply(nx_batcher* b, Batch* bt) {
 // Queue the jobs apply() re-walked into the collecting batch (after every job already in it: those of
 // the same decoder were walked before the re-walk and deliver nothing).  The next poll()/wait() launches it.
 void queue_continuations(nx_batcher* b) {
+    // take every moved job out of its batch first, and pin those batches (live) so that none is reset
+    // for reuse below while a job listed here may still go back to it
     for (auto& [j, from] : b->cont) {
-        Batch* to = b->cur ? b->cur : reuse_or_new_batch(b);
-        nx_snappy_frame_decoder* d = j->dec;
         for (size_t k = 0; k < from->jobs.size(); ++k)
             if (from->jobs[k] == j) {
                 from->jobs.erase(from->jobs.begin() + (ptrdiff_t)k);
                 break;
             }
+        from->live += 1;
+    }
+    for (auto& [j, from] : b->cont) {
+        Batch* to = b->cur ? b->cur : reuse_or_new_batch(b);
+        nx_snappy_frame_decoder* d = j->dec;
         auto it = b->tickets.find(j->ticket);
         const bool live = it != b->tickets.end();
         const uint8_t* S = d->hist.at(j->s_base);  // the owned segment rewalk() made, from s_base on
@@ -823,6 +828,7 @@ void queue_continuations(nx_batcher* b) {
         }
         b->kick = true;
     }
+    for (auto& [j, from] : b->cont) from->live -= 1;
     b->cont.clear();
 }
 

@@ -411,3 +411,24 @@ def test_batcher_validating_leftover_registered_autoflush(nx, oracle):
         assert b.stats()["flushes"] > 1
     finally:
         nx.Batcher.unregister(base)
+
+
+def test_batcher_leftover_with_released_tickets(nx, oracle):
+    """Re-walks of two decoders' jobs whose tickets were released before they completed (the caller
+    discarded them): their batch may be reused while the continuations are queued; the batcher stays
+    consistent and later jobs complete."""
+    from netty_amd import _lib
+    L = _lib.load()
+    stream, _, _ = leftover_streams(oracle)[0]
+    b = nx.Batcher()
+    decs = [nx.SnappyFrameDecoder(True) for _ in range(2)]
+    for d in decs:
+        t = b.submit_decode(d, stream)
+        assert L.nx_batcher_release(b._h, t) == 0
+    b.flush()
+    other = nx.SnappyFrameDecoder(True)
+    data = oracle.textgen_chunk(99, 20000)
+    for _ in range(3):  # each submit applies what completed; the continuations go out at poll/wait
+        t = b.submit_decode(other, oracle.snappy_frame_encode(data, started=_ > 0)[0])
+        b.wait(t)
+        assert b"".join(b.result(t)) == data
