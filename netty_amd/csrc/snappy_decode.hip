@@ -268,12 +268,21 @@ struct FrameIO {
     }
 };
 
+// Where k_expand's next record window starts: its first record (relative to this window), the
+// pieces of that record already produced, and the record's output start.
+struct Window {
+    uint32_t rec, pdone, O;
+};
+
 // Expand output [O, E) from the producing tags on lanes `prodm` (lane order = stream order):
 // tag on lane l starts at output position ostart, xv = bit31 copy | offset, or the literal's input
 // position.  Returns false if the round guard tripped (never on valid input: the lowest pending
 // piece always has its producers done).
+// Pieces [0, P0s) are already produced.  `last`: run to the end, the final pass partial; otherwise
+// run only full 64-piece passes and report in *nw where the next window starts (k_expand slides its
+// 64-record window there, so no pass is cut short at a window's end; prodm must be a lane prefix).
 __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t E, bool prod, uint64_t prodm, uint32_t ostart,
-                            uint32_t xv, int lane) {
+                            uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr) {
     WaveLds& L = io.L;
     const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);
     const uint32_t* lds32 = L.ring;  // ring at dwords [0, 1024), stage at [1024, 1280)
@@ -288,7 +297,9 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
     const uint32_t Ptot = ((E + 3u) >> 2) - (O >> 2) + (uint32_t)__popcll(unal & ~first_bit);
     uint32_t rc = 0;   // rank of the last tag started in an earlier pass
     uint32_t pbc = 0;  // its first piece
-    for (uint32_t P0 = 0; P0 < Ptot; P0 += 64u) {
+    // (a non-last window holds >= 64 unproduced pieces: its first record has one, every other one)
+    const uint32_t Pend = last ? Ptot : P0s + ((Ptot - P0s) & ~63u);
+    for (uint32_t P0 = P0s; P0 < Pend; P0 += 64u) {
         // piece -> tag: each tag marks its first piece, then a max-scan over the lanes
         L.scratch[lane] = 0u;
         wave_sync();
@@ -432,6 +443,18 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
         // for those loads (gfx950's vmcnt also counts older stores) rarely waits on a fresh store.
         // Same blocks, one pass earlier; 58.8 -> 57.9 ms per 262 144 frames with the gval change below.
         io.flush_to(pe);
+    }
+    if (!last) {
+        if (Pend == Ptot) {  // the window is done: the next starts at its successor
+            nw->rec = (uint32_t)__popcll(prodm);
+            nw->pdone = 0u;
+            nw->O = E;
+        } else {  // the record holding piece Pend (the last one starting at or before it)
+            const uint32_t idx = (uint32_t)__popcll(__ballot(prod && pbase <= Pend)) - 1u;
+            nw->rec = idx;
+            nw->pdone = Pend - uni((uint32_t)__builtin_amdgcn_readlane((int)pbase, (int)idx));
+            nw->O = uni((uint32_t)__builtin_amdgcn_readlane((int)ostart, (int)idx));
+        }
     }
     return true;
 }
@@ -901,19 +924,22 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
         Frame f{in + in_off[c], in_len[c], out + out_off[c], 0u};
         FrameIO io(*s.L, f, s.sT, s.sSH, do_crc, lane);
         const uint32_t* __restrict__ R = rec + (size_t)c * kRecCap;
-        uint32_t O = 0;
+        // A window of 64 records [b, b + 64) whose first `pdone` pieces are produced; it runs full
+        // 64-piece passes only, then slides to the record holding the first piece left (round 3: the
+        // window's last pass was ~85 % full on average; 456 -> ~370 passes per text frame).
+        uint32_t O = 0;  // output start of record b
+        uint32_t pdone = 0;
         bool primed = false;
-        uint32_t rnext = (uint32_t)lane < N ? R[lane] : 0u;
-        for (uint32_t b = 0; b < N; b += 64u) {
-            const uint32_t r = rnext;
+        uint32_t r = (uint32_t)lane < N ? R[lane] : 0u;
+        for (uint32_t b = 0; b < N;) {
             const bool valid = b + (uint32_t)lane < N;
             const bool isc = (r >> 31) != 0u;
             const uint32_t len = valid ? ((r >> 25) & 63u) + 1u : 0u;
-            // Issue the next batch's prefetch only after this batch's records are in use: vmcnt counts
+            // Issue the next window's prefetch only after this window's records are in use: vmcnt counts
             // in order, so a wait for `r` placed after the new load also waited for the new load
-            // (a memory latency per batch; 57.8 -> 57.0 ms per 262 144 frames).
+            // (a memory latency per window; 57.8 -> 57.0 ms per 262 144 frames).
             asm volatile("" ::"v"(len) : "memory");
-            rnext = b + 64u + (uint32_t)lane < N ? R[b + 64u + lane] : 0u;  // prefetch the next batch
+            const uint32_t rnext = b + 64u + (uint32_t)lane < N ? R[b + 64u + lane] : 0u;  // records [b + 64, b + 128)
             const uint32_t x = r & 0x1FFFFFFu;
             const uint32_t incl = incl_scan(len);
             const uint32_t ostart = O + incl - len;
@@ -931,11 +957,24 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
                 wave_sync();  // stage bytes written by other lanes
             }
             const uint32_t xv = isc ? (0x80000000u | x) : x;
-            if (!expand_tags(io, s.lds_base, O, E, valid, __ballot(valid), ostart, xv, lane)) {
+            const bool last = b + 64u >= N;
+            Window nw{0u, 0u, 0u};
+            if (!expand_tags(io, s.lds_base, O, E, valid, __ballot(valid), ostart, xv, lane, pdone, last, &nw)) {
                 st = kGuardTrip + 2;
                 break;
             }
-            O = E;
+            if (last) {
+                O = E;
+                break;
+            }
+            // slide: the new window's lane l takes record b + nw.rec + l, from this window or the prefetch
+            const uint32_t src = (uint32_t)lane + nw.rec;
+            const uint32_t from_r = (uint32_t)__shfl((int)r, (int)(src & 63u));
+            const uint32_t from_n = (uint32_t)__shfl((int)rnext, (int)(src & 63u));
+            r = src < 64u ? from_r : from_n;
+            b += nw.rec;
+            pdone = nw.pdone;
+            O = nw.O;
         }
         if (st == kGuardTrip + 2) O = Ofin;  // unreachable on a consistent record stream
         const uint32_t crc = io.finish(O, &tabs->NS[0][0][0]);
