@@ -1,0 +1,44 @@
+"""Per-frame pass / round counters of k_expand from a diagnostic build (netty_amd/build_variants/
+mk_stats.py adds them; the product library has no such symbol).
+
+    python scripts/dec_stats.py [chunks]
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from netty_amd import batch as B
+    from netty_amd import _lib
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    L = 65536
+    dev = torch.device("cuda:0")
+    src = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    B.textgen(src, 0, n, L)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * L
+    ln = torch.full((n,), L, dtype=torch.int32, device=dev)
+    cap = (B.snappy_max_compressed_length(L) + 15) // 16 * 16
+    enc = torch.empty(n * cap, dtype=torch.uint8, device=dev)
+    eoff = torch.arange(n, dtype=torch.int64, device=dev) * cap
+    elen, est = B.snappy_encode(src, off, ln, enc, eoff)
+    crc = B.crc32c_masked(src, off, ln)
+    lib = C.CDLL(_lib.LIB_PATH)
+    buf = (C.c_ulonglong * 8)()
+    lib.nx_dec_stats_read(buf)  # reset
+    dec = torch.empty_like(src)
+    r = B.snappy_decode(enc, eoff, elen, dec, off, expected_crc=crc)
+    torch.cuda.synchronize()
+    assert lib.nx_dec_stats_read(buf) == 0
+    names = ["windows", "passes", "rounds", "map_passes", "far_or_unstaged_passes", "overlap_passes", "-", "pieces"]
+    ok = bool(torch.equal(dec, src)) and int((r["status"] != 0).sum()) == 0
+    print(json.dumps({"chunks": n, "verified": ok, "per_frame": {k: round(buf[i] / n, 2) for i, k in enumerate(names) if k != "-"}}))
+
+
+if __name__ == "__main__":
+    main()
