@@ -1,5 +1,5 @@
-"""Per-frame pass / round counters of k_expand from a diagnostic build (netty_amd/build_variants/
-mk_stats.py adds them; the product library has no such symbol).
+"""Per-frame pass / round counters of k_expand from a diagnostic build (scripts/mk_dec_stats.py
+adds them; the product library has no such symbol).
 
     python scripts/dec_stats.py [chunks]
 """
