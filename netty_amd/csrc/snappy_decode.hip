@@ -80,6 +80,8 @@ static_assert(2 * (kTabBytes + kWaves * sizeof(WaveLds)) <= 160 * 1024, "two wor
 typedef uint32_t __attribute__((aligned(1))) u32u;
 typedef __attribute__((address_space(1))) const uint8_t gu8;
 typedef __attribute__((address_space(1))) const u32u gu32u;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4u gv4u;
 
 __device__ __forceinline__ uint32_t shift_byte_tab(const uint32_t* __restrict__ S, uint32_t c) {
     return S[c & 0xFF] ^ S[256 + ((c >> 8) & 0xFF)] ^ S[512 + ((c >> 16) & 0xFF)] ^ S[768 + (c >> 24)];
@@ -723,17 +725,25 @@ struct BurstWinT {
         const uint32_t q = p + pad;
         return q >= base && (q + 5u <= base + kBytes || base + kBytes >= end);
     }
+    // (called with p inside the chunk, so end >= 1).  Every block is loaded, those wholly past the
+    // end from the last block that holds a chunk byte instead (their bytes are unspecified), so the
+    // NB loads issue back to back and the lane waits once; a guarded load per block made the
+    // compiler wait after each one (NB memory latencies per burst).
     __device__ __forceinline__ void load(uint32_t p) {
         base = (p + pad) & ~15u;
+        const uint32_t last = (end - 1u) & ~15u;
+        v4u x[NB];
 #pragma unroll
         for (uint32_t k = 0; k < NB; ++k) {
-            if (base + 16u * k < end) {
-                const uint4 x = *reinterpret_cast<const uint4*>(origin + base + 16u * k);
-                w[4 * k] = x.x;
-                w[4 * k + 1] = x.y;
-                w[4 * k + 2] = x.z;
-                w[4 * k + 3] = x.w;
-            }
+            const uint32_t o = base + 16u * k;
+            x[k] = *(const gv4u*)(origin + (o <= last ? o : last));
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < NB; ++k) {
+            w[4 * k] = x[k].x;
+            w[4 * k + 1] = x[k].y;
+            w[4 * k + 2] = x[k].z;
+            w[4 * k + 3] = x[k].w;
         }
     }
     // 8 bytes at chunk position p, has(p) (bytes at or past the chunk end are unspecified)
