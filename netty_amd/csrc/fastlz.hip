@@ -33,6 +33,26 @@ __device__ __forceinline__ int32_t hashf(const uint8_t* in, int32_t o, int32_t l
     return v & HASH_MASK;
 }
 
+typedef uint32_t __attribute__((aligned(1))) u32u;
+typedef uint64_t __attribute__((aligned(1))) u64u;
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const u32u*>(p); }
+__device__ __forceinline__ uint64_t ld64(const uint8_t* p) { return *reinterpret_cast<const u64u*>(p); }
+
+// hashFunction at o from the dword w = bytes o..o+3 (readU16's limit applied per half)
+__device__ __forceinline__ int32_t hash_w(uint32_t w, int32_t o, int32_t lim) {
+    const int32_t b0 = (int32_t)(w & 0xFFu), b1 = (int32_t)((w >> 8) & 0xFFu), b2 = (int32_t)((w >> 16) & 0xFFu);
+    int32_t v = o + 1 >= lim ? b0 : (b1 << 8) | b0;
+    const int32_t u = o + 2 >= lim ? b1 : (b2 << 8) | b1;
+    v ^= u ^ (v >> (16 - HASH_LOG));
+    return v & HASH_MASK;
+}
+
+// The serial matcher of FastLz.compress (FastLz.java:96-399) with its reads batched: the hash and
+// the literal byte come from one dword load, the first 3 (level-2 far: 5) bytes of a candidate are
+// compared as one word, matches extend 8 bytes per compare (first mismatch by count-trailing-zeros,
+// stopping where Java's byte loop stops: at ipBound, or one past the mismatch), and the table probe
+// (read the slot, store the anchor) is one atomic exchange.  Positions near the chunk end, where a
+// word load could pass it, take Java's byte reads.
 template <class O>
 __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O& out, int32_t proposedLevel,
                             int32_t lim, uint32_t* __restrict__ htab, uint32_t stamp) {
@@ -43,8 +63,8 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
     int32_t op = 0;
     int32_t copy;
     const uint32_t stag = stamp << 16;
-#define HGET(h) ((htab[(h)] & 0xFFFF0000u) == stag ? (int32_t)(htab[(h)] & 0xFFFFu) : 0)
-#define HSET(h, v) (htab[(h)] = stag | (uint32_t)(v))
+#define HREF(e) (((e) & 0xFFFF0000u) == stag ? (int32_t)((e) & 0xFFFFu) : 0)
+#define HSET(h, v) __hip_atomic_store(htab + (h), stag | (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
     if (inLength < 4) {
         if (inLength != 0) {
             out.set(op++, (uint8_t)(inLength - 1));
@@ -59,14 +79,19 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
     out.set(op++, MAX_COPY - 1);
     out.set(op++, in[ip++]);
     out.set(op++, in[ip++]);
-    while (ip < ipLimit) {
-        int32_t ref = 0;
-        int64_t distance = 0;
+    while (ip < ipLimit) {  // ip + 12 < inLength: word loads at ip - 1 .. ip + 8 stay in the chunk
+        int32_t ref;
+        int64_t distance;
         int32_t len = 3;
-        int32_t anchor = ip;
+        const int32_t anchor = ip;
+        const uint32_t w = ld32(in + ip);
         bool matchLabel = false;
         if (level == 2) {
-            if (in[ip] == in[ip - 1] && read_u16(in, ip - 1, lim) == read_u16(in, ip + 1, lim)) {
+            const uint32_t wm = ld32(in + ip - 1);  // bytes ip-1 .. ip+2
+            const uint32_t c0 = wm & 0xFFu, c1 = (wm >> 8) & 0xFFu, c2 = (wm >> 16) & 0xFFu, c3 = wm >> 24;
+            const uint32_t ua = ip >= lim ? c0 : (c1 << 8) | c0;       // readU16(ip - 1)
+            const uint32_t ub = ip + 2 >= lim ? c2 : (c3 << 8) | c2;   // readU16(ip + 1)
+            if (c1 == c0 && ua == ub) {
                 distance = 1;
                 ip += 3;
                 ref = anchor + (3 - 1);
@@ -74,32 +99,20 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
             }
         }
         if (!matchLabel) {
-            const int32_t hval = hashf(in, ip, lim);
-            ref = HGET(hval);
+            const int32_t hval = hash_w(w, ip, lim);
+            const uint32_t e = __hip_atomic_exchange(htab + hval, stag | (uint32_t)anchor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ref = HREF(e);
             distance = anchor - ref;
-            HSET(hval, anchor);
-            bool lit = false;
-            if (distance == 0 || (level == 1 ? distance >= MAX_DISTANCE : distance >= MAX_FARDISTANCE)) {
-                lit = true;
-            } else if (in[ref++] != in[ip++]) {
-                lit = true;
-            } else if (in[ref++] != in[ip++]) {
-                lit = true;
-            } else if (in[ref++] != in[ip++]) {
-                lit = true;
-            }
-            if (!lit && level == 2 && distance >= MAX_DISTANCE) {
-                if (in[ip++] != in[ref++]) {
-                    lit = true;
-                } else if (in[ip++] != in[ref++]) {
-                    lit = true;
-                } else {
-                    len += 2;
-                }
+            bool lit = distance == 0 || (level == 1 ? distance >= MAX_DISTANCE : distance >= MAX_FARDISTANCE);
+            if (!lit) {
+                const bool far = level == 2 && distance >= MAX_DISTANCE;  // far: 5 bytes must match
+                const uint64_t x = ld64(in + ref) ^ ld64(in + anchor);
+                lit = (x & (far ? 0xFFFFFFFFFFull : 0xFFFFFFull)) != 0ull;
+                if (far) len += 2;
             }
             if (lit) {
-                out.set(op++, in[anchor++]);
-                ip = anchor;
+                out.set(op++, w & 0xFFu);  // in[anchor]
+                ip = anchor + 1;
                 copy++;
                 if (copy == MAX_COPY) {
                     copy = 0;
@@ -107,26 +120,61 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
                 }
                 continue;
             }
+            ref += len;
         }
         ip = anchor + len;
         distance--;
         if (distance == 0) {
-            const uint8_t x = in[ip - 1];
-            while (ip < ipBound) {
-                if (in[ref++] != x) break;
-                ip++;
-            }
-        } else {
-            bool missMatch = false;
-            for (int i = 0; i < 8; i++) {
-                if (in[ref++] != in[ip++]) {
-                    missMatch = true;
+            // a run of x = in[ip - 1]: Java compares in[ip - 1] and steps ip while it equals x and
+            // ip < ipBound, so ip ends at (first position >= ip - 1 holding another byte) + 1, or ipBound
+            const uint32_t x = in[ip - 1];
+            const uint64_t x8 = (uint64_t)x * 0x0101010101010101ull;
+            for (;;) {
+                if (ip >= ipBound) break;
+                const int32_t p = ip - 1;
+                if (p + 8 > inLength) {
+                    while (ip < ipBound && in[ip - 1] == x) ip++;
                     break;
                 }
+                const uint64_t d = ld64(in + p) ^ x8;
+                const int32_t k = d ? (int32_t)(__builtin_ctzll(d) >> 3) : 8;
+                const int32_t room = ipBound - ip;
+                if (k < 8 || room <= 8) {
+                    ip += k < room ? k : room;
+                    break;
+                }
+                ip += 8;
             }
-            if (!missMatch) {
-                while (ip < ipBound) {
-                    if (in[ref++] != in[ip++]) break;
+        } else {
+            // the first 8 bytes unconditionally (ip + 8 <= inLength here), then until ipBound; ip ends
+            // one past the first mismatch, or at ipBound (or at ip + 8 when that is already past it)
+            const uint64_t x0 = ld64(in + ref) ^ ld64(in + ip);
+            if (x0) {
+                ip += (int32_t)(__builtin_ctzll(x0) >> 3) + 1;
+            } else {
+                ip += 8;
+                ref += 8;
+                for (;;) {
+                    if (ip >= ipBound) break;
+                    if (ip + 8 > inLength) {
+                        while (ip < ipBound) {
+                            if (in[ref++] != in[ip++]) break;
+                        }
+                        break;
+                    }
+                    const uint64_t x = ld64(in + ref) ^ ld64(in + ip);
+                    const int32_t k = x ? (int32_t)(__builtin_ctzll(x) >> 3) : 8;
+                    const int32_t room = ipBound - ip;
+                    if (k < 8 && k < room) {
+                        ip += k + 1;
+                        break;
+                    }
+                    if (room <= 8) {
+                        ip = ipBound;
+                        break;
+                    }
+                    ip += 8;
+                    ref += 8;
                 }
             }
         }
@@ -183,12 +231,12 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
                 out.set(op++, (uint8_t)(distance & 255));
             }
         }
-        int32_t hv = hashf(in, ip, lim);
-        HSET(hv, ip);
-        ip++;
-        hv = hashf(in, ip, lim);
-        HSET(hv, ip);
-        ip++;
+        // the two positions after the match (readU16 may reach past the chunk end here: bytes)
+        for (int t = 0; t < 2; ++t) {
+            const int32_t hv = ip + 4 <= inLength ? hash_w(ld32(in + ip), ip, lim) : hashf(in, ip, lim);
+            HSET(hv, ip);
+            ip++;
+        }
         out.set(op++, MAX_COPY - 1);
     }
     ipBound++;
@@ -206,7 +254,7 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
         op--;
     }
     if (level == 2) out.set(0, out.get(0) | (1u << 5));
-#undef HGET
+#undef HREF
 #undef HSET
     out.finish(op);
     return op;

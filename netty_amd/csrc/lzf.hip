@@ -19,6 +19,11 @@ constexpr int32_t MAX_OFF = 8192;
 constexpr int32_t MAX_REF = 264;
 constexpr int32_t MAX_LIT = 32;
 
+typedef uint32_t __attribute__((aligned(1))) u32u;
+typedef uint64_t __attribute__((aligned(1))) u64u;
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const u32u*>(p); }
+__device__ __forceinline__ uint64_t ld64(const uint8_t* p) { return *reinterpret_cast<const u64u*>(p); }
+
 // ChunkEncoder.hash: Java int multiply (wraps), arithmetic shift
 __device__ __forceinline__ uint32_t jhash(int32_t h) { return (uint32_t)(((int32_t)((uint32_t)h * 57321u) >> 9) & (HSIZE - 1)); }
 __device__ __forceinline__ int32_t first2(const uint8_t* in, int32_t p) {  // ChunkEncoder.first: (in[p] << 8) + (in[p+1] & 0xFF), in[p] signed
@@ -42,12 +47,13 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& o
         const uint8_t p2 = in[ip + 2];
         seen = (int32_t)(((uint32_t)seen << 8) + p2);
         const uint32_t h = jhash(seen);
-        const uint32_t e = htab[h];
+        // read the slot and store this position: one atomic exchange
+        const uint32_t e = __hip_atomic_exchange(htab + h, stag | (uint32_t)(ip + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int32_t ref = ((e & 0xFFFF0000u) == stag) ? (int32_t)(e & 0xFFFFu) - 1 : 0;
-        htab[h] = stag | (uint32_t)(ip + 1);
         int32_t off = ip - ref;
-        if (ref < 0 || ref >= ip || off > MAX_OFF || in[ref + 2] != p2 || in[ref + 1] != (uint8_t)(seen >> 8) ||
-            in[ref] != (uint8_t)(seen >> 16)) {
+        // the 3-byte check as one word compare (ref + 3 <= ip + 2 < n)
+        const uint32_t tri = (((uint32_t)seen >> 16) & 0xFFu) | ((uint32_t)seen & 0xFF00u) | ((uint32_t)p2 << 16);
+        if (ref < 0 || ref >= ip || off > MAX_OFF || ((ld32(in + ref) ^ tri) & 0xFFFFFFu) != 0u) {
             out.set(7 + op++, in[ip++]);
             if (++lit == MAX_LIT) {
                 out.set(7 + op - 33, 31);
@@ -65,7 +71,15 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& o
             lit = 0;
         }
         int32_t len = 3;
-        while (len < maxLen && in[ref + len] == in[ip + len]) len++;
+        // extend 8 bytes per compare while the words stay inside the chunk, then byte by byte
+        while (len < maxLen && ip + len + 8 <= n) {
+            const uint64_t x = ld64(in + ref + len) ^ ld64(in + ip + len);
+            const int32_t k = x ? (int32_t)(__builtin_ctzll(x) >> 3) : 8;
+            len = len + k < maxLen ? len + k : maxLen;
+            if (k < 8) break;
+        }
+        if (len < maxLen && ip + len + 8 > n)
+            while (len < maxLen && in[ref + len] == in[ip + len]) len++;
         len -= 2;
         --off;
         if (len < 7) {
@@ -79,10 +93,10 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& o
         ip += len;  // matchEnd - 2 (<= n - 4)
         seen = first2(in, ip);
         seen = (int32_t)(((uint32_t)seen << 8) + in[ip + 2]);
-        htab[jhash(seen)] = stag | (uint32_t)(ip + 1);
+        __hip_atomic_store(htab + jhash(seen), stag | (uint32_t)(ip + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ++ip;
         seen = (int32_t)(((uint32_t)seen << 8) + in[ip + 2]);
-        htab[jhash(seen)] = stag | (uint32_t)(ip + 1);
+        __hip_atomic_store(htab + jhash(seen), stag | (uint32_t)(ip + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ++ip;
     }
     while (ip < n) {  // handleTail
