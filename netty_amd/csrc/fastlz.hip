@@ -53,18 +53,20 @@ __device__ __forceinline__ int32_t hash_w(uint32_t w, int32_t o, int32_t lim) {
 // stopping where Java's byte loop stops: at ipBound, or one past the mismatch), and the table probe
 // (read the slot, store the anchor) is one atomic exchange.  Positions near the chunk end, where a
 // word load could pass it, take Java's byte reads.
+// Table entries are 64-bit: stamp[63:48] | position[47:32] | the 4 bytes at the position[31:0], so
+// the 3-byte candidate check reads no input (a level-2 far candidate loads its 5th byte).
 template <class O>
 __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O& out, int32_t proposedLevel,
-                            int32_t lim, uint32_t* __restrict__ htab, uint32_t stamp) {
+                            int32_t lim, uint64_t* __restrict__ htab, uint32_t stamp) {
     const int32_t level = proposedLevel == 0 ? (inLength < 65536 ? 1 : 2) : proposedLevel;
     int32_t ip = 0;
     int32_t ipBound = ip + inLength - 2;
     const int32_t ipLimit = ip + inLength - 12;
     int32_t op = 0;
     int32_t copy;
-    const uint32_t stag = stamp << 16;
-#define HREF(e) (((e) & 0xFFFF0000u) == stag ? (int32_t)((e) & 0xFFFFu) : 0)
-#define HSET(h, v) __hip_atomic_store(htab + (h), stag | (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+    const uint64_t stag = (uint64_t)stamp << 48;
+#define HENT(pos, w) (stag | ((uint64_t)(uint32_t)(pos) << 32) | (uint64_t)(w))
+#define HSET(h, pos, w) __hip_atomic_store(htab + (h), HENT(pos, w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
     if (inLength < 4) {
         if (inLength != 0) {
             out.set(op++, (uint8_t)(inLength - 1));
@@ -79,6 +81,8 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
     out.set(op++, MAX_COPY - 1);
     out.set(op++, in[ip++]);
     out.set(op++, in[ip++]);
+    // Java's fresh table reads position 0 everywhere: a stale entry is position 0 and its bytes
+    const uint32_t w_zero = ld32(in);  // inLength >= 4 here
     while (ip < ipLimit) {  // ip + 12 < inLength: word loads at ip - 1 .. ip + 8 stay in the chunk
         int32_t ref;
         int64_t distance;
@@ -100,15 +104,18 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
         }
         if (!matchLabel) {
             const int32_t hval = hash_w(w, ip, lim);
-            const uint32_t e = __hip_atomic_exchange(htab + hval, stag | (uint32_t)anchor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ref = HREF(e);
+            const uint64_t e = __hip_atomic_exchange(htab + hval, HENT(anchor, w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool fresh = (e & 0xFFFF000000000000ull) == stag;
+            ref = fresh ? (int32_t)((e >> 32) & 0xFFFFu) : 0;
+            const uint32_t rw = fresh ? (uint32_t)e : w_zero;  // the bytes at ref
             distance = anchor - ref;
             bool lit = distance == 0 || (level == 1 ? distance >= MAX_DISTANCE : distance >= MAX_FARDISTANCE);
             if (!lit) {
-                const bool far = level == 2 && distance >= MAX_DISTANCE;  // far: 5 bytes must match
-                const uint64_t x = ld64(in + ref) ^ ld64(in + anchor);
-                lit = (x & (far ? 0xFFFFFFFFFFull : 0xFFFFFFull)) != 0ull;
-                if (far) len += 2;
+                lit = ((rw ^ w) & 0xFFFFFFu) != 0u;
+                if (!lit && level == 2 && distance >= MAX_DISTANCE) {  // far: 5 bytes must match
+                    lit = (rw >> 24) != (w >> 24) || in[ref + 4] != in[anchor + 4];
+                    len += 2;
+                }
             }
             if (lit) {
                 out.set(op++, w & 0xFFu);  // in[anchor]
@@ -232,9 +239,12 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
             }
         }
         // the two positions after the match (readU16 may reach past the chunk end here: bytes)
+        // (an entry there is never probed again in this chunk, so its bytes may stay 0)
         for (int t = 0; t < 2; ++t) {
-            const int32_t hv = ip + 4 <= inLength ? hash_w(ld32(in + ip), ip, lim) : hashf(in, ip, lim);
-            HSET(hv, ip);
+            const bool inside = ip + 4 <= inLength;
+            const uint32_t wi = inside ? ld32(in + ip) : 0u;
+            const int32_t hv = inside ? hash_w(wi, ip, lim) : hashf(in, ip, lim);
+            HSET(hv, ip, wi);
             ip++;
         }
         out.set(op++, MAX_COPY - 1);
@@ -254,7 +264,7 @@ __device__ int32_t compress(const uint8_t* __restrict__ in, int32_t inLength, O&
         op--;
     }
     if (level == 2) out.set(0, out.get(0) | (1u << 5));
-#undef HREF
+#undef HENT
 #undef HSET
     out.finish(op);
     return op;
@@ -355,11 +365,11 @@ __global__ void __launch_bounds__(256) k_compress(const uint8_t* __restrict__ in
                                                   const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                   const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
                                                   const int32_t* __restrict__ level, const int32_t* __restrict__ lim,
-                                                  int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ ws,
+                                                  int32_t* __restrict__ status, uint32_t n, uint64_t* __restrict__ ws,
                                                   uint32_t stamp_base) {
     uint32_t tid, nthreads;
     if (!chunk_slot<SPREAD>(tid, nthreads)) return;
-    uint32_t* htab = ws + (size_t)tid * HASH_SIZE;
+    uint64_t* htab = ws + (size_t)tid * HASH_SIZE;
     uint8_t* slot = nullptr;
     if constexpr (!SPREAD) {
         __shared__ __attribute__((aligned(16))) uint8_t stages[256 * kStageStride];
@@ -474,7 +484,7 @@ __global__ void __launch_bounds__(256) k_adler32(const uint8_t* __restrict__ in,
 }  // namespace nx
 
 #include "workspace.hpp"
-static_assert(nx::kWsSpec[(int)nx::WsKind::FastLzEnc].entry_bytes == sizeof(uint32_t) &&
+static_assert(nx::kWsSpec[(int)nx::WsKind::FastLzEnc].entry_bytes == sizeof(uint64_t) &&
                   (int)nx::kWsSpec[(int)nx::WsKind::FastLzEnc].lg == nx::flz::HASH_LOG,
               "FastLZ table geometry");
 
@@ -487,12 +497,12 @@ extern "C" int32_t nx_fastlz_compress_batch(const uint8_t* in, const uint64_t* i
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const hipStream_t st = (hipStream_t)stream;
-    const size_t per = (size_t)nx::flz::HASH_SIZE * sizeof(uint32_t);
+    const size_t per = (size_t)nx::flz::HASH_SIZE * sizeof(uint64_t);
     nx::WsLease lease(nx::WsKind::FastLzEnc, dev, st);
     NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::FastLzEnc, n, cus)));
     nx::SharedWs& W = lease.ws();
     const nx::LaneGrid g = nx::ws_grid(nx::WsKind::FastLzEnc, n, cus, W.slots);
-    uint32_t* ws = static_cast<uint32_t*>(W.p);
+    uint64_t* ws = static_cast<uint64_t*>(W.p);
     const uint32_t iters = (uint32_t)((n + g.slots - 1) / g.slots);
     if ((uint64_t)W.stamp + iters >= 65535u) {
         NX_HIP_CHECK(hipMemsetAsync(ws, 0, W.slots * per, st));
