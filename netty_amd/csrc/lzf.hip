@@ -37,9 +37,14 @@ __device__ __forceinline__ int32_t first2(const uint8_t* in, int32_t p) {  // Ch
 // (or a never-written slot) can never pass the 3-byte check (oracle/netty_oracle.c, above
 // lzf_try_compress; tests/test_oracle_kat.py::test_lzf_encoder_state_across_messages).
 // The body goes to output positions 7.. (after the LZFChunk header, written last).
+// Entries are 64-bit: that word in the high half, the 3 bytes at the position in the low one, so the
+// candidate check reads no input.
 template <class O>
-__device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& out, uint32_t* __restrict__ htab, uint32_t stamp) {
+__device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& out, uint64_t* __restrict__ htab, uint32_t stamp) {
     const uint32_t stag = stamp << 16;
+    const uint32_t tri_zero = (uint32_t)in[0] | ((uint32_t)in[1] << 8) | ((uint32_t)in[2] << 16);  // a stale entry: position 0
+#define LENT(pos1, tri) (((uint64_t)(stag | (uint32_t)(pos1)) << 32) | (uint64_t)(tri))
+#define LTRI(sv) ((((uint32_t)(sv) >> 16) & 0xFFu) | ((uint32_t)(sv) & 0xFF00u) | (((uint32_t)(sv) & 0xFFu) << 16))
     const int32_t inEnd = n - 4;
     int32_t ip = 0, op = 1, lit = 0;
     int32_t seen = first2(in, 0);
@@ -47,13 +52,15 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& o
         const uint8_t p2 = in[ip + 2];
         seen = (int32_t)(((uint32_t)seen << 8) + p2);
         const uint32_t h = jhash(seen);
+        const uint32_t tri = LTRI(seen);  // bytes ip .. ip+2
         // read the slot and store this position: one atomic exchange
-        const uint32_t e = __hip_atomic_exchange(htab + h, stag | (uint32_t)(ip + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int32_t ref = ((e & 0xFFFF0000u) == stag) ? (int32_t)(e & 0xFFFFu) - 1 : 0;
+        const uint64_t e64 = __hip_atomic_exchange(htab + h, LENT(ip + 1, tri), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t e = (uint32_t)(e64 >> 32);
+        const bool fresh = (e & 0xFFFF0000u) == stag;
+        const int32_t ref = fresh ? (int32_t)(e & 0xFFFFu) - 1 : 0;
+        const uint32_t rtri = fresh ? (uint32_t)e64 : tri_zero;  // the bytes at ref
         int32_t off = ip - ref;
-        // the 3-byte check as one word compare (ref + 3 <= ip + 2 < n)
-        const uint32_t tri = (((uint32_t)seen >> 16) & 0xFFu) | ((uint32_t)seen & 0xFF00u) | ((uint32_t)p2 << 16);
-        if (ref < 0 || ref >= ip || off > MAX_OFF || ((ld32(in + ref) ^ tri) & 0xFFFFFFu) != 0u) {
+        if (ref < 0 || ref >= ip || off > MAX_OFF || ((rtri ^ tri) & 0xFFFFFFu) != 0u) {
             out.set(7 + op++, in[ip++]);
             if (++lit == MAX_LIT) {
                 out.set(7 + op - 33, 31);
@@ -93,10 +100,10 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& o
         ip += len;  // matchEnd - 2 (<= n - 4)
         seen = first2(in, ip);
         seen = (int32_t)(((uint32_t)seen << 8) + in[ip + 2]);
-        __hip_atomic_store(htab + jhash(seen), stag | (uint32_t)(ip + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(htab + jhash(seen), LENT(ip + 1, LTRI(seen)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ++ip;
         seen = (int32_t)(((uint32_t)seen << 8) + in[ip + 2]);
-        __hip_atomic_store(htab + jhash(seen), stag | (uint32_t)(ip + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(htab + jhash(seen), LENT(ip + 1, LTRI(seen)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ++ip;
     }
     while (ip < n) {  // handleTail
@@ -112,12 +119,14 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& o
     } else {
         op--;
     }
+#undef LENT
+#undef LTRI
     return op;
 }
 
 // One LZFChunk.  Writes the compressed body at out+7 first; falls back to a raw block.
 template <class O>
-__device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t n, O& out, uint32_t* htab, uint32_t stamp) {
+__device__ uint32_t encode_chunk(const uint8_t* __restrict__ in, int32_t n, O& out, uint64_t* htab, uint32_t stamp) {
     if (n >= 16) {
         const int32_t clen = compress_body(in, n, out, htab, stamp);
         if (clen + 7 < n + 5) {
@@ -177,10 +186,10 @@ template <bool SPREAD>
 __global__ void __launch_bounds__(256) k_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                 const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                 const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
-                                                int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ ws, uint32_t stamp_base) {
+                                                int32_t* __restrict__ status, uint32_t n, uint64_t* __restrict__ ws, uint32_t stamp_base) {
     uint32_t tid, nthreads;
     if (!chunk_slot<SPREAD>(tid, nthreads)) return;
-    uint32_t* htab = ws + (size_t)tid * HSIZE;
+    uint64_t* htab = ws + (size_t)tid * HSIZE;
     uint8_t* slot = nullptr;
     if constexpr (!SPREAD) {
         __shared__ __attribute__((aligned(16))) uint8_t stages[256 * kStageStride];
@@ -224,7 +233,7 @@ __global__ void __launch_bounds__(256) k_decode_finish(const uint8_t* __restrict
 }  // namespace nx
 
 #include "workspace.hpp"
-static_assert(nx::kWsSpec[(int)nx::WsKind::LzfEnc].entry_bytes == sizeof(uint32_t) &&
+static_assert(nx::kWsSpec[(int)nx::WsKind::LzfEnc].entry_bytes == sizeof(uint64_t) &&
                   (1 << nx::kWsSpec[(int)nx::WsKind::LzfEnc].lg) == nx::lzf::HSIZE,
               "LZF table geometry");
 
@@ -236,12 +245,12 @@ extern "C" int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const hipStream_t st = (hipStream_t)stream;
-    const size_t per = (size_t)nx::lzf::HSIZE * sizeof(uint32_t);
+    const size_t per = (size_t)nx::lzf::HSIZE * sizeof(uint64_t);
     nx::WsLease lease(nx::WsKind::LzfEnc, dev, st);
     NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::LzfEnc, n, cus)));
     nx::SharedWs& W = lease.ws();
     const nx::LaneGrid g = nx::ws_grid(nx::WsKind::LzfEnc, n, cus, W.slots);
-    uint32_t* ws = static_cast<uint32_t*>(W.p);
+    uint64_t* ws = static_cast<uint64_t*>(W.p);
     const uint32_t iters = (uint32_t)((n + g.slots - 1) / g.slots);
     if ((uint64_t)W.stamp + iters >= 65535u) {
         NX_HIP_CHECK(hipMemsetAsync(ws, 0, W.slots * per, st));
