@@ -48,8 +48,12 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& o
     const int32_t inEnd = n - 4;
     int32_t ip = 0, op = 1, lit = 0;
     int32_t seen = first2(in, 0);
+    int32_t pfp = -1;  // the byte at pfp was loaded one step ahead (a literal step moves ip by one)
+    uint32_t pfv = 0;
     while (ip < inEnd) {
-        const uint8_t p2 = in[ip + 2];
+        const uint32_t p2 = pfp == ip + 2 ? pfv : (uint32_t)in[ip + 2];
+        pfv = in[ip + 3];  // ip + 3 < n
+        pfp = ip + 3;
         seen = (int32_t)(((uint32_t)seen << 8) + p2);
         const uint32_t h = jhash(seen);
         const uint32_t tri = LTRI(seen);  // bytes ip .. ip+2
@@ -61,7 +65,8 @@ __device__ int32_t compress_body(const uint8_t* __restrict__ in, int32_t n, O& o
         const uint32_t rtri = fresh ? (uint32_t)e64 : tri_zero;  // the bytes at ref
         int32_t off = ip - ref;
         if (ref < 0 || ref >= ip || off > MAX_OFF || ((rtri ^ tri) & 0xFFFFFFu) != 0u) {
-            out.set(7 + op++, in[ip++]);
+            out.set(7 + op++, tri & 0xFFu);  // in[ip]
+            ip++;
             if (++lit == MAX_LIT) {
                 out.set(7 + op - 33, 31);
                 lit = 0;
