@@ -47,37 +47,48 @@ __device__ __forceinline__ uint32_t put_len(O& out, uint32_t op, uint32_t v) {  
 
 // Large == false: blocks < 65547 bytes, entries stamp << 16 | index.  Large == true: blocks of up
 // to 32 MiB, raw indices in a table the lane zeroes before and after the block.
+// Entries are 64-bit: that word in the high half and the 4 bytes at the index in the low half, so
+// the candidate's 4-byte check reads no input (an entry that reads as index 0 — stale, zeroed or
+// position 0 itself — is checked against the block's first 4 bytes).
 template <bool Large, class O>
-__device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, O& out, uint32_t* __restrict__ table, uint32_t stamp) {
+__device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, O& out, uint64_t* __restrict__ table, uint32_t stamp) {
     const uint32_t stag = stamp << 16;
 #define XCH(h, v) __hip_atomic_exchange(table + (h), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #define PUT(h, v) __hip_atomic_store(table + (h), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-#define ENT(i) (Large ? (uint32_t)(i) : (stag | (uint32_t)(i)))
-    auto idx = [stag](uint32_t e) -> int32_t { return Large ? (int32_t)e : ((e & 0xFFFF0000u) == stag ? (int32_t)(e & 0xFFFFu) : 0); };
+#define ENT(i, w) (((uint64_t)(Large ? (uint32_t)(i) : (stag | (uint32_t)(i))) << 32) | (uint64_t)(w))
+    auto idx = [stag](uint64_t e64) -> int32_t {
+        const uint32_t e = (uint32_t)(e64 >> 32);
+        return Large ? (int32_t)e : ((e & 0xFFFF0000u) == stag ? (int32_t)(e & 0xFFFFu) : 0);
+    };
+    const uint32_t w_zero = n >= 4 ? ld32(in) : 0u;
+    auto bytes_at = [w_zero](uint64_t e64, int32_t i) -> uint32_t { return i == 0 ? w_zero : (uint32_t)e64; };
     if (Large)
-        for (uint32_t k = 0; k < 4096u; ++k) PUT(k, 0u);
+        for (uint32_t k = 0; k < 4096u; ++k) PUT(k, 0ull);
     uint32_t op = 0;
     int32_t ip = 0, anchor = 0;
     const int32_t mflimit_plus_one = n - kMfLimit + 1, matchlimit = n - kLastLiterals;
     if (n >= kMinLength) {
-        PUT(hash_at<Large>(in), ENT(0));  // first byte
+        PUT(hash_at<Large>(in), ENT(0, w_zero));  // first byte
         ip = 1;
         uint32_t forward_h = hash_at<Large>(in + 1);
+        uint32_t forward_w = ld32(in + 1);
         for (;;) {
             int32_t match;
             {   // find a match
                 int32_t forward_ip = ip, step = 1, search_nb = 1 << 6;
                 for (;;) {
-                    const uint32_t h = forward_h;
+                    const uint32_t h = forward_h, cw = forward_w;
                     const int32_t current = forward_ip;
                     ip = forward_ip;
                     forward_ip += step;
                     step = search_nb++ >> 6;
                     if (forward_ip > mflimit_plus_one) goto last_literals;
                     forward_h = hash_at<Large>(in + forward_ip);
-                    match = idx(XCH(h, ENT(current)));
+                    forward_w = ld32(in + forward_ip);
+                    const uint64_t e = XCH(h, ENT(current, cw));
+                    match = idx(e);
                     if (Large && match + 65535 < current) continue;  // too far
-                    if (ld32(in + match) == ld32(in + ip)) break;
+                    if (bytes_at(e, match) == cw) break;
                 }
             }
             while (ip > anchor && match > 0 && in[ip - 1] == in[match - 1]) {  // catch up
@@ -120,9 +131,11 @@ __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, O& o
                 }
                 anchor = ip;
                 if (ip >= mflimit_plus_one) goto last_literals;
-                PUT(hash_at<Large>(in + ip - 2), ENT(ip - 2));  // fill table
-                const int32_t mi = idx(XCH(hash_at<Large>(in + ip), ENT(ip)));  // test next position
-                if ((!Large || mi + 65535 >= ip) && ld32(in + mi) == ld32(in + ip)) {
+                PUT(hash_at<Large>(in + ip - 2), ENT(ip - 2, ld32(in + ip - 2)));  // fill table
+                const uint32_t iw = ld32(in + ip);
+                const uint64_t e = XCH(hash_at<Large>(in + ip), ENT(ip, iw));  // test next position
+                const int32_t mi = idx(e);
+                if ((!Large || mi + 65535 >= ip) && bytes_at(e, mi) == iw) {
                     match = mi;
                     token = op++;
                     out.set(token, 0u);
@@ -131,6 +144,7 @@ __device__ uint32_t encode_block(const uint8_t* __restrict__ in, int32_t n, O& o
                 break;
             }
             forward_h = hash_at<Large>(in + ++ip);  // prepare next loop
+            forward_w = ld32(in + ip);
         }
     }
 last_literals:
@@ -138,7 +152,7 @@ last_literals:
 #undef PUT
 #undef ENT
     if (Large)
-        for (uint32_t k = 0; k < 4096u; ++k) __hip_atomic_store(table + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t k = 0; k < 4096u; ++k) __hip_atomic_store(table + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t lit = (uint32_t)(n - anchor);  // last literals
     if (lit >= 15u) {
         out.set(op++, 15u << 4);
@@ -155,11 +169,11 @@ template <bool SPREAD>
 __global__ void __launch_bounds__(256) k_lz4_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                     const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
-                                                    int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ workspace,
+                                                    int32_t* __restrict__ status, uint32_t n, uint64_t* __restrict__ workspace,
                                                     uint32_t stamp_base) {
     uint32_t tid, nthreads;
     if (!chunk_slot<SPREAD>(tid, nthreads)) return;
-    uint32_t* table = workspace + (size_t)tid * kTableSlots;
+    uint64_t* table = workspace + (size_t)tid * kTableSlots;
     uint8_t* slot = nullptr;
     if constexpr (!SPREAD) {
         __shared__ __attribute__((aligned(16))) uint8_t stages[256 * kStageStride];
@@ -192,7 +206,7 @@ __global__ void __launch_bounds__(256) k_lz4_encode(const uint8_t* __restrict__ 
 
 namespace {
 constexpr uint32_t kMaxStamp = 0xFFFFu;
-static_assert(nx::kWsSpec[(int)nx::WsKind::Lz4Enc].entry_bytes == sizeof(uint32_t) &&
+static_assert(nx::kWsSpec[(int)nx::WsKind::Lz4Enc].entry_bytes == sizeof(uint64_t) &&
                   (1u << nx::kWsSpec[(int)nx::WsKind::Lz4Enc].lg) == nx::lz4::kTableSlots,
               "LZ4 table geometry");
 }  // namespace
@@ -209,12 +223,12 @@ extern "C" int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const hipStream_t st = (hipStream_t)stream;
-    const size_t per = nx::lz4::kTableSlots * sizeof(uint32_t);
+    const size_t per = nx::lz4::kTableSlots * sizeof(uint64_t);
     nx::WsLease lease(nx::WsKind::Lz4Enc, dev, st);
     NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::Lz4Enc, n, cus)));
     nx::SharedWs& W = lease.ws();
     const nx::LaneGrid g = nx::ws_grid(nx::WsKind::Lz4Enc, n, cus, W.slots);  // 16 waves per CU, as the Snappy encoder
-    uint32_t* ws = static_cast<uint32_t*>(W.p);
+    uint64_t* ws = static_cast<uint64_t*>(W.p);
     const uint32_t iters = (uint32_t)((n + g.slots - 1) / g.slots);
     if (W.stamp + iters >= kMaxStamp) {
         NX_HIP_CHECK(hipMemsetAsync(ws, 0, W.slots * per, st));

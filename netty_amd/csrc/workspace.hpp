@@ -24,7 +24,7 @@ struct WsSpec {
     uint32_t lg;
     unsigned waves_per_cu;
 };
-constexpr WsSpec kWsSpec[] = {{8, 14, 16}, {4, 13, 16}, {8, 13, 8}, {8, 14, 8}, {0, 0, 0}};
+constexpr WsSpec kWsSpec[] = {{8, 14, 16}, {8, 13, 16}, {8, 13, 8}, {8, 14, 8}, {0, 0, 0}};
 constexpr size_t kDecSlotBytes = 16384u * 4u + 8u;  // records of one frame + its count and length
 constexpr uint32_t kDecMaxFrames = 262144;           // frames per parse/expand launch pair
 
