@@ -869,14 +869,12 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
             // NOT_ENOUGH_INPUT (silent stop, the tag byte consumed): operands, or the literal's bytes
             const bool nei = avail < hdr || (isl && !lneg && in_len - dpos < lj);
             const uint32_t len = isl ? lj : clen;
-            int32_t err = 0;
-            if (isl) {
-                err = lneg ? NX_ERR_SNAPPY_LITERAL_LEN_INVALID : 0;
-            } else {
-                err = coff == 0u ? NX_ERR_SNAPPY_OFFSET_ZERO
-                                 : ((int32_t)coff < 0 ? NX_ERR_SNAPPY_OFFSET_NEGATIVE : (coff > op ? NX_ERR_SNAPPY_OFFSET_BEYOND : 0));
-            }
-            if (err == 0 && (uint64_t)op + len > cap) err = NX_ERR_SNAPPY_OUTPUT_OVERFLOW;
+            // Java's check order as selects (no divergent branches): literal length, then offset zero /
+            // negative / beyond, then the output limit (op <= cap, so cap - op cannot wrap)
+            const int32_t cerr = coff == 0u ? NX_ERR_SNAPPY_OFFSET_ZERO
+                                            : ((int32_t)coff < 0 ? NX_ERR_SNAPPY_OFFSET_NEGATIVE : (coff > op ? NX_ERR_SNAPPY_OFFSET_BEYOND : 0));
+            const int32_t terr = isl ? (lneg ? NX_ERR_SNAPPY_LITERAL_LEN_INVALID : 0) : cerr;
+            const int32_t err = terr != 0 ? terr : (len > cap - op ? NX_ERR_SNAPPY_OUTPUT_OVERFLOW : 0);
             if (nei || err != 0) {  // rare: the frame stops here
                 ip = nei ? after_tag : dpos;
                 st = nei ? NX_OK : err;
