@@ -335,19 +335,12 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
         const uint32_t tlen = tend - tstart;
         const bool overlap = !lit && xo < tlen;  // copy reads bytes it produces
         const uint32_t pin = xo + (x0 - tstart);  // literal: input position
-        uint32_t sp, lbase, lmask;  // LDS read: dwords lbase + ((sp >> 2) [+1] & lmask)
-        bool gl;
-        if (lit) {
-            sp = pin + io.a;
-            gl = (sp - io.sbase) > (uint32_t)(kStage - 8);  // outside the stage: read the input from HBM
-            lbase = kRing / 4;
-            lmask = kStage / 4 - 1;
-        } else {
-            sp = x0 - xo;
-            gl = !overlap && pe > (uint32_t)kRing && sp < pe - (uint32_t)kRing;  // far copy
-            lbase = 0;
-            lmask = kRing / 4 - 1;
-        }
+        // LDS read: dwords lbase + ((sp >> 2) [+1] & lmask); selects, not a divergent branch
+        const uint32_t sp = lit ? pin + io.a : x0 - xo;
+        const bool gl = lit ? (sp - io.sbase) > (uint32_t)(kStage - 8)                        // outside the stage: HBM
+                            : (!overlap && pe > (uint32_t)kRing && sp < pe - (uint32_t)kRing);  // far copy
+        const uint32_t lbase = lit ? (uint32_t)(kRing / 4) : 0u;
+        const uint32_t lmask = lit ? (uint32_t)(kStage / 4 - 1) : (uint32_t)(kRing / 4 - 1);
         const uint32_t nbytes = x1 - x0;
         const uint32_t sh = 8u * (x0 & 3u);
         const uint32_t bmask = (nbytes >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nbytes)) - 1u)) << sh;
