@@ -378,14 +378,15 @@ def probe_ceiling(torch, dev, lanes=262144, steps=16384):
     lib.nx_probe_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
     # The rate depends on where the table lands; the encoder's workspace is the best of
-    # several placements (snappy_encode.hip alloc_workspace), so the ceiling is too: the fastest of up
-    # to three tables held at once (each drawn while the others stay allocated).
+    # six placements (nx_common.hpp alloc_placed_workspace), so the ceiling is too: the fastest of up
+    # to six tables held at once (each drawn while the others stay allocated; fewer if memory is short).
+    # With three, a box whose three draws all landed slowly reported a ceiling below the encoder's rate.
     inp = torch.empty(lanes * 16384, dtype=torch.int32, device=dev)
     sink = torch.empty(lanes, dtype=torch.int32, device=dev)
     loads = round(1000 * ENC_CANDIDATE_LOADS_PER_CHUNK / ENC_PROBES_PER_CHUNK)
     inserts = round(1000 * ENC_INSERTS_PER_CHUNK / ENC_PROBES_PER_CHUNK)
-    tabs, best = [], {}
-    for k in range(3):
+    tabs, best, per = [], {}, []
+    for k in range(6):
         if k and torch.cuda.mem_get_info(dev)[0] < lanes * 16384 * 8 + (8 << 30):
             break
         tabs.append(torch.empty(lanes * 16384, dtype=torch.int64, device=dev))
@@ -394,9 +395,14 @@ def probe_ceiling(torch, dev, lanes=262144, steps=16384):
             rc = lib.nx_probe_ceiling(tabs[-1].data_ptr(), inp.data_ptr(), sink.data_ptr(), lanes, steps, loads, ins,
                                       ctypes.byref(ms), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
             if rc == 0 and ms.value > 0:
-                best[key] = max(best.get(key, 0.0), lanes * steps / (ms.value / 1e3))
+                rate = lanes * steps / (ms.value / 1e3)
+                best[key] = max(best.get(key, 0.0), rate)
+                if key == "with_inserts":
+                    per.append(round(rate / 1e9, 2))
     del tabs, inp, sink
     torch.cuda.empty_cache()
+    if best:
+        best["placements_gprobes_per_s"] = per  # with inserts, one per table placement tried
     return best or None
 
 
@@ -477,7 +483,7 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
     traffic = load_traffic() if gpu else (None, "cpu test leg")
     r_dec = roofline(C_ + U, t_dec, n, DEC_KERNELS, traffic, copy_gbs)  # decode: C_in + U_out per chunk
     r_enc = roofline(U + C_, t_enc, n, ENC_KERNELS, traffic, copy_gbs)  # encode: U_in + C_out per chunk
-    if gpu and t_enc and not args.no_probe_ceiling:
+    def fill_random_access():
         ceil = probe_ceiling(torch, dev) or {}
         got = ENC_PROBES_PER_CHUNK * n / (t_enc / 1e3)
         cw, cn = ceil.get("with_inserts"), ceil.get("no_inserts")
@@ -491,9 +497,15 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
             "frac": round(got / cw, 4) if cw else None,
             "ceiling_no_inserts_probes_per_s": round(cn / 1e9, 3) * 1e9 if cn else None,
             "frac_no_inserts": round(got / cn, 4) if cn else None,
+            "ceiling_placements_gprobes_per_s": ceil.get("placements_gprobes_per_s"),
             "ceiling_source": "netty_amd/tools/probe_ceiling.hip, the same request mix without compute (exchanges, "
                               "insert stores and candidate loads in the census proportions; and without the stores), "
-                              "262144 lanes, timed live, fastest of up to 3 table placements (as the encoder chooses its workspace)"}
+                              "262144 lanes, timed live, fastest of up to 6 table placements (as the encoder chooses its "
+                              "workspace), drawn after the job's buffers are freed at N=1"}
+
+    want_ceiling = bool(gpu and t_enc and not args.no_probe_ceiling)
+    if want_ceiling and not (rank == 0 and world == 1):
+        fill_random_access()
     if gpu:
         r_enc["workspace_placement"] = encoder_placement()
     dominant = r_enc if t_enc >= t_dec else r_dec
@@ -549,6 +561,8 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
             torch.cuda.empty_cache()
         del leg
         torch.cuda.empty_cache()
+        if want_ceiling:  # with the job's buffers freed, the ceiling can draw as many placements as the encoder
+            fill_random_access()
         if not args.no_alt:
             line["alt_codecs"] = bench_alt_codecs(torch, B, dev, args.alt_chunks)
             torch.cuda.empty_cache()
