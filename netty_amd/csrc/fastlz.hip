@@ -3,8 +3,9 @@
 // FastLZ is a serial byte-oriented LZ77 whose match search depends on an evolving 8192-entry
 // hash table (FastLz.java:112,139-142), so each chunk runs as one lane's serial state machine;
 // a batch of thousands of 4–64 KiB chunks fills the chip.  The hash table lives in a per-lane
-// device workspace with the same (stamp << 16 | position) trick as the Snappy encoder.  Java's
-// `htab` is initialised to 0 (= position 0) on every call; a stamp mismatch reads as 0.
+// device workspace with a stamp as the Snappy encoder (64-bit entries: stamp | position | the 4 bytes
+// at the position, compress() below).  Java's `htab` is initialised to 0 (= position 0) on every
+// call; a stamp mismatch reads as position 0.
 //
 // The readU16 quirk (FastLz.java:552-557: an ABSOLUTE index compared against readableBytes())
 // is reproduced through the per-chunk u16_limit = readableBytes() - inOffset of the Java call.

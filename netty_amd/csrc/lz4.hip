@@ -12,7 +12,7 @@
 //     backwards over equal bytes (catch up) and forwards up to 5 bytes before the end, and after a
 //     match position ip-2 is inserted and ip is tested at once (a zero-literal sequence).
 //
-// Each lane owns a 32 KiB table in an HBM workspace.  Small blocks store stamp << 16 | index
+// Each lane owns a 64 KiB table (8192 64-bit entries) in an HBM workspace.  Small blocks store stamp << 16 | index
 // (a stamp mismatch reads as the zeroed table), so the table is never cleared between blocks;
 // a large block zeroes its 4096 slots before and after itself, so none of its raw indices can pass
 // a later small block's stamp check.

@@ -30,8 +30,8 @@ __device__ __forceinline__ int32_t first2(const uint8_t* in, int32_t p) {  // Ch
     return (int32_t)((uint32_t)(int32_t)(int8_t)in[p] << 8) + in[p + 1];
 }
 
-// Returns body length.  htab entries: (stamp << 16) | (position + 1); a stamp mismatch is the Java
-// zero (position 0).  A fresh table per chunk is exact for Netty's long-lived per-handler encoder
+// Returns body length.  htab entries: (stamp << 16) | (position + 1) in the high word (the bytes at
+// the position in the low one, below); a stamp mismatch is the Java zero (position 0).  A fresh table per chunk is exact for Netty's long-lived per-handler encoder
 // (LzfEncoder.java:57,161-163,219), whose table keeps earlier chunks' and messages' entries: the first
 // occurrence of every trigram in a chunk is written before any probe reads its slot, so a stale entry
 // (or a never-written slot) can never pass the 3-byte check (oracle/netty_oracle.c, above
