@@ -411,11 +411,11 @@ def encoder_placement():
     import ctypes
     from netty_amd import _lib
     L = _lib.load()
-    ms = (ctypes.c_float * 8)()
+    ms = (ctypes.c_float * 16)()
     n, pick = ctypes.c_int32(0), ctypes.c_int32(-1)
-    if L.nx_snappy_encode_placement(ms, 8, ctypes.byref(n), ctypes.byref(pick)) != 0:
+    if L.nx_snappy_encode_placement(ms, 16, ctypes.byref(n), ctypes.byref(pick)) != 0:
         return None
-    return {"note": "k_ws_probe ms per candidate workspace (256 dependent exchanges per lane); the encoder keeps the fastest",
+    return {"note": "k_ws_probe ms per candidate workspace (256 dependent exchanges per lane), two draws of up to six; the encoder keeps the fastest",
             "probe_ms": [round(ms[k], 3) for k in range(n.value)], "pick": pick.value}
 
 
