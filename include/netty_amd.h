@@ -377,6 +377,34 @@ int32_t nx_batcher_stats(nx_batcher* b, uint64_t* flushes, uint64_t* launches, u
  * pages, results into mapped memory) overlaps the next batch's kernels; results are applied in flush
  * order, so per-decoder semantics are those of one serial execution. */
 int32_t nx_batcher_set_flush_bytes(nx_batcher* b, size_t bytes);
+/* Hold the device workspaces of the given kinds (bit NX_WS_* per kind) for this batcher now, so that
+ * no submit pays for it: a server calls it at start-up.  Otherwise the first submit that needs a kind
+ * holds it (Snappy tables for 65 536 lanes, records for 65 536 frames, 16 384 lanes of the other
+ * encoders' tables; a quarter of that, and so on down to 1 024, when the device cannot spare it).
+ * nx_batcher_new itself reserves nothing (a decode-only batcher never holds encoder tables). */
+int32_t nx_batcher_reserve(nx_batcher* b, uint32_t kinds);
+
+/* The FastLZ, LZF and LZ4 handlers as batcher jobs, with the Snappy jobs' contract (one launch per
+ * codec kernel per flush for every job of every channel; results applied in submission order per
+ * handle, a failing decoder job marking the decoder corrupted; the handle may be freed while its jobs
+ * are in flight).  Inputs are copied at submit.
+ *   FastLzFrameEncoder.encode (FastLzFrameEncoder.java:111-172) over buf[reader_index .. + n): one
+ *     message, the framed blocks.
+ *   LzfEncoder.encode (LzfEncoder.java:169-246): one message.
+ *   Lz4FrameEncoder (Lz4FrameEncoder.java:221-336): op 0 = encode(in) — the full blocks of the handle's
+ *     block buffer leave, the rest stays buffered; op 1 = encode(in) then flush() (the partial block
+ *     too); op 2 = encode(in) then close() (flush + the end block; later jobs pass bytes through).
+ *   FastLzFrameDecoder / LzfDecoder / Lz4FrameDecoder .decode over the cumulation in[0..n):
+ *     *consumed = bytes the caller discards now; result: the decoded messages, then the failure. */
+int64_t nx_fastlz_frame_encoder_submit(nx_fastlz_frame_encoder* e, nx_batcher* b, const uint8_t* buf, size_t reader_index,
+                                       size_t n);
+int64_t nx_lzf_encoder_submit(nx_lzf_encoder* e, nx_batcher* b, const uint8_t* in, size_t n);
+int64_t nx_lz4_frame_encoder_submit(nx_lz4_frame_encoder* e, nx_batcher* b, const uint8_t* in, size_t n, int32_t op);
+int64_t nx_fastlz_frame_decoder_submit(nx_fastlz_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
+                                       size_t* consumed);
+int64_t nx_lzf_decoder_submit(nx_lzf_decoder* d, nx_batcher* b, const uint8_t* in, size_t n, size_t* consumed);
+int64_t nx_lz4_frame_decoder_submit(nx_lz4_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
+                                    size_t* consumed);
 
 #ifdef __cplusplus
 }

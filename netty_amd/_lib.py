@@ -71,6 +71,13 @@ _SIGS = {
     "nx_batcher_release": (i32, [vp, i64]),
     "nx_batcher_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]),
     "nx_batcher_set_flush_bytes": (i32, [vp, sz]),
+    "nx_batcher_reserve": (i32, [vp, C.c_uint32]),
+    "nx_fastlz_frame_encoder_submit": (i64, [vp, vp, vp, sz, sz]),
+    "nx_lzf_encoder_submit": (i64, [vp, vp, vp, sz]),
+    "nx_lz4_frame_encoder_submit": (i64, [vp, vp, vp, sz, i32]),
+    "nx_fastlz_frame_decoder_submit": (i64, [vp, vp, vp, sz, C.POINTER(sz)]),
+    "nx_lzf_decoder_submit": (i64, [vp, vp, vp, sz, C.POINTER(sz)]),
+    "nx_lz4_frame_decoder_submit": (i64, [vp, vp, vp, sz, C.POINTER(sz)]),
     # host handler layer
     "nx_snappy_frame_encoder_new": (vp, [i32]),
     "nx_snappy_frame_encoder_free": (None, [vp]),

@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+#include <algorithm>
 #include <deque>
 #include <map>
 #include <mutex>
@@ -46,6 +47,7 @@
 #include "../../include/netty_amd.h"
 #include "frame_parse.hpp"
 #include "handles.hpp"
+#include "alt_frames.hpp"
 #include "nx_common.hpp"
 #include "workspace.hpp"
 
@@ -197,11 +199,180 @@ __global__ void __launch_bounds__(256) k_dec_finish(const uint8_t* __restrict__ 
             R.len = dlen[A.chunk];
             R.crc = dcrc[A.chunk];
             R.cons = dcons[A.chunk];
+            if (R.status == NX_ERR_SNAPPY_LITERAL_LEN_INVALID && R.cons >= 4u) {  // the literal's length field, for the message
+                const uint8_t* f = din + A.in_off + R.cons - 4u;
+                R.crc = f[0] | (f[1] << 8) | (f[2] << 16) | ((uint32_t)f[3] << 24);
+            }
             if (R.status == NX_OK) wave_copy(out + pos, slots + dslot[A.chunk], R.len, lane);
         }
         if (lane == 0) res[a] = R;
         if (R.status != NX_OK) break;
         pos += R.len;
+    }
+}
+
+// ---------------------------------------------------------------- FastLZ / LZF / LZ4 jobs
+// An alt-codec job's output is a list of PIECES in stream order: for an encoder one framed block each
+// (written back to back into the job's output), for a decoder one block's message each.  The codec
+// kernels of the flush leave their results in the alt slots and result arrays; k_alt_finish (one wave
+// per job) writes each piece into mapped host memory and records where it went.
+enum : uint32_t {
+    AK_FLZ_ENC = 1,  // FastLzFrameEncoder block (:115-168): header, then compressed (slot) or raw (input) bytes
+    AK_LZF_ENC,      // a complete "ZV" block from the LZF encoder (slot)
+    AK_LZF_RAW,      // a non-compressed "ZV" block (encodeNonCompress, LzfEncoder.java:223-246)
+    AK_LZ4_ENC,      // a framed block from the LZ4 frame encoder (slot; header included)
+    AK_LZ4_END,      // Lz4FrameEncoder's end block (:326-335)
+    AK_RAW,          // input bytes as they are (Lz4FrameEncoder after close(), :233-239)
+    AK_DEC_FLZ,      // a FastLZ block decoded into its slot
+    AK_DEC_LZF,      // an LZF block decoded into its slot
+    AK_DEC_LZ4,      // an LZ4 block decoded into its slot
+    AK_DEC_RAW,      // a non-compressed block: its payload (input)
+};
+struct AltPiece {
+    uint64_t src;   // input arena offset of the raw bytes / payload
+    uint64_t slot;  // alt slot offset of the codec's output
+    uint32_t len;   // input bytes
+    uint32_t olen;  // decoder: decoded bytes
+    uint32_t kind;
+    uint32_t res;   // index into the codec's result arrays
+    uint32_t aux;   // AK_FLZ_ENC: bit 0 = with Adler32; AK_LZ4_END: compression level
+    uint32_t pad;
+};
+struct AltJobD {
+    uint64_t out_off;  // in the mapped output arena
+    uint32_t p0, np;   // pieces
+};
+struct AltRes {  // per piece
+    uint64_t off;    // bytes in the output arena
+    uint32_t len;    // AK_DEC_FLZ failing: decompress()'s return value
+    int32_t status;  // NX_OK, or the codec status
+    uint32_t cks;    // decoder pieces with a checksum: Adler32 / XXH32 of the block's bytes
+    uint32_t pad;
+};
+struct AltArrays {  // the flush's codec result arrays (device)
+    const uint32_t* flz_clen;
+    const int32_t* flz_st;
+    const uint32_t* flz_adler;
+    const uint32_t* lzf_olen;
+    const int32_t* lzf_st;
+    const uint32_t* lz4_olen;
+    const int32_t* lz4_st;
+    const int32_t* dflz_r;
+    const int32_t* dlzf_st;
+    const int32_t* dlz4_st;
+    const uint32_t* dcks;  // decoder checksums, indexed by AltPiece::aux - 1
+};
+
+__global__ void __launch_bounds__(256) k_alt_finish(const uint8_t* __restrict__ din, const uint8_t* __restrict__ aslots,
+                                                    const AltPiece* __restrict__ pcs, const AltJobD* __restrict__ jobs, uint32_t njobs,
+                                                    AltArrays R, uint8_t* __restrict__ out, AltRes* __restrict__ res) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= njobs) return;
+    const AltJobD J = jobs[j];
+    uint64_t pos = J.out_off;
+    for (uint32_t k = J.p0; k < J.p0 + J.np; ++k) {
+        const AltPiece P = pcs[k];
+        AltRes r{pos, 0, NX_OK, 0, 0};
+        if (P.kind >= AK_DEC_FLZ && P.aux) r.cks = R.dcks[P.aux - 1];
+        uint8_t* o = out + pos;
+        switch (P.kind) {
+            case AK_FLZ_ENC: {  // FastLzFrameEncoder.java:115-168
+                const bool cks = (P.aux & 1u) != 0;
+                const int32_t st = R.flz_st[P.res];
+                if (st != NX_OK) {
+                    r.status = st;
+                    break;
+                }
+                const uint32_t clen = R.flz_clen[P.res];
+                const bool comp = P.len >= 32u && clen < P.len;  // MIN_LENGTH_TO_COMPRESSION, :150-158
+                const uint32_t hdr = 4u + (cks ? 4u : 0u) + (comp ? 4u : 2u);
+                if (lane == 0) {
+                    o[0] = 'F';
+                    o[1] = 'L';
+                    o[2] = 'Z';
+                    o[3] = (uint8_t)((comp ? 1u : 0u) | (cks ? 0x10u : 0u));
+                    uint32_t q = 4;
+                    if (cks) {
+                        const uint32_t a = R.flz_adler[P.res];
+                        o[4] = (uint8_t)(a >> 24);
+                        o[5] = (uint8_t)(a >> 16);
+                        o[6] = (uint8_t)(a >> 8);
+                        o[7] = (uint8_t)a;
+                        q = 8;
+                    }
+                    if (comp) {
+                        o[q] = (uint8_t)(clen >> 8);
+                        o[q + 1] = (uint8_t)clen;
+                        q += 2;
+                    }
+                    o[q] = (uint8_t)(P.len >> 8);
+                    o[q + 1] = (uint8_t)P.len;
+                }
+                if (comp) wave_copy(o + hdr, aslots + P.slot, clen, lane);
+                else wave_copy(o + hdr, din + P.src, P.len, lane);
+                r.len = hdr + (comp ? clen : P.len);
+                break;
+            }
+            case AK_LZF_ENC:
+            case AK_LZ4_ENC: {
+                const int32_t st = P.kind == AK_LZF_ENC ? R.lzf_st[P.res] : R.lz4_st[P.res];
+                if (st != NX_OK) {
+                    r.status = st;
+                    break;
+                }
+                r.len = P.kind == AK_LZF_ENC ? R.lzf_olen[P.res] : R.lz4_olen[P.res];
+                wave_copy(o, aslots + P.slot, r.len, lane);
+                break;
+            }
+            case AK_LZF_RAW:  // LZFChunk.appendNonCompressed: 'Z' 'V' 0 len(BE16) bytes
+                if (lane == 0) {
+                    o[0] = 'Z';
+                    o[1] = 'V';
+                    o[2] = 0;
+                    o[3] = (uint8_t)(P.len >> 8);
+                    o[4] = (uint8_t)P.len;
+                }
+                wave_copy(o + 5, din + P.src, P.len, lane);
+                r.len = 5u + P.len;
+                break;
+            case AK_LZ4_END:  // magic, token = BLOCK_TYPE_NON_COMPRESSED | level, then 12 zero bytes
+                if (lane < 21) o[lane] = lane < 8 ? (uint8_t)"LZ4Block"[lane] : (lane == 8 ? (uint8_t)(0x10u | P.aux) : 0);
+                r.len = 21;
+                break;
+            case AK_RAW:
+            case AK_DEC_RAW:
+                wave_copy(o, din + P.src, P.len, lane);
+                r.len = P.len;
+                break;
+            case AK_DEC_FLZ: {  // FastLzFrameDecoder.java:154-165: decompress() must return originalLength
+                const int32_t v = R.dflz_r[P.res];
+                if (v < 0 || (uint32_t)v != P.olen) {
+                    r.status = v < 0 ? v : NX_ERR_FASTLZ_LENGTH_MISMATCH;
+                    r.len = (uint32_t)v;  // the value, for the message
+                    break;
+                }
+                wave_copy(o, aslots + P.slot, P.olen, lane);
+                r.len = P.olen;
+                break;
+            }
+            case AK_DEC_LZF:
+            case AK_DEC_LZ4: {
+                const int32_t st = P.kind == AK_DEC_LZF ? R.dlzf_st[P.res] : R.dlz4_st[P.res];
+                if (st != NX_OK) {
+                    r.status = st;
+                    break;
+                }
+                wave_copy(o, aslots + P.slot, P.olen, lane);
+                r.len = P.olen;
+                break;
+            }
+            default:
+                r.status = NX_ERR_INTERNAL;
+        }
+        if (lane == 0) res[k] = r;
+        if (r.status != NX_OK) break;
+        pos += r.len;
     }
 }
 
@@ -248,7 +419,7 @@ struct Pinned {  // hipHostMalloc'd, mapped into the device address space; grows
 
 struct Job {
     uint64_t ticket = 0;
-    int kind = 0;  // 0 encode, 1 decode
+    int kind = 0;  // 0 Snappy encode, 1 Snappy decode, 2 alt-codec encode, 3 alt-codec decode
     nx_snappy_frame_decoder* dec = nullptr;
     uint32_t index = 0;  // EncJob / DecJob index in its batch
     std::vector<SnappyAction> acts;  // decode: the parsed actions (host copy, stream order)
@@ -264,10 +435,20 @@ struct Job {
     bool walked = false;
     std::vector<std::vector<uint8_t>> owned;  // messages delivered before a re-walk moved the job (a moved
                                               // vector keeps its buffer; a deque would allocate per Job)
+    // alt-codec jobs (FastLZ / LZF / LZ4)
+    int codec = -1;                     // 0 FastLZ, 1 LZF, 2 LZ4
+    nx_alt_decoder_base* adec = nullptr;  // decoder jobs hold a reference (alt_frames.hpp)
+    bool validate = false;
+    std::vector<nx::af::Blk> ablk;      // decoder: the walked blocks, in order
+    nx::af::WalkErr awerr;              // decoder: the walk's header failure after them
+    uint64_t astage = 0;                // decoder: staging offset of the walked bytes (block data are relative)
     Job() = default;
     Job(const Job&) = delete;
     Job& operator=(const Job&) = delete;
-    ~Job() { nx_decoder_unref(dec); }  // a decoder job holds a reference to its handle (handles.hpp)
+    ~Job() {  // a decoder job holds a reference to its handle (handles.hpp)
+        nx_decoder_unref(dec);
+        nx_alt_decoder_unref(adec);
+    }
 };
 
 struct Batch {
@@ -295,8 +476,26 @@ struct Batch {
     std::vector<uint64_t> du_off;  // uncompressed chunks (CRC32C)
     std::vector<uint32_t> du_len;
     std::vector<uint8_t> du_direct;
+    // alt-codec jobs: their pieces and the launch lists of the codec kernels (inputs all staged)
+    std::vector<nx::bt::AltPiece> apc;
+    std::vector<nx::bt::AltJobD> ajob;
+    uint64_t aslots = 0;  // alt slot bytes
+    struct AltList {
+        std::vector<uint64_t> off, slot;
+        std::vector<uint32_t> len, aux;  // aux: FastLZ encode level / decode in_avail; LZ4 encode level; decode olen
+        std::vector<int32_t> lim;        // FastLZ encode: readU16 limit
+        void clear() {
+            off.clear();
+            slot.clear();
+            len.clear();
+            aux.clear();
+            lim.clear();
+        }
+        size_t size() const { return off.size(); }
+    };
+    AltList flz_e, lzf_e, lz4_e, flz_d, lzf_d, lz4_d;
     Pinned out;  // mapped result arena: job outputs, then the result records
-    uint64_t out_used = 0, res_enc = 0, res_dec = 0;
+    uint64_t out_used = 0, res_enc = 0, res_dec = 0, res_alt = 0;
     std::vector<Job*> jobs;
     nx::h::DevBuf din, slots, gops;
     hipEvent_t ev = nullptr;
@@ -322,7 +521,16 @@ struct Batch {
         du_off.clear();
         du_len.clear();
         du_direct.clear();
-        out_used = res_enc = res_dec = 0;
+        out_used = res_enc = res_dec = res_alt = 0;
+        apc.clear();
+        ajob.clear();
+        aslots = 0;
+        flz_e.clear();
+        lzf_e.clear();
+        lz4_e.clear();
+        flz_d.clear();
+        lzf_d.clear();
+        lz4_d.clear();
         for (Job* j : jobs) delete j;
         jobs.clear();
         inflight = done = false;
@@ -370,7 +578,7 @@ struct nx_batcher {
     std::mutex mu;
     hipStream_t s[kStreams] = {};
     int dev = 0;
-    bool held_enc = false, held_dec = false;  // shared workspaces reserved at creation (workspace.hpp)
+    uint32_t held = 0;  // bit per nx::WsKind whose shared workspace the batcher holds (workspace.hpp)
     std::deque<Batch*> all;  // every batch object (collecting, in flight, or done)
     Batch* cur = nullptr;    // the collecting batch
     std::unordered_map<uint64_t, std::pair<Batch*, Job*>> tickets;
@@ -591,6 +799,66 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
     // arrays the kernels fill (device only)
     const uint64_t o_eclen = Ld.put(4ull * nes), o_est = Ld.put(4ull * nes), o_ecrc = Ld.put(4ull * nes), o_dlen = Ld.put(4ull * ndc),
                    o_dcons = Ld.put(4ull * ndc), o_dst = Ld.put(4ull * ndc), o_dcrc = Ld.put(4ull * ndc), o_ducrc = Ld.put(4ull * ndu);
+    // ---- FastLZ / LZF / LZ4 jobs: codec lists, decoder checksum lists, pieces
+    const uint32_t nap = (uint32_t)bt->apc.size(), naj = (uint32_t)bt->ajob.size();
+    Batch::AltList* AL[6] = {&bt->flz_e, &bt->lzf_e, &bt->lz4_e, &bt->flz_d, &bt->lzf_d, &bt->lz4_d};
+    // LZ4 frame encode takes one compression level per launch: order its entries by level
+    std::vector<uint32_t> lz4_perm(bt->lz4_e.size());
+    for (uint32_t i = 0; i < lz4_perm.size(); ++i) lz4_perm[i] = i;
+    std::stable_sort(lz4_perm.begin(), lz4_perm.end(), [&](uint32_t a, uint32_t c) { return bt->lz4_e.aux[a] < bt->lz4_e.aux[c]; });
+    {
+        Batch::AltList& Z = bt->lz4_e;
+        Batch::AltList P;
+        std::vector<uint32_t> pos(Z.size());
+        for (uint32_t k = 0; k < lz4_perm.size(); ++k) {
+            const uint32_t i = lz4_perm[k];
+            pos[i] = k;
+            P.off.push_back(Z.off[i]);
+            P.slot.push_back(Z.slot[i]);
+            P.len.push_back(Z.len[i]);
+            P.aux.push_back(Z.aux[i]);
+            P.lim.push_back(Z.lim[i]);
+        }
+        Z = std::move(P);
+        for (nx::bt::AltPiece& q : bt->apc)
+            if (q.kind == nx::bt::AK_LZ4_ENC) q.res = pos[q.res];
+    }
+    Batch::AltList ck[4];  // decoder checksums: Adler32 over slot / input, XXH32 over slot / input
+    for (nx::bt::AltPiece& q : bt->apc) {
+        if (q.kind < nx::bt::AK_DEC_FLZ || !q.pad) continue;
+        const bool raw = q.kind == nx::bt::AK_DEC_RAW;
+        const int li = (q.pad == 2 ? 2 : 0) + (raw ? 1 : 0);
+        ck[li].off.push_back(raw ? q.src : q.slot);
+        ck[li].len.push_back(raw ? q.len : q.olen);
+        q.aux = (uint32_t)ck[li].off.size();  // 1-based within its list; made global below
+    }
+    const uint32_t nck[4] = {(uint32_t)ck[0].off.size(), (uint32_t)ck[1].off.size(), (uint32_t)ck[2].off.size(), (uint32_t)ck[3].off.size()};
+    const uint32_t ck0[4] = {0, nck[0], nck[0] + nck[1], nck[0] + nck[1] + nck[2]};
+    for (nx::bt::AltPiece& q : bt->apc) {
+        if (q.kind < nx::bt::AK_DEC_FLZ || !q.pad) continue;
+        const int li = (q.pad == 2 ? 2 : 0) + (q.kind == nx::bt::AK_DEC_RAW ? 1 : 0);
+        q.aux += ck0[li];
+    }
+    const uint32_t ncks = ck0[3] + nck[3];
+    uint64_t o_al[6][5], o_ck[4][2];
+    for (int c = 0; c < 6; ++c) {
+        const uint64_t m = AL[c]->size();
+        o_al[c][0] = Lh.put(8 * m);
+        o_al[c][1] = Lh.put(4 * m);
+        o_al[c][2] = Lh.put(8 * m);
+        o_al[c][3] = Lh.put(4 * m);
+        o_al[c][4] = Lh.put(4 * m);
+    }
+    for (int c = 0; c < 4; ++c) {
+        o_ck[c][0] = Lh.put(8ull * nck[c]);
+        o_ck[c][1] = Lh.put(4ull * nck[c]);
+    }
+    const uint64_t o_apc = Lh.put(sizeof(nx::bt::AltPiece) * nap), o_ajob = Lh.put(sizeof(nx::bt::AltJobD) * naj);
+    const uint32_t nfe = (uint32_t)bt->flz_e.size(), nle = (uint32_t)bt->lzf_e.size(), nze = (uint32_t)bt->lz4_e.size();
+    const uint32_t nfd = (uint32_t)bt->flz_d.size(), nld = (uint32_t)bt->lzf_d.size(), nzd = (uint32_t)bt->lz4_d.size();
+    const uint64_t o_fclen = Ld.put(4ull * nfe), o_fst = Ld.put(4ull * nfe), o_fadl = Ld.put(4ull * nfe), o_lolen = Ld.put(4ull * nle),
+                   o_lst = Ld.put(4ull * nle), o_zolen = Ld.put(4ull * nze), o_zst = Ld.put(4ull * nze), o_dfr = Ld.put(4ull * nfd),
+                   o_dlst = Ld.put(4ull * nld), o_dzst = Ld.put(4ull * nzd), o_dcks = Ld.put(4ull * ncks);
     uint64_t st_arr = 0;
     uint8_t* h = bt->stage(Lh.at + 16, &st_arr);
     if (!h) return NX_ERR_HIP;
@@ -633,12 +901,31 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
     cp(o_duoff, bt->du_off.data(), 8ull * ndu);
     cp(o_dulen, bt->du_len.data(), 4ull * ndu);
     // result records in the mapped arena, after the job outputs
+    if (naj) {
+        for (int c = 0; c < 6; ++c) {
+            const Batch::AltList& L = *AL[c];
+            const size_t m = L.size();
+            cp(o_al[c][0], L.off.data(), 8 * m);
+            cp(o_al[c][1], L.len.data(), 4 * m);
+            cp(o_al[c][2], L.slot.data(), 8 * m);
+            cp(o_al[c][3], L.aux.data(), 4 * m);
+            cp(o_al[c][4], L.lim.data(), 4 * m);
+        }
+        for (int c = 0; c < 4; ++c) {
+            cp(o_ck[c][0], ck[c].off.data(), 8ull * nck[c]);
+            cp(o_ck[c][1], ck[c].len.data(), 4ull * nck[c]);
+        }
+        cp(o_apc, bt->apc.data(), sizeof(nx::bt::AltPiece) * nap);
+        cp(o_ajob, bt->ajob.data(), sizeof(nx::bt::AltJobD) * naj);
+        if (!bt->reserve_out(sizeof(nx::bt::AltRes) * nap + 8, &bt->res_alt)) return NX_ERR_HIP;
+    }
     if (!bt->reserve_out(8ull * nej + 8, &bt->res_enc) || !bt->reserve_out(sizeof(DecRes) * nda + 8, &bt->res_dec)) return NX_ERR_HIP;
-    if (!bt->din.ensure(d0 + bt->direct_used + 16) || !bt->slots.ensure(bt->eslots + dslot_bytes + Ld.at + 64)) return NX_ERR_HIP;
+    if (!bt->din.ensure(d0 + bt->direct_used + 16) || !bt->slots.ensure(bt->eslots + dslot_bytes + bt->aslots + Ld.at + 128)) return NX_ERR_HIP;
     uint8_t* din = bt->din.as<uint8_t>();
     uint8_t* slots = bt->slots.as<uint8_t>();
     uint8_t* dslots = slots + bt->eslots;
-    uint8_t* D = dslots + dslot_bytes;
+    uint8_t* aslots = reinterpret_cast<uint8_t*>(((uintptr_t)(dslots + dslot_bytes) + 15) & ~(uintptr_t)15);
+    uint8_t* D = aslots + bt->aslots;
     D = reinterpret_cast<uint8_t*>(((uintptr_t)D + 15) & ~(uintptr_t)15);
     if (hipMemcpyAsync(din, bt->staging.h, bt->st_used, hipMemcpyHostToDevice, s) != hipSuccess) return NX_ERR_HIP;
     if (!bt->direct.empty()) {  // registered inputs: one gather launch reading the mapped host pages
@@ -690,6 +977,69 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         b->launches += 1;
         b->chunks += ndc + ndu;
     }
+    if (naj) {  // FastLZ / LZF / LZ4: one launch per codec kernel for every job of every channel
+        auto U64 = [&](int c, int f) { return (const uint64_t*)(A + o_al[c][f]); };
+        auto U32 = [&](int c, int f) { return (const uint32_t*)(A + o_al[c][f]); };
+        auto I32 = [&](int c, int f) { return (const int32_t*)(A + o_al[c][f]); };
+        if (nfe) {  // FastLz.compress + the frame's Adler32 of every block (FastLzFrameEncoder.java:136-158)
+            r = nx_fastlz_compress_batch(din, U64(0, 0), U32(0, 1), aslots, U64(0, 2), (uint32_t*)(D + o_fclen), I32(0, 3), I32(0, 4),
+                                         (int32_t*)(D + o_fst), nfe, s);
+            if (r != NX_OK) return r;
+            r = nx_adler32_batch(din, U64(0, 0), U32(0, 1), (uint32_t*)(D + o_fadl), nfe, s);
+            if (r != NX_OK) return r;
+            b->launches += 2;
+        }
+        if (nle) {
+            r = nx_lzf_encode_batch(din, U64(1, 0), U32(1, 1), aslots, U64(1, 2), (uint32_t*)(D + o_lolen), (int32_t*)(D + o_lst), nle, s);
+            if (r != NX_OK) return r;
+            b->launches += 1;
+        }
+        for (uint32_t a0 = 0; a0 < nze;) {  // one launch per compression level (usually one)
+            uint32_t a1 = a0;
+            while (a1 < nze && bt->lz4_e.aux[a1] == bt->lz4_e.aux[a0]) ++a1;
+            r = nx_lz4_frame_encode_batch(din, U64(2, 0) + a0, U32(2, 1) + a0, aslots, U64(2, 2) + a0, (uint32_t*)(D + o_zolen) + a0,
+                                          (int32_t)bt->lz4_e.aux[a0], (int32_t*)(D + o_zst) + a0, a1 - a0, s);
+            if (r != NX_OK) return r;
+            b->launches += 1;
+            a0 = a1;
+        }
+        if (nfd) {  // FastLz.decompress (in_avail = the cumulation's readable bytes from the block on)
+            r = nx_fastlz_decompress_batch(din, U64(3, 0), U32(3, 1), U32(3, 3), aslots, U64(3, 2), (const uint32_t*)I32(3, 4),
+                                           (int32_t*)(D + o_dfr), nfd, s);
+            if (r != NX_OK) return r;
+            b->launches += 1;
+        }
+        if (nld) {
+            r = nx_lzf_decode_batch(din, U64(4, 0), U32(4, 1), aslots, U64(4, 2), U32(4, 3), (int32_t*)(D + o_dlst), nld, s);
+            if (r != NX_OK) return r;
+            b->launches += 1;
+        }
+        if (nzd) {
+            r = nx_lz4_decode_batch(din, U64(5, 0), U32(5, 1), aslots, U64(5, 2), U32(5, 3), (int32_t*)(D + o_dzst), nzd, s);
+            if (r != NX_OK) return r;
+            b->launches += 1;
+        }
+        uint32_t* dcks = (uint32_t*)(D + o_dcks);
+        for (int c = 0; c < 4; ++c) {  // decoder checksums (after the decodes: stream order)
+            if (!nck[c]) continue;
+            const uint8_t* base = (c & 1) ? din : aslots;
+            const uint64_t* co = (const uint64_t*)(A + o_ck[c][0]);
+            const uint32_t* cl = (const uint32_t*)(A + o_ck[c][1]);
+            r = c < 2 ? nx_adler32_batch(base, co, cl, dcks + ck0[c], nck[c], s)
+                      : nx_xxhash32_batch(base, co, cl, nx::af::kLz4Seed, dcks + ck0[c], nck[c], s);
+            if (r != NX_OK) return r;
+            b->launches += 1;
+        }
+        const nx::bt::AltArrays R{(const uint32_t*)(D + o_fclen), (const int32_t*)(D + o_fst), (const uint32_t*)(D + o_fadl),
+                                  (const uint32_t*)(D + o_lolen), (const int32_t*)(D + o_lst), (const uint32_t*)(D + o_zolen),
+                                  (const int32_t*)(D + o_zst), (const int32_t*)(D + o_dfr), (const int32_t*)(D + o_dlst),
+                                  (const int32_t*)(D + o_dzst), dcks};
+        hipLaunchKernelGGL(nx::bt::k_alt_finish, dim3((naj + 3) / 4), dim3(256), 0, s, din, aslots, (const nx::bt::AltPiece*)(A + o_apc),
+                           (const nx::bt::AltJobD*)(A + o_ajob), naj, R, bt->out.d, (nx::bt::AltRes*)(bt->out.d + bt->res_alt));
+        if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
+        b->launches += 1;
+        b->chunks += nfe + nle + nze + nfd + nld + nzd;
+    }
     if (hipEventRecord(bt->ev, s) != hipSuccess) return NX_ERR_HIP;
     bt->inflight = true;
     bt->seq = b->flushes;
@@ -713,6 +1063,7 @@ int32_t fail_batch(nx_batcher* b, Batch* bt, int32_t code) {
             j->dec->corrupted = true;
             trim_hist(j->dec);
         }
+        if (j->kind == 3 && j->adec) j->adec->corrupted = true;
     }
     bt->inflight = false;
     bt->done = true;
@@ -724,12 +1075,77 @@ int32_t launch(nx_batcher* b, Batch* bt) {
     return r == NX_OK ? NX_OK : fail_batch(b, bt, r);
 }
 
+// An alt-codec job's result (its batch complete): an encoder's framed bytes as one message, or the
+// decoder's messages in block order up to its first failure, with the reference's message
+// (FastLzFrameDecoder.java:154-180, LzfDecoder.java:205, Lz4FrameDecoder.java:215-241); then the
+// walk's header failure, if any.  A failure marks the decoder corrupted; jobs applied after that on
+// the same decoder deliver nothing (Java skips all later input).
+void apply_alt(Batch* bt, Job* j, const nx::bt::AltRes* ares) {
+    using namespace nx::bt;
+    j->applied = true;
+    const AltJobD& J = bt->ajob[j->index];
+    if (j->kind == 2) {  // encoder
+        uint64_t total = 0;
+        for (uint32_t k = J.p0; k < J.p0 + J.np; ++k) {
+            if (ares[k].status != NX_OK) {
+                j->status = ares[k].status;
+                j->err = nx_status_string(ares[k].status);
+                return;
+            }
+            total += ares[k].len;
+        }
+        j->msgs.push_back({bt->out.h + J.out_off, (size_t)total});
+        return;
+    }
+    nx_alt_decoder_base* d = j->adec;
+    if (d->corrupted) return;
+    auto fail = [&](int32_t code, const std::string& msg) {
+        j->status = code;
+        j->err = msg;
+        d->corrupted = true;
+    };
+    for (uint32_t i = 0; i < J.np; ++i) {
+        const AltRes& R = ares[J.p0 + i];
+        const AltPiece& P = bt->apc[J.p0 + i];
+        const nx::af::Blk& B = j->ablk[i];
+        if (R.status != NX_OK) {
+            if (j->codec == 0) {
+                int32_t code;
+                std::string msg;
+                const int32_t v = R.status == NX_ERR_FASTLZ_LENGTH_MISMATCH ? (int32_t)R.len : R.status;
+                const uint8_t first = B.clen ? bt->staging.h[P.src] : 0;
+                (void)nx::af::flz_block_error(v, B.olen, first, &code, &msg);
+                fail(code, msg);
+            } else {
+                fail(R.status, j->codec == 1 ? nx::af::lzf_block_error() : nx::af::lz4_block_error());
+            }
+            return;
+        }
+        if (j->codec == 0 && B.has_cks && j->validate && R.cks != B.cks) {
+            fail(NX_ERR_FASTLZ_CRC_MISMATCH, nx::af::flz_checksum_error(R.cks, B.cks));
+            return;
+        }
+        if (j->codec == 2 && j->validate && (R.cks & 0x0FFFFFFFu) != B.cks) {
+            fail(NX_ERR_LZ4_CHECKSUM_MISMATCH, nx::af::lz4_checksum_error(R.cks & 0x0FFFFFFFu, B.cks));
+            return;
+        }
+        const bool emit = j->codec == 0 ? B.olen > 0 : (j->codec == 1 ? (B.comp || B.clen > 0) : true);
+        if (emit) j->msgs.push_back({bt->out.h + R.off, (size_t)R.len});
+    }
+    if (j->awerr.set) fail(j->awerr.code, j->awerr.msg);
+}
+
 // The batch is complete: turn the result records into each job's messages, in submission order.
 void apply(nx_batcher* b, Batch* bt) {
     const int64_t* res_len = reinterpret_cast<const int64_t*>(bt->out.h + bt->res_enc);
     const DecRes* dres = reinterpret_cast<const DecRes*>(bt->out.h + bt->res_dec);
     char buf[160];
+    const nx::bt::AltRes* ares = reinterpret_cast<const nx::bt::AltRes*>(bt->out.h + bt->res_alt);
     for (Job* j : bt->jobs) {
+        if (j->kind >= 2) {
+            apply_alt(bt, j, ares);
+            continue;
+        }
         if (j->kind == 0) {
             const EncJob& E = bt->ejob[j->index];
             const int64_t r = res_len[j->index];
@@ -768,7 +1184,7 @@ void apply(nx_batcher* b, Batch* bt) {
                     snprintf(buf, sizeof buf, "mismatching checksum: %x (expected: %x)", R.crc, A.crc);
                     j->err = buf;
                 } else {
-                    j->err = nx_status_string(R.status);
+                    j->err = nx::fr::snappy_block_error(R.status, R.crc, nx_status_string);
                 }
                 failed = true;
                 break;
@@ -866,6 +1282,23 @@ bool poll_batch(nx_batcher* b, Batch* bt, bool block) {
     return advance(b, bt->seq, block) && bt->done;
 }
 
+// Hold the shared workspace of kind k for the batcher's flushes (they run in a NoGrowScope): the full
+// reservation, or a smaller one when the device cannot spare it (a flush caps its grid to what is
+// held).  Done by the first submit that needs the kind, or up front by nx_batcher_reserve.
+bool ensure_held(nx_batcher* b, nx::WsKind k) {
+    const uint32_t bit = 1u << (int)k;
+    if (b->held & bit) return true;
+    const uint32_t first = k == nx::WsKind::SnappyEnc ? nx::kBatcherEncHoldUnits
+                         : k == nx::WsKind::DecRecords ? nx::kBatcherDecHoldUnits : nx::kBatcherHoldUnits;
+    for (uint32_t u = first; u >= nx::kHandleHoldUnits; u /= 4) {
+        if (nx::ws_hold(k, b->dev, u, b->s[0]) == NX_OK) {
+            b->held |= bit;
+            return true;
+        }
+    }
+    return false;
+}
+
 // Auto-flush: launch the collecting batch once its input reaches the threshold (batcher lock held).
 int32_t maybe_autoflush(nx_batcher* b, Batch* bt) {
     if (!b->flush_bytes || bt != b->cur || bt->st_used + bt->direct_used < b->flush_bytes) return NX_OK;
@@ -888,16 +1321,22 @@ extern "C" nx_batcher* nx_batcher_new(void) {
             return nullptr;
         }
     }
-    // One Snappy table workspace and one record workspace for the whole batcher, whichever of its
-    // streams a flush lands on (a flush waits on the device for the previous flush's kernels).
-    b->held_enc = hipGetDevice(&b->dev) == hipSuccess &&
-                  nx::ws_hold(nx::WsKind::SnappyEnc, b->dev, nx::kBatcherEncHoldUnits, b->s[0]) == NX_OK;
-    b->held_dec = b->held_enc && nx::ws_hold(nx::WsKind::DecRecords, b->dev, nx::kBatcherDecHoldUnits, b->s[0]) == NX_OK;
-    if (!b->held_dec) {
+    // The workspaces (one per kind for the whole batcher, whichever of its streams a flush lands on)
+    // are held by the first submit that needs them, or by nx_batcher_reserve.
+    if (hipGetDevice(&b->dev) != hipSuccess) {
         nx_batcher_free(b);
         return nullptr;
     }
     return b;
+}
+
+extern "C" int32_t nx_batcher_reserve(nx_batcher* b, uint32_t kinds) {
+    if (!b) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    for (int k = 0; k < (int)nx::WsKind::Count; ++k)
+        if ((kinds >> k) & 1u)
+            if (!ensure_held(b, (nx::WsKind)k)) return NX_ERR_HIP;
+    return NX_OK;
 }
 
 extern "C" void nx_batcher_free(nx_batcher* b) {
@@ -905,8 +1344,8 @@ extern "C" void nx_batcher_free(nx_batcher* b) {
     for (int i = 0; i < kStreams; ++i) (void)hipStreamSynchronize(b->s[i]);
     for (Batch* x : b->all) delete x;
     for (int i = 0; i < kStreams; ++i) (void)hipStreamDestroy(b->s[i]);
-    if (b->held_enc) nx::ws_unhold(nx::WsKind::SnappyEnc, b->dev);
-    if (b->held_dec) nx::ws_unhold(nx::WsKind::DecRecords, b->dev);
+    for (int k = 0; k < (int)nx::WsKind::Count; ++k)
+        if ((b->held >> k) & 1u) nx::ws_unhold((nx::WsKind)k, b->dev);
     delete b;
 }
 
@@ -936,6 +1375,7 @@ extern "C" int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx
                                                   int32_t in_registered) {
     if (!e || !b || (!in && n)) return NX_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(b->mu);
+    if (!ensure_held(b, nx::WsKind::SnappyEnc)) return NX_ERR_HIP;
     Batch* bt = collecting(b);
     if (!bt) return NX_ERR_HIP;
     Job* j = new Job();
@@ -1013,6 +1453,7 @@ namespace {
 int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n, size_t* consumed, bool registered) {
     if (!d || !b || (!in && n) || !consumed) return NX_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(b->mu);
+    if (!ensure_held(b, nx::WsKind::DecRecords)) return NX_ERR_HIP;
     Batch* bt = collecting(b);
     if (!bt) return NX_ERR_HIP;
     Job* j = new Job();
@@ -1114,6 +1555,336 @@ extern "C" int64_t nx_snappy_frame_decoder_submit(nx_snappy_frame_decoder* d, nx
 extern "C" int64_t nx_snappy_frame_decoder_submit_registered(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
                                                              size_t* consumed) {
     return decoder_submit(d, b, in, n, consumed, true);
+}
+
+// ---------------------------------------------------------------- FastLZ / LZF / LZ4 submits
+namespace {
+using nx::bt::AltPiece;
+
+inline uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
+
+// Register job j (its pieces already in bt->apc from p0 on) with an output reservation of `out_need`.
+int64_t queue_alt(nx_batcher* b, Batch* bt, Job* j, uint32_t p0, size_t out_need) {
+    nx::bt::AltJobD J{};
+    J.p0 = p0;
+    J.np = (uint32_t)bt->apc.size() - p0;
+    if (!bt->reserve_out(out_need + 16, &J.out_off)) return NX_ERR_HIP;
+    j->index = (uint32_t)bt->ajob.size();
+    bt->ajob.push_back(J);
+    bt->jobs.push_back(j);
+    bt->live += 1;
+    b->tickets[j->ticket] = {bt, j};
+    (void)maybe_autoflush(b, bt);  // a failed launch completes the job with the error (result())
+    return (int64_t)j->ticket;
+}
+
+// Undo the pieces / list entries a failed submit added (the batch's other jobs stay valid).
+struct AltMark {
+    size_t apc, fe, le, ze, fd, ld, zd;
+    uint64_t aslots;
+    explicit AltMark(const Batch* bt)
+        : apc(bt->apc.size()), fe(bt->flz_e.size()), le(bt->lzf_e.size()), ze(bt->lz4_e.size()), fd(bt->flz_d.size()),
+          ld(bt->lzf_d.size()), zd(bt->lz4_d.size()), aslots(bt->aslots) {}
+    void undo(Batch* bt) const {
+        auto cut = [](Batch::AltList& L, size_t n) {
+            L.off.resize(n);
+            L.slot.resize(n);
+            L.len.resize(n);
+            L.aux.resize(n);
+            if (!L.lim.empty()) L.lim.resize(n);
+        };
+        bt->apc.resize(apc);
+        cut(bt->flz_e, fe);
+        cut(bt->lzf_e, le);
+        cut(bt->lz4_e, ze);
+        cut(bt->flz_d, fd);
+        cut(bt->lzf_d, ld);
+        cut(bt->lz4_d, zd);
+        bt->aslots = aslots;
+    }
+};
+
+uint32_t push_list(Batch::AltList& L, uint64_t off, uint32_t len, uint64_t slot, uint32_t aux, int32_t lim = 0) {
+    L.off.push_back(off);
+    L.len.push_back(len);
+    L.slot.push_back(slot);
+    L.aux.push_back(aux);
+    L.lim.push_back(lim);
+    return (uint32_t)L.off.size() - 1;
+}
+
+Job* new_alt_job(nx_batcher* b, int kind, int codec) {
+    Job* j = new Job();
+    j->ticket = b->next_ticket++;
+    j->kind = kind;
+    j->codec = codec;
+    return j;
+}
+
+// Decoder submit, shared by the three codecs: the header walk runs now (the decoder's state advances
+// in call order, as ByteToMessageDecoder would call decode()); the walked bytes are staged; the blocks
+// decode at flush; apply() delivers messages / the first failure in order.
+template <class D, class St, class Walk>
+int64_t alt_decoder_submit(D* d, St& st, nx_batcher* b, const uint8_t* in, size_t n, size_t* consumed, int codec, bool validate,
+                           Walk walk) {
+    if (!d || !b || (!in && n) || !consumed) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (!ensure_held(b, nx::WsKind::DecRecords)) return NX_ERR_HIP;
+    Batch* bt = collecting(b);
+    if (!bt) return NX_ERR_HIP;
+    Job* j = new_alt_job(b, 3, codec);
+    j->validate = validate;
+    const AltMark mark(bt);
+    const uint32_t p0 = (uint32_t)bt->apc.size();
+    size_t p = n;
+    size_t out_need = 0;
+    St ns = st;
+    const bool skipping = d->corrupted || d->parse_failed;  // an earlier input failed: Java skips everything
+    if (!skipping) {
+        p = walk(in, n, ns, j->ablk, j->awerr);
+        if (j->awerr.set) p = n;  // the rest is skipped once the decoder is corrupted
+    }
+    if (!j->ablk.empty()) {
+        // stage from the first block on; FastLZ's decompress() may read on to the end of the cumulation
+        const size_t lo = j->ablk.front().data, hi = codec == 0 ? n : j->ablk.back().end;
+        uint64_t off = 0;
+        uint8_t* stg = bt->stage(hi - lo, &off);
+        if (!stg) {
+            delete j;
+            return NX_ERR_HIP;
+        }
+        memcpy(stg, in + lo, hi - lo);
+        j->astage = off - lo;  // block b's payload is at staging offset astage + b.data
+        for (const nx::af::Blk& k : j->ablk) {
+            AltPiece P{};
+            P.src = j->astage + k.data;
+            P.len = k.clen;
+            P.olen = k.olen;
+            const bool cks = validate && k.has_cks;
+            P.pad = cks ? (codec == 0 ? 1u : 2u) : 0u;  // checksum kind: 1 Adler32, 2 XXH32 (assigned at launch)
+            if (!k.comp) {
+                P.kind = nx::bt::AK_DEC_RAW;
+            } else {
+                P.slot = bt->aslots;
+                bt->aslots += align16(k.olen) + 16;
+                Batch::AltList& L = codec == 0 ? bt->flz_d : (codec == 1 ? bt->lzf_d : bt->lz4_d);
+                // FastLZ: aux = in_avail (readable bytes from the block on); LZF / LZ4: the decoded length
+                P.res = push_list(L, P.src, k.clen, P.slot, codec == 0 ? (uint32_t)(n - k.data) : k.olen);
+                P.kind = codec == 0 ? nx::bt::AK_DEC_FLZ : (codec == 1 ? nx::bt::AK_DEC_LZF : nx::bt::AK_DEC_LZ4);
+            }
+            bt->apc.push_back(P);
+            out_need += align16(k.olen);
+        }
+    }
+    const int64_t t = queue_alt(b, bt, j, p0, out_need);
+    if (t < 0) {
+        mark.undo(bt);
+        delete j;
+        return t;
+    }
+    j->adec = d;
+    d->refs.fetch_add(1);  // released with the job (~Job)
+    *consumed = p;
+    if (!skipping) {
+        st = ns;
+        if (j->awerr.set) d->parse_failed = true;  // later submits skip; corrupted once applied
+    }
+    return t;
+}
+}  // namespace
+
+extern "C" int64_t nx_fastlz_frame_decoder_submit(nx_fastlz_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
+                                                  size_t* consumed) {
+    if (!d) return NX_ERR_INVALID_ARG;
+    return alt_decoder_submit(d, d->st, b, in, n, consumed, 0, d->validate, nx::af::flz_walk);
+}
+
+extern "C" int64_t nx_lzf_decoder_submit(nx_lzf_decoder* d, nx_batcher* b, const uint8_t* in, size_t n, size_t* consumed) {
+    if (!d) return NX_ERR_INVALID_ARG;
+    return alt_decoder_submit(d, d->st, b, in, n, consumed, 1, false, nx::af::lzf_walk);
+}
+
+extern "C" int64_t nx_lz4_frame_decoder_submit(nx_lz4_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
+                                               size_t* consumed) {
+    if (!d) return NX_ERR_INVALID_ARG;
+    if (d->st.state == 2 && !d->corrupted && !d->parse_failed) {  // FINISHED: everything is skipped (:250-254)
+        std::lock_guard<std::mutex> lk(b->mu);
+        Batch* bt = collecting(b);
+        if (!bt) return NX_ERR_HIP;
+        Job* j = new_alt_job(b, 3, 2);
+        const int64_t t = queue_alt(b, bt, j, (uint32_t)bt->apc.size(), 0);
+        if (t < 0) {
+            delete j;
+            return t;
+        }
+        j->adec = d;
+        d->refs.fetch_add(1);
+        *consumed = n;
+        return t;
+    }
+    return alt_decoder_submit(d, d->st, b, in, n, consumed, 2, d->validate, nx::af::lz4_walk);
+}
+
+// FastLzFrameEncoder.encode(ctx, in, out) over buf[r0 .. r0 + n) as a job (the reader index enters the
+// readU16 quirk, FastLz.java:552-557).  The message is copied now.
+extern "C" int64_t nx_fastlz_frame_encoder_submit(nx_fastlz_frame_encoder* e, nx_batcher* b, const uint8_t* buf, size_t r0, size_t n) {
+    if (!e || !b || (!buf && n)) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (!ensure_held(b, nx::WsKind::FastLzEnc)) return NX_ERR_HIP;
+    Batch* bt = collecting(b);
+    if (!bt) return NX_ERR_HIP;
+    Job* j = new_alt_job(b, 2, 0);
+    const AltMark mark(bt);
+    const uint32_t p0 = (uint32_t)bt->apc.size();
+    if (n) {
+        uint64_t off = 0;
+        uint8_t* stg = bt->stage(n, &off);
+        if (!stg) {
+            delete j;
+            return NX_ERR_HIP;
+        }
+        memcpy(stg, buf + r0, n);
+        std::vector<nx::af::FlzPlan> plan;
+        nx::af::flz_plan(r0, n, plan);
+        for (const nx::af::FlzPlan& q : plan) {
+            AltPiece P{};
+            P.kind = nx::bt::AK_FLZ_ENC;
+            P.src = off + q.ioff;
+            P.len = q.ilen;
+            P.slot = bt->aslots;
+            bt->aslots += align16(nx_fastlz_max_compressed_length(q.ilen) + 16);
+            P.res = push_list(bt->flz_e, P.src, q.ilen, P.slot, (uint32_t)e->level, q.lim);
+            P.aux = e->checksum ? 1u : 0u;
+            bt->apc.push_back(P);
+        }
+    }
+    const int64_t t = queue_alt(b, bt, j, p0, nx_fastlz_frame_max_encoded_length(n));
+    if (t < 0) {
+        mark.undo(bt);
+        delete j;
+    }
+    return t;
+}
+
+// LzfEncoder.encode(ctx, in, out) as a job (LzfEncoder.java:169-246): below the compress threshold the
+// message leaves as non-compressed blocks, else every 65535-byte chunk goes to the GPU encoder.
+extern "C" int64_t nx_lzf_encoder_submit(nx_lzf_encoder* e, nx_batcher* b, const uint8_t* in, size_t n) {
+    if (!e || !b || (!in && n)) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (!ensure_held(b, nx::WsKind::LzfEnc)) return NX_ERR_HIP;
+    Batch* bt = collecting(b);
+    if (!bt) return NX_ERR_HIP;
+    Job* j = new_alt_job(b, 2, 1);
+    const AltMark mark(bt);
+    const uint32_t p0 = (uint32_t)bt->apc.size();
+    uint64_t off = 0;
+    if (n) {
+        uint8_t* stg = bt->stage(n, &off);
+        if (!stg) {
+            delete j;
+            return NX_ERR_HIP;
+        }
+        memcpy(stg, in, n);
+    }
+    const bool comp = (int64_t)n >= e->threshold;
+    size_t ip = 0;
+    do {  // encodeNonCompress writes one (possibly empty) block even for n == 0 (:223-246)
+        const uint32_t len = (uint32_t)((n - ip) < 65535 ? (n - ip) : 65535);
+        AltPiece P{};
+        P.src = off + ip;
+        P.len = len;
+        if (comp) {
+            P.kind = nx::bt::AK_LZF_ENC;
+            P.slot = bt->aslots;
+            bt->aslots += align16(nx_lzf_max_compressed_length(len) + 16);
+            P.res = push_list(bt->lzf_e, P.src, len, P.slot, 0);
+        } else {
+            P.kind = nx::bt::AK_LZF_RAW;
+        }
+        bt->apc.push_back(P);
+        ip += len;
+    } while (ip < n);
+    const int64_t t = queue_alt(b, bt, j, p0, nx_lzf_frame_max_encoded_length(n));
+    if (t < 0) {
+        mark.undo(bt);
+        delete j;
+    }
+    return t;
+}
+
+// Lz4FrameEncoder as jobs: op 0 = encode(in) (full blocks of the block buffer leave, :231-248), 1 =
+// flush() (the partial block too, :291-300), 2 = close() (flush + the end block, :317-336; afterwards
+// encode passes bytes through, :233-239).  The handle's block buffer advances at submit.
+extern "C" int64_t nx_lz4_frame_encoder_submit(nx_lz4_frame_encoder* e, nx_batcher* b, const uint8_t* in, size_t n, int32_t op) {
+    if (!e || !b || (!in && n) || op < 0 || op > 2) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (!ensure_held(b, nx::WsKind::Lz4Enc)) return NX_ERR_HIP;
+    Batch* bt = collecting(b);
+    if (!bt) return NX_ERR_HIP;
+    Job* j = new_alt_job(b, 2, 2);
+    const AltMark mark(bt);
+    const uint32_t p0 = (uint32_t)bt->apc.size();
+    std::vector<uint8_t> nbuf;  // the block buffer after this job
+    size_t out_need = 0;
+    auto fail = [&](int64_t code) {
+        mark.undo(bt);
+        delete j;
+        return code;
+    };
+    if (e->finished) {  // pass-through (:233-239); flush / close after close write nothing
+        if (n) {
+            uint64_t off = 0;
+            uint8_t* stg = bt->stage(n, &off);
+            if (!stg) return fail(NX_ERR_HIP);
+            memcpy(stg, in, n);
+            AltPiece P{};
+            P.kind = nx::bt::AK_RAW;
+            P.src = off;
+            P.len = (uint32_t)n;
+            bt->apc.push_back(P);
+            out_need = n;
+        }
+        nbuf = e->buf;
+    } else {
+        const size_t have = e->buf.size(), total = have + n, bs = e->block_size;
+        const size_t full = op == 0 ? total / bs * bs : total;  // flush / close take the partial block too
+        if (full) {
+            uint64_t off = 0;
+            uint8_t* stg = bt->stage(full, &off);
+            if (!stg) return fail(NX_ERR_HIP);
+            const size_t from_buf = have < full ? have : full;
+            memcpy(stg, e->buf.data(), from_buf);
+            if (full > from_buf) memcpy(stg + from_buf, in, full - from_buf);
+            for (size_t q = 0; q < full; q += bs) {
+                const uint32_t len = (uint32_t)((full - q) < bs ? (full - q) : bs);
+                AltPiece P{};
+                P.kind = nx::bt::AK_LZ4_ENC;
+                P.src = off + q;
+                P.len = len;
+                P.slot = bt->aslots;
+                const uint64_t cap = nx::af::kLz4Header + nx_lz4_max_compressed_length(len);
+                bt->aslots += align16(cap) + 16;
+                P.res = push_list(bt->lz4_e, P.src, len, P.slot, (uint32_t)e->level);
+                bt->apc.push_back(P);
+                out_need += cap;
+            }
+        }
+        if (full < have) nbuf.assign(e->buf.begin() + (ptrdiff_t)full, e->buf.end());  // (op 0 with a short input)
+        if (full >= have) nbuf.assign(in + (full - have), in + n);
+        else nbuf.insert(nbuf.end(), in, in + n);
+        if (op == 2) {
+            AltPiece P{};
+            P.kind = nx::bt::AK_LZ4_END;
+            P.aux = (uint32_t)e->level;
+            bt->apc.push_back(P);
+            out_need += nx::af::kLz4Header;
+        }
+    }
+    const int64_t t = queue_alt(b, bt, j, p0, out_need);
+    if (t < 0) return fail(t);
+    if (!e->finished) e->buf.swap(nbuf);
+    if (op == 2) e->finished = true;
+    return t;
 }
 
 extern "C" int32_t nx_batcher_flush(nx_batcher* b) {

@@ -6,6 +6,7 @@
 #include <string.h>
 #include <string>
 #include <vector>
+#include "../../include/netty_amd_status.h"
 
 namespace nx {
 namespace fr {
@@ -20,6 +21,20 @@ inline const char* bytebuf_oob(char* buf, size_t cap, size_t reader, int len, si
              writer);
     return buf;
 }
+// Snappy.decode's failure as SnappyFrameDecoder.decode() throws it: the DecompressionException texts
+// (nx_status_string), except a code-63 literal whose Java int length + 1 is negative.  There
+// decodeLiteral's out.writeBytes(in, length) fails in ensureWritable's argument check
+// (Snappy.java:480-492, AbstractByteBuf.java:279-281), an IllegalArgumentException that
+// ByteToMessageDecoder wraps in a DecoderException; `field` = the literal's 4 length bytes (LE).
+inline std::string snappy_block_error(int32_t st, uint32_t field, const char* (*status_string)(int32_t)) {
+    if (st == NX_ERR_SNAPPY_LITERAL_LEN_INVALID) {
+        char buf[96];
+        snprintf(buf, sizeof buf, "java.lang.IllegalArgumentException: minWritableBytes : %d (expected: >= 0)", (int32_t)(field + 1u));
+        return buf;
+    }
+    return status_string(st);
+}
+
 enum class SAct { Stream, Skip, Uncomp, Comp, Error };
 struct SnappyAction {
     SAct kind;

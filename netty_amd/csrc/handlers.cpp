@@ -21,6 +21,7 @@
 #include "nx_common.hpp"
 #include "frame_parse.hpp"
 #include "handles.hpp"
+#include "alt_frames.hpp"
 
 extern "C" int32_t nx_snappy_decode_batch(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*, const uint64_t*,
                                           const uint32_t*, uint32_t*, uint32_t*, int32_t*, const uint32_t*, uint32_t*, uint32_t,
@@ -294,7 +295,9 @@ extern "C" int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, co
                              nx::host_mask(nx::host_crc32c(outs[j].data(), olen[j])), a.crc);
                     return corrupt(a.end, st[j], buf);
                 }
-                if (st[j] != NX_OK) return corrupt(a.end, st[j], nx_status_string(st[j]));
+                if (st[j] != NX_OK)
+                    return corrupt(a.end, st[j], nx::fr::snappy_block_error(st[j], cons[j] >= 4 ? le32(in + a.data + cons[j] - 4) : 0u,
+                                                                           nx_status_string));
                 ml.owned.push_back(std::move(outs[j]));
                 ml.msgs.push_back({ml.owned.back().data(), olen[j]});
                 if (d->validate && cons[j] < a.dlen) {
@@ -315,11 +318,6 @@ extern "C" int32_t nx_snappy_frame_decoder_decode(nx_snappy_frame_decoder* d, co
 }
 
 // ======================================================================= FastLZ frame encoder
-struct nx_fastlz_frame_encoder {
-    Gpu g;
-    int32_t level;
-    bool checksum;
-};
 
 extern "C" nx_fastlz_frame_encoder* nx_fastlz_frame_encoder_new(int32_t level, int32_t checksum) {
     if (level != 0 && level != 1 && level != 2) return nullptr;  // FastLzFrameEncoder.java:101-105
@@ -418,15 +416,6 @@ extern "C" int64_t nx_fastlz_frame_encoder_encode(nx_fastlz_frame_encoder* e, co
 }
 
 // ======================================================================= FastLZ frame decoder
-struct nx_fastlz_frame_decoder {
-    Gpu g;
-    bool validate;
-    int state = 0;  // 0 INIT_BLOCK, 1 INIT_BLOCK_PARAMS, 2 DECOMPRESS_DATA, 3 CORRUPTED
-    uint32_t chunkLength = 0, originalLength = 0, currentChecksum = 0;
-    bool isCompressed = false, hasChecksum = false;
-    MsgList ml;
-};
-
 extern "C" nx_fastlz_frame_decoder* nx_fastlz_frame_decoder_new(int32_t validate) {
     auto* d = new nx_fastlz_frame_decoder();
     if (!d->g.hold(nx::WsKind::DecRecords)) {  // FastLZ blocks decode through the record expander
@@ -436,7 +425,7 @@ extern "C" nx_fastlz_frame_decoder* nx_fastlz_frame_decoder_new(int32_t validate
     d->validate = validate != 0;
     return d;
 }
-extern "C" void nx_fastlz_frame_decoder_free(nx_fastlz_frame_decoder* d) { delete d; }
+extern "C" void nx_fastlz_frame_decoder_free(nx_fastlz_frame_decoder* d) { nx_alt_decoder_unref(d); }
 
 extern "C" int32_t nx_fastlz_frame_decoder_decode(nx_fastlz_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
                                                   const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {
@@ -452,59 +441,20 @@ extern "C" int32_t nx_fastlz_frame_decoder_decode(nx_fastlz_frame_decoder* d, co
         if (err_msg) *err_msg = ml.err.empty() ? nullptr : ml.err.c_str();
         return r;
     };
-    if (d->state == 3) {
+    if (d->corrupted || d->st.state == 3) {  // CORRUPTED (:197-199)
         rd = n;
         return finish(NX_OK);
     }
-    struct Blk {
-        size_t data, end;
-        uint32_t clen, olen, cks;
-        bool comp, has_cks;
-        int job;
-        std::string err;
+    struct Blk : nx::af::Blk {
+        int job = -1;
     };
-    std::vector<Blk> blks;
     // host parse (FastLzFrameDecoder.decode as driven by callDecode); persistent header state
-    int state = d->state;
-    uint32_t chunkLength = d->chunkLength, originalLength = d->originalLength, cks = d->currentChecksum;
-    bool isCompressed = d->isCompressed, hasChecksum = d->hasChecksum;
-    size_t p = 0;
-    std::string perr;
-    size_t perr_at = 0;
-    bool have_err = false;
-    for (;;) {
-        if (state == 0) {
-            if (n - p < 4) break;
-            if (be24(in + p) != (('F' << 16) | ('L' << 8) | 'Z')) {
-                perr = "unexpected block identifier";
-                perr_at = p + 3;
-                have_err = true;
-                break;
-            }
-            const uint8_t options = in[p + 3];
-            isCompressed = (options & 0x01) == 1;
-            hasChecksum = (options & 0x10) == 0x10;
-            p += 4;
-            state = 1;
-        }
-        if (state == 1) {
-            const size_t need = 2 + (isCompressed ? 2 : 0) + (hasChecksum ? 4 : 0);
-            if (n - p < need) break;
-            cks = hasChecksum ? be32(in + p) : 0;
-            p += hasChecksum ? 4 : 0;
-            chunkLength = be16(in + p);
-            p += 2;
-            originalLength = isCompressed ? be16(in + p) : chunkLength;
-            p += isCompressed ? 2 : 0;
-            state = 2;
-        }
-        if (state == 2) {
-            if (n - p < chunkLength) break;
-            blks.push_back({p, p + chunkLength, chunkLength, originalLength, cks, isCompressed, hasChecksum, -1, {}});
-            p += chunkLength;
-            state = 0;
-        }
-    }
+    nx::af::FlzState ns = d->st;
+    std::vector<nx::af::Blk> walked;
+    nx::af::WalkErr werr;
+    const size_t p = nx::af::flz_walk(in, n, ns, walked, werr);
+    std::vector<Blk> blks(walked.size());
+    for (size_t i = 0; i < walked.size(); ++i) static_cast<nx::af::Blk&>(blks[i]) = walked[i];
     // GPU: decompress every compressed block; Adler32 over every produced block if verifying
     // (decompressed blocks in dout, raw blocks straight from the staged cumulation in din)
     uint32_t nz = 0;
@@ -598,19 +548,14 @@ extern "C" int32_t nx_fastlz_frame_decoder_decode(nx_fastlz_frame_decoder* d, co
         uint32_t len;
         if (b.comp) {
             const int32_t r = res[b.job];
-            if (r < 0 || (uint32_t)r != b.olen) {
-                char buf[160];
-                if (r == NX_ERR_FASTLZ_BAD_LEVEL) {
-                    snprintf(buf, sizeof buf, "invalid level: %d (expected: %d or %d)", ((int8_t)in[b.data] >> 5) + 1, 1, 2);
-                } else if (r < 0) {
-                    snprintf(buf, sizeof buf, "%s", nx_status_string(r));
-                } else {
-                    snprintf(buf, sizeof buf, "stream corrupted: originalLength(%u) and actual length(%d) mismatch", b.olen, r);
-                }
-                ml.err = buf;
-                d->state = 3;
+            int32_t code;
+            std::string emsg;
+            if (nx::af::flz_block_error(r, b.olen, b.data < n ? in[b.data] : 0, &code, &emsg)) {
+                ml.err = emsg;
+                d->st.state = 3;
+                d->corrupted = true;
                 rd = b.data;
-                return finish(r < 0 ? r : NX_ERR_FASTLZ_LENGTH_MISMATCH);
+                return finish(code);
             }
             data = hout.data() + ooff[b.job];
             len = b.olen;
@@ -619,10 +564,9 @@ extern "C" int32_t nx_fastlz_frame_decoder_decode(nx_fastlz_frame_decoder* d, co
             len = b.clen;
         }
         if (b.has_cks && want_cks && adl[i] != b.cks) {  // FastLzFrameDecoder.java:171-180
-            char buf[160];
-            snprintf(buf, sizeof buf, "stream corrupted: mismatching checksum: %d (expected: %d)", (int32_t)adl[i], (int32_t)b.cks);
-            ml.err = buf;
-            d->state = 3;
+            ml.err = nx::af::flz_checksum_error(adl[i], b.cks);
+            d->st.state = 3;
+            d->corrupted = true;
             rd = b.data;
             return finish(NX_ERR_FASTLZ_CRC_MISMATCH);
         }
@@ -636,27 +580,19 @@ extern "C" int32_t nx_fastlz_frame_decoder_decode(nx_fastlz_frame_decoder* d, co
         }
         rd = b.end;
     }
-    if (have_err) {
-        ml.err = perr;
-        d->state = 3;
-        rd = perr_at;
-        return finish(NX_ERR_FRAME_CORRUPT);
+    if (werr.set) {
+        ml.err = werr.msg;
+        d->st.state = 3;
+        d->corrupted = true;
+        rd = werr.at;
+        return finish(werr.code);
     }
     rd = p;
-    d->state = state;
-    d->chunkLength = chunkLength;
-    d->originalLength = originalLength;
-    d->currentChecksum = cks;
-    d->isCompressed = isCompressed;
-    d->hasChecksum = hasChecksum;
+    d->st = ns;
     return finish(NX_OK);
 }
 
 // ======================================================================= LZF encoder / decoder
-struct nx_lzf_encoder {
-    Gpu g;
-    int32_t threshold;
-};
 extern "C" nx_lzf_encoder* nx_lzf_encoder_new(int32_t compress_threshold) {
     if (compress_threshold < 16) return nullptr;  // LzfEncoder.java:155-160
     auto* e = new nx_lzf_encoder();
@@ -721,13 +657,6 @@ extern "C" int64_t nx_lzf_encoder_encode(nx_lzf_encoder* e, const uint8_t* in, s
     return (int64_t)op;
 }
 
-struct nx_lzf_decoder {
-    Gpu g;
-    int state = 0;  // 0 INIT_BLOCK, 1 INIT_ORIGINAL_LENGTH, 2 DECOMPRESS_DATA, 3 CORRUPTED
-    uint32_t chunkLength = 0, originalLength = 0;
-    bool isCompressed = false;
-    MsgList ml;
-};
 extern "C" nx_lzf_decoder* nx_lzf_decoder_new(void) {
     auto* d = new nx_lzf_decoder();
     if (!d->g.hold(nx::WsKind::DecRecords)) {  // LZF blocks decode through the record expander
@@ -736,7 +665,7 @@ extern "C" nx_lzf_decoder* nx_lzf_decoder_new(void) {
     }
     return d;
 }
-extern "C" void nx_lzf_decoder_free(nx_lzf_decoder* d) { delete d; }
+extern "C" void nx_lzf_decoder_free(nx_lzf_decoder* d) { nx_alt_decoder_unref(d); }
 
 extern "C" int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, size_t n, size_t* consumed, const nx_msg** msgs,
                                          size_t* n_msgs, const char** err_msg) {
@@ -752,61 +681,19 @@ extern "C" int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, s
         if (err_msg) *err_msg = ml.err.empty() ? nullptr : ml.err.c_str();
         return r;
     };
-    if (d->state == 3) {
+    if (d->corrupted || d->st.state == 3) {  // CORRUPTED (:229-231)
         rd = n;
         return finish(NX_OK);
     }
-    struct Blk {
-        size_t data, end;
-        uint32_t clen, olen;
-        bool comp;
-        int job;
+    struct Blk : nx::af::Blk {
+        int job = -1;
     };
-    std::vector<Blk> blks;
-    int state = d->state;
-    uint32_t chunkLength = d->chunkLength, originalLength = d->originalLength;
-    bool isCompressed = d->isCompressed;
-    size_t p = 0;
-    std::string perr;
-    size_t perr_at = 0;
-    bool have_err = false;
-    for (;;) {
-        if (state == 0) {
-            if (n - p < 5) break;  // HEADER_LEN_NOT_COMPRESSED
-            if (be16(in + p) != (('Z' << 8) | 'V')) {
-                perr = "unexpected block identifier";
-                perr_at = p + 2;
-                have_err = true;
-                break;
-            }
-            const int8_t type = (int8_t)in[p + 2];
-            if (type != 0 && type != 1) {
-                char buf[96];
-                snprintf(buf, sizeof buf, "unknown type of chunk: %d (expected: %d or %d)", (int)type, 0, 1);
-                perr = buf;
-                perr_at = p + 3;
-                have_err = true;
-                break;
-            }
-            isCompressed = type == 1;
-            chunkLength = be16(in + p + 3);
-            p += 5;
-            state = isCompressed ? 1 : 2;
-            if (!isCompressed) continue;
-        }
-        if (state == 1) {
-            if (n - p < 2) break;
-            originalLength = be16(in + p);
-            p += 2;
-            state = 2;
-        }
-        if (state == 2) {
-            if (n - p < chunkLength) break;
-            blks.push_back({p, p + chunkLength, chunkLength, originalLength, isCompressed, -1});
-            p += chunkLength;
-            state = 0;
-        }
-    }
+    nx::af::LzfState ns = d->st;
+    std::vector<nx::af::Blk> walked;
+    nx::af::WalkErr werr;
+    const size_t p = nx::af::lzf_walk(in, n, ns, walked, werr);
+    std::vector<Blk> blks(walked.size());
+    for (size_t i = 0; i < walked.size(); ++i) static_cast<nx::af::Blk&>(blks[i]) = walked[i];
     uint32_t nz = 0;
     uint64_t ocap = 0;
     std::vector<uint64_t> ooff;
@@ -845,8 +732,9 @@ extern "C" int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, s
     for (auto& b : blks) {
         if (b.comp) {
             if (st[b.job] != NX_OK) {
-                ml.err = "Corrupt LZF data";
-                d->state = 3;
+                ml.err = nx::af::lzf_block_error();
+                d->st.state = 3;
+                d->corrupted = true;
                 rd = b.data;
                 return finish(st[b.job]);
             }
@@ -857,17 +745,15 @@ extern "C" int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, s
         }
         rd = b.end;
     }
-    if (have_err) {
-        ml.err = perr;
-        d->state = 3;
-        rd = perr_at;
-        return finish(NX_ERR_FRAME_CORRUPT);
+    if (werr.set) {
+        ml.err = werr.msg;
+        d->st.state = 3;
+        d->corrupted = true;
+        rd = werr.at;
+        return finish(werr.code);
     }
     rd = p;
-    d->state = state;
-    d->chunkLength = chunkLength;
-    d->originalLength = originalLength;
-    d->isCompressed = isCompressed;
+    d->st = ns;
     return finish(NX_OK);
 }
 
@@ -876,19 +762,10 @@ extern "C" int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, s
 //   Lz4FrameDecoder   Lz4FrameDecoder.java:121-261
 // Every full block of one encode() call (and every block of one decode() call) goes to the GPU in
 // one batch: nx_lz4_frame_encode_batch / nx_lz4_decode_batch + nx_xxhash32_batch.
-namespace {
-const uint8_t kLz4Magic[8] = {'L', 'Z', '4', 'B', 'l', 'o', 'c', 'k'};
-constexpr uint32_t kLz4Header = 21;
-constexpr uint32_t kLz4Seed = 0x9747b28cu;  // Lz4Constants.java:70
-}  // namespace
+using nx::af::kLz4Header;
+using nx::af::kLz4Magic;
+using nx::af::kLz4Seed;
 
-struct nx_lz4_frame_encoder {
-    Gpu g;
-    uint32_t block_size = 65536;
-    int32_t level = 6;
-    bool finished = false;
-    std::vector<uint8_t> buf;  // the block buffer (Lz4FrameEncoder.java:221-226)
-};
 
 extern "C" nx_lz4_frame_encoder* nx_lz4_frame_encoder_new(int32_t block_size) {
     // compressionLevel(blockSize) :158-166; the device block encoder takes blocks below 32 MiB
@@ -1009,14 +886,6 @@ extern "C" int64_t nx_lz4_frame_encoder_close(nx_lz4_frame_encoder* e, uint8_t* 
     return w + kLz4Header;
 }
 
-struct nx_lz4_frame_decoder {
-    Gpu g;
-    bool validate = false;
-    int state = 0;  // 0 INIT_BLOCK, 1 DECOMPRESS_DATA, 2 FINISHED, 3 CORRUPTED
-    uint32_t blockType = 0, compressedLength = 0, decompressedLength = 0, currentChecksum = 0;
-    MsgList ml;
-};
-
 extern "C" nx_lz4_frame_decoder* nx_lz4_frame_decoder_new(int32_t validate_checksums) {
     auto* d = new nx_lz4_frame_decoder();
     if (!d->g.hold(nx::WsKind::DecRecords)) {
@@ -1026,7 +895,7 @@ extern "C" nx_lz4_frame_decoder* nx_lz4_frame_decoder_new(int32_t validate_check
     d->validate = validate_checksums != 0;
     return d;
 }
-extern "C" void nx_lz4_frame_decoder_free(nx_lz4_frame_decoder* d) { delete d; }
+extern "C" void nx_lz4_frame_decoder_free(nx_lz4_frame_decoder* d) { nx_alt_decoder_unref(d); }
 
 extern "C" int32_t nx_lz4_frame_decoder_decode(nx_lz4_frame_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
                                                const nx_msg** msgs, size_t* n_msgs, const char** err_msg) {
@@ -1042,83 +911,19 @@ extern "C" int32_t nx_lz4_frame_decoder_decode(nx_lz4_frame_decoder* d, const ui
         if (err_msg) *err_msg = ml.err.empty() ? nullptr : ml.err.c_str();
         return r;
     };
-    if (d->state >= 2) {  // FINISHED / CORRUPTED :251-254
+    if (d->corrupted || d->st.state >= 2) {  // FINISHED / CORRUPTED :250-254
         rd = n;
         return finish(NX_OK);
     }
-    struct Blk {
-        size_t data, end;
-        uint32_t type, clen, dlen, chk;
-        int job;
+    struct Blk : nx::af::Blk {
+        int job = -1;
     };
-    std::vector<Blk> blks;
-    int state = d->state;
-    uint32_t blockType = d->blockType, clen = d->compressedLength, dlen = d->decompressedLength, chk = d->currentChecksum;
-    size_t p = 0;
-    std::string perr;
-    int32_t perr_code = NX_OK;
-    size_t perr_at = 0;
-    char mbuf[160];
-    auto fail = [&](int32_t code, const char* msg, size_t at) {
-        perr = msg;
-        perr_code = code;
-        perr_at = at;
-    };
-    while (perr_code == NX_OK && state < 2) {
-        if (state == 0) {
-            if (n - p < kLz4Header) break;  // :124-126
-            const uint8_t* h = in + p;
-            if (memcmp(h, kLz4Magic, 8) != 0) {  // :127-130
-                fail(NX_ERR_LZ4_BAD_MAGIC, "unexpected block identifier", p + 8);
-                break;
-            }
-            const uint32_t token = h[8];
-            const uint32_t level = (token & 0x0Fu) + 10u;
-            blockType = token & 0xF0u;
-            const int32_t c = (int32_t)le32(h + 9), u = (int32_t)le32(h + 13);
-            if (c < 0 || c > (1 << 25)) {  // :136-141
-                snprintf(mbuf, sizeof mbuf, "invalid compressedLength: %d (expected: 0-%d)", c, 1 << 25);
-                fail(NX_ERR_LZ4_COMPRESSED_LENGTH, mbuf, p + 13);
-                break;
-            }
-            const int64_t maxd = (int64_t)1 << level;
-            if (u < 0 || u > maxd) {  // :143-149
-                snprintf(mbuf, sizeof mbuf, "invalid decompressedLength: %d (expected: 0-%lld)", u, (long long)maxd);
-                fail(NX_ERR_LZ4_DECOMPRESSED_LENGTH, mbuf, p + 17);
-                break;
-            }
-            if ((u == 0) != (c == 0) || (blockType == 0x10u && u != c)) {  // :150-156
-                snprintf(mbuf, sizeof mbuf, "stream corrupted: compressedLength(%d) and decompressedLength(%d) mismatch", c, u);
-                fail(NX_ERR_LZ4_LENGTH_MISMATCH, mbuf, p + 17);
-                break;
-            }
-            chk = le32(h + 17);
-            p += kLz4Header;
-            clen = (uint32_t)c;
-            dlen = (uint32_t)u;
-            if (u == 0) {  // :158-166
-                if (chk != 0u) {
-                    fail(NX_ERR_LZ4_END_CHECKSUM, "stream corrupted: checksum error", p);
-                    break;
-                }
-                state = 2;
-                p = n;  // callDecode runs decode() again; FINISHED skips the rest
-                break;
-            }
-            state = 1;
-        }
-        if (state == 1) {
-            if (n - p < clen) break;  // :180-182
-            if (blockType != 0x10u && blockType != 0x20u) {  // :209-213
-                snprintf(mbuf, sizeof mbuf, "unexpected blockType: %u (expected: %d or %d)", blockType, 0x10, 0x20);
-                fail(NX_ERR_LZ4_BLOCK_TYPE, mbuf, p);
-                break;
-            }
-            blks.push_back({p, p + clen, blockType, clen, dlen, chk, -1});
-            p += clen;
-            state = 0;
-        }
-    }
+    nx::af::Lz4State ns = d->st;
+    std::vector<nx::af::Blk> walked;
+    nx::af::WalkErr werr;
+    const size_t p = nx::af::lz4_walk(in, n, ns, walked, werr);
+    std::vector<Blk> blks(walked.size());
+    for (size_t i = 0; i < walked.size(); ++i) static_cast<nx::af::Blk&>(blks[i]) = walked[i];
     // GPU: decode the compressed blocks; hash every block's bytes when validating
     uint32_t nz = 0;
     uint64_t ocap = 0;
@@ -1127,7 +932,7 @@ extern "C" int32_t nx_lz4_frame_decoder_decode(nx_lz4_frame_decoder* d, const ui
         if (b.type == 0x20u) {
             b.job = (int)nz++;
             ooff.push_back(ocap);
-            ocap += ((uint64_t)b.dlen + 15) & ~15ull;
+            ocap += ((uint64_t)b.olen + 15) & ~15ull;
         }
     const uint32_t nb = (uint32_t)blks.size();
     std::vector<int32_t> st(nz);
@@ -1145,7 +950,7 @@ extern "C" int32_t nx_lz4_frame_decoder_decode(nx_lz4_frame_decoder* d, const ui
             if (b.job >= 0) {
                 ioff[b.job] = b.data - lo;
                 ilen[b.job] = b.clen;
-                olen[b.job] = b.dlen;
+                olen[b.job] = b.olen;
             }
         }
         if (!g.din.ensure(span + 1) || !g.dout.ensure(ocap + 16) || !g.a0.ensure(8ull * nb) || !g.a1.ensure(8ull * nb) ||
@@ -1185,9 +990,10 @@ extern "C" int32_t nx_lz4_frame_decoder_decode(nx_lz4_frame_decoder* d, const ui
         const Blk& b = blks[k];
         const uint8_t* data;
         if (b.job >= 0) {
-            if (st[b.job] != NX_OK) {  // LZ4Exception → DecompressionException (:218-219)
-                ml.err = "LZ4 block decompression failed: malformed input";
-                d->state = 3;
+            if (st[b.job] != NX_OK) {  // LZ4Exception → DecompressionException (:240-241)
+                ml.err = nx::af::lz4_block_error();
+                d->st.state = 3;
+                d->corrupted = true;
                 rd = b.data;
                 return finish(st[b.job]);
             }
@@ -1197,34 +1003,30 @@ extern "C" int32_t nx_lz4_frame_decoder_decode(nx_lz4_frame_decoder* d, const ui
         }
         if (d->validate) {  // CompressionUtil.checkChecksum (:226-228; Lz4XXHash32.getValue masks, :101)
             const uint32_t got = (b.job >= 0 ? hz[b.job] : hr[k]) & 0x0FFFFFFFu;
-            if (got != b.chk) {
-                snprintf(mbuf, sizeof mbuf, "stream corrupted: mismatching checksum: %d (expected: %d)", (int32_t)got,
-                         (int32_t)b.chk);
-                ml.err = mbuf;
-                d->state = 3;
+            if (got != b.cks) {
+                ml.err = nx::af::lz4_checksum_error(got, b.cks);
+                d->st.state = 3;
+                d->corrupted = true;
                 rd = b.end;
                 return finish(NX_ERR_LZ4_CHECKSUM_MISMATCH);
             }
         }
         if (b.job >= 0) {
-            ml.owned.emplace_back(data, data + b.dlen);
-            ml.msgs.push_back({ml.owned.back().data(), b.dlen});
+            ml.owned.emplace_back(data, data + b.olen);
+            ml.msgs.push_back({ml.owned.back().data(), b.olen});
         } else {
-            ml.msgs.push_back({in + b.data, b.dlen});
+            ml.msgs.push_back({in + b.data, b.olen});
         }
         rd = b.end;
     }
-    if (perr_code != NX_OK) {
-        ml.err = perr;
-        d->state = 3;
-        rd = perr_at;
-        return finish(perr_code);
+    if (werr.set) {
+        ml.err = werr.msg;
+        d->st.state = 3;
+        d->corrupted = true;
+        rd = werr.at;
+        return finish(werr.code);
     }
     rd = p;
-    d->state = state;
-    d->blockType = blockType;
-    d->compressedLength = clen;
-    d->decompressedLength = dlen;
-    d->currentChecksum = chk;
+    d->st = ns;
     return finish(NX_OK);
 }

@@ -327,10 +327,34 @@ class Batcher:
 
     __del__ = close
 
-    def submit_encode(self, encoder: "SnappyFrameEncoder", data, registered_ptr: int | None = None) -> int:
-        """SnappyFrameEncoder.encode as a job.  With registered_ptr (an address inside memory passed to
-        register()), the bytes are DMA'd from there at flush and must stay valid until completion."""
+    def reserve(self, kinds: int = 0x1F):
+        """Hold the device workspaces of the given kinds now (bit NX_WS_* per kind; default all), so no
+        submit pays for them (nx_batcher_reserve)."""
+        r = _lib.load().nx_batcher_reserve(self._h, kinds)
+        if r != 0:
+            raise RuntimeError(f"nx_batcher_reserve: {_lib.status_string(r)}")
+
+    def _ticket(self, t, what):
+        if t < 0:
+            raise RuntimeError(f"{what}: {_lib.status_string(t)}")
+        return t
+
+    def submit_encode(self, encoder, data, registered_ptr: int | None = None, reader_index: int = 0, op: int = 0) -> int:
+        """encode() of any encoder handler as a job: SnappyFrameEncoder (with registered_ptr, an address
+        inside memory passed to register(), the bytes are DMA'd from there at flush and must stay valid
+        until completion), FastLzFrameEncoder (``reader_index`` as in encode()), LzfEncoder,
+        Lz4FrameEncoder (``op`` 0 encode, 1 encode + flush, 2 encode + close)."""
         L = _lib.load()
+        if isinstance(encoder, FastLzFrameEncoder):
+            buf = bytes(reader_index) + bytes(data)
+            return self._ticket(L.nx_fastlz_frame_encoder_submit(encoder._h, self._h, buf, reader_index, len(data)),
+                                "nx_fastlz_frame_encoder_submit")
+        if isinstance(encoder, LzfEncoder):
+            buf = bytes(data)
+            return self._ticket(L.nx_lzf_encoder_submit(encoder._h, self._h, buf, len(buf)), "nx_lzf_encoder_submit")
+        if isinstance(encoder, Lz4FrameEncoder):
+            buf = bytes(data)
+            return self._ticket(L.nx_lz4_frame_encoder_submit(encoder._h, self._h, buf, len(buf), op), "nx_lz4_frame_encoder_submit")
         if registered_ptr is not None:
             t = L.nx_snappy_frame_encoder_submit(encoder._h, self._h, C.c_void_p(registered_ptr), len(data), 1)
         else:
@@ -340,16 +364,21 @@ class Batcher:
             raise RuntimeError(f"nx_snappy_frame_encoder_submit: {_lib.status_string(t)}")
         return t
 
-    def submit_decode(self, decoder: "SnappyFrameDecoder", data) -> int:
-        """SnappyFrameDecoder.decode over the decoder's cumulation + data as a job; the consumed bytes
-        leave the cumulation now (ByteToMessageDecoder.channelRead)."""
+    _DECODE_SUBMIT = {"SnappyFrameDecoder": "nx_snappy_frame_decoder_submit",
+                      "FastLzFrameDecoder": "nx_fastlz_frame_decoder_submit",
+                      "LzfDecoder": "nx_lzf_decoder_submit",
+                      "Lz4FrameDecoder": "nx_lz4_frame_decoder_submit"}
+
+    def submit_decode(self, decoder, data) -> int:
+        """decode() of any decoder handler over its cumulation + data as a job; the consumed bytes leave
+        the cumulation now (ByteToMessageDecoder.channelRead)."""
         L = _lib.load()
+        fn = next(v for k, v in self._DECODE_SUBMIT.items() if type(decoder).__name__ == k or
+                  any(c.__name__ == k for c in type(decoder).__mro__))
         decoder._cum += bytes(data)
         buf = bytes(decoder._cum)
         consumed = C.c_size_t(0)
-        t = L.nx_snappy_frame_decoder_submit(decoder._h, self._h, buf, len(buf), C.byref(consumed))
-        if t < 0:
-            raise RuntimeError(f"nx_snappy_frame_decoder_submit: {_lib.status_string(t)}")
+        t = self._ticket(getattr(L, fn)(decoder._h, self._h, buf, len(buf), C.byref(consumed)), fn)
         del decoder._cum[:consumed.value]
         return t
 
