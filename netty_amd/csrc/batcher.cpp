@@ -1668,8 +1668,9 @@ int64_t alt_decoder_submit(D* d, St& st, nx_batcher* b, const uint8_t* in, size_
                 P.slot = bt->aslots;
                 bt->aslots += align16(k.olen) + 16;
                 Batch::AltList& L = codec == 0 ? bt->flz_d : (codec == 1 ? bt->lzf_d : bt->lz4_d);
-                // FastLZ: aux = in_avail (readable bytes from the block on); LZF / LZ4: the decoded length
-                P.res = push_list(L, P.src, k.clen, P.slot, codec == 0 ? (uint32_t)(n - k.data) : k.olen);
+                // FastLZ: aux = in_avail (readable bytes from the block on), lim = originalLength;
+                // LZF / LZ4: aux = the decoded length
+                P.res = push_list(L, P.src, k.clen, P.slot, codec == 0 ? (uint32_t)(n - k.data) : k.olen, (int32_t)k.olen);
                 P.kind = codec == 0 ? nx::bt::AK_DEC_FLZ : (codec == 1 ? nx::bt::AK_DEC_LZF : nx::bt::AK_DEC_LZ4);
             }
             bt->apc.push_back(P);
@@ -1927,6 +1928,12 @@ extern "C" int32_t nx_batcher_wait(nx_batcher* b, int64_t ticket) {
         }
         if (hipEventSynchronize(bt->ev) != hipSuccess) return NX_ERR_HIP;
         std::lock_guard<std::mutex> lk(b->mu);
+        // Unlocked, another thread's apply() may have moved the job into a continuation batch (a
+        // re-walk), after which bt can be reset and reused: look the ticket up again, and wait on
+        // its new batch if it moved.
+        auto it = b->tickets.find((uint64_t)ticket);
+        if (it == b->tickets.end()) return NX_ERR_INVALID_ARG;
+        if (it->second.first != bt) continue;
         if (!poll_batch(b, bt, true)) return NX_ERR_HIP;
         kick(b);
         if (j->applied) return NX_OK;

@@ -71,8 +71,8 @@ struct WaveLds {
     // tag records {start (absolute output position), x (bit31 = copy; low 31 bits = literal source
     // position or copy offset)}; the start of record r+1 is the end of record r (sentinel after the last)
     uint32_t tagw[2 * 64 + 2];
-    uint32_t scratch[64];        // parse: tag-start marks; expand: first-piece marks, then byte -> piece map
-    uint32_t pad[2];
+    uint32_t scratch[65];        // parse: tag-start marks; expand: first-piece marks (+ a spare slot), then byte -> piece map
+    uint32_t pad[1];
 };
 static_assert(sizeof(WaveLds) % 16 == 0, "keep per-wave LDS 16-byte aligned");
 static_assert(2 * (kTabBytes + kWaves * sizeof(WaveLds)) <= 160 * 1024, "two workgroups per CU");
@@ -301,11 +301,18 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
     uint32_t pbc = 0;  // its first piece
     // (a non-last window holds >= 64 unproduced pieces: its first record has one, every other one)
     const uint32_t Pend = last ? Ptot : P0s + ((Ptot - P0s) & ~63u);
+    // marks go to scratch[pbase - P0]; a tag whose first piece lies outside the pass writes the spare
+    // slot scratch[64] instead, so the store needs no divergent branch
+    uint32_t* const marks = L.scratch;
     for (uint32_t P0 = P0s; P0 < Pend; P0 += 64u) {
         // piece -> tag: each tag marks its first piece, then a max-scan over the lanes
         L.scratch[lane] = 0u;
         wave_sync();
-        if (prod && pbase >= P0 && pbase < P0 + 64u) L.scratch[pbase - P0] = ((rank + 1u) << 6) | (pbase - P0);
+        {
+            const uint32_t rel = pbase - P0;  // wraps for pbase < P0
+            const bool in_pass = prod && rel < 64u;
+            marks[in_pass ? rel : 64u] = ((rank + 1u) << 6) | (rel & 63u);
+        }
         wave_sync();
         const uint32_t mk = incl_max_scan(L.scratch[lane]);
         const uint32_t P = P0 + lane;
@@ -345,6 +352,30 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
         const uint32_t sh = 8u * (x0 & 3u);
         const uint32_t bmask = (nbytes >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nbytes)) - 1u)) << sh;
         const uint32_t waddr = lds_base + 4u * ((x0 >> 2) & (kRing / 4 - 1));
+        // Sources that do not depend on this pass, loaded first so that their latency overlaps the
+        // producer map and the first round: far copies (the frame's own flushed output) and literal
+        // bytes outside the stage, from HBM.  A literal piece among the chunk's last 3 bytes reads
+        // the chunk's last dword and shifts (chunks under 4 bytes take the byte loop).
+        // (gval is used untouched until the first round: any operation on it here, a phi with
+        // another path's value included, would make the compiler wait for the load at once.)
+        uint32_t gval;       // read only by lanes with gl (a zero store here made the compiler wait for every in-flight load and store)
+        uint32_t gsh = 0;    // right shift of gval (a read of the chunk's last dword)
+        uint32_t gtiny = 0;  // chunks under 4 bytes: the bytes, read one by one
+        const bool gld = valid && gl;
+        const bool tiny = io.in_len < 4u;
+        if (__ballot(gld)) {
+            const bool tail = lit && pin + 4u > io.in_len;
+            const uint8_t* ga = !lit ? io.dst + sp : io.src + (tail ? io.in_len - 4u : pin);
+            if (gld && !tiny) gval = g_ld32u(ga);
+            gsh = tail ? 8u * (pin + 4u - io.in_len) : 0u;
+            if (tiny && __ballot(gld)) {
+                if (gld) {
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i)
+                        if (pin + i < io.in_len) gtiny |= g_ld8(io.src + pin + i) << (8 * i);
+                }
+            }
+        }
         // Producer map: byte x of this pass holds the lane (piece) that writes it.  A copy whose
         // source bytes lie in this pass depends on the contiguous piece range that produces them,
         // and runs in the first round after all of those are done.  The map aliases `scratch`
@@ -355,7 +386,8 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
         const uint32_t dhi = overlap ? tstart : sp + nbytes;  // end of the source bytes this piece reads
         const bool dep = valid && !lit && !gl && dhi > ps;
         uint64_t need = 0;
-        if (__ballot(dep)) {
+        const uint64_t depm = __ballot(dep);
+        if (depm) {
             wave_sync();
             {
                 const uint32_t mm = valid ? bmask : 0u;
@@ -363,75 +395,58 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
                 asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(maddr), "v"(mm), "v"(((uint32_t)lane * 0x01010101u) & mm) : "memory");
             }
             wave_sync();
-            if (dep) {
-                const uint32_t lo0 = overlap ? tstart - xo : sp;
-                const uint8_t* M8 = reinterpret_cast<const uint8_t*>(L.scratch);
-                const uint32_t lo = lo0 > ps ? lo0 : ps;
-                const uint32_t pa = M8[lo - psal], pb = M8[dhi - 1u - psal];
-                need = (pb >= 63u ? ~0ull : ((2ull << pb) - 1ull)) & ~((1ull << (pa & 63u)) - 1ull);
-            }
-        }
-        // Sources that do not depend on this pass, fetched once before the rounds: far copies (the
-        // frame's own flushed output) and literal bytes outside the stage, from HBM.  (Guarded by
-        // wave-uniform branches so that passes without such pieces skip them entirely.)
-        uint32_t gval;  // read only by lanes with gl (a zero store here made the compiler wait for every in-flight load and store)
-        if (__ballot(valid && gl)) {
-            if (valid && gl) {
-                if (!lit) {
-                    gval = g_ld32u(io.dst + sp);  // flushed and drained output of this frame
-                } else if (pin + 4u <= io.in_len) {
-                    gval = g_ld32u(io.src + pin);
-                } else {
-                    gval = 0;
-#pragma unroll
-                    for (uint32_t i = 0; i < 4; ++i)
-                        if (pin + i < io.in_len) gval |= g_ld8(io.src + pin + i) << (8 * i);
-                }
-            }
+            // every lane reads (non-dependent lanes at byte 0) and keeps the result only if dependent
+            const uint32_t lo0 = overlap ? tstart - xo : sp;
+            const uint8_t* M8 = reinterpret_cast<const uint8_t*>(L.scratch);
+            const uint32_t lo = lo0 > ps ? lo0 : ps;
+            const uint32_t pa = M8[dep ? lo - psal : 0u], pb = M8[dep ? dhi - 1u - psal : 0u];
+            const uint64_t nm = (pb >= 63u ? ~0ull : ((2ull << pb) - 1ull)) & ~((1ull << (pa & 63u)) - 1ull);
+            need = dep ? nm : 0ull;
         }
         // Overlapping copies (offset < length): out[x] = out[tstart - xo + ((x - tstart) mod xo)],
-        // xo < tlen <= 64; the four ring byte addresses, packed 4 x 12 bits into two dwords.
+        // xo < tlen <= 64; the four ring byte addresses, packed 4 x 12 bits into two dwords
+        // (computed by every lane, used by overlapping pieces only).
         const bool has_ov = __ballot(valid && overlap) != 0ull;
         uint32_t ova = 0, ovb = 0;
         if (has_ov) {
-            if (valid && overlap) {
-                const uint32_t n0 = x0 - tstart;
-                const uint32_t inv = (uint32_t)(__builtin_amdgcn_rcpf((float)xo) * 65536.0f) + 1u;  // floor(n0/xo) exact for n0, xo < 64
-                const uint32_t m0 = n0 - xo * ((n0 * inv) >> 16);
-                const uint32_t q = tstart - xo;
-                uint32_t ad[4];
-                uint32_t mi = m0;  // (n0 + i) mod xo, stepped: m0 < xo, so one wrap test per byte
+            const uint32_t n0 = x0 - tstart;
+            const uint32_t inv = (uint32_t)(__builtin_amdgcn_rcpf((float)xo) * 65536.0f) + 1u;  // floor(n0/xo) exact for n0, xo < 64
+            const uint32_t m0 = n0 - xo * ((n0 * inv) >> 16);
+            const uint32_t q = tstart - xo;
+            uint32_t ad[4];
+            uint32_t mi = m0;  // (n0 + i) mod xo, stepped: m0 < xo, so one wrap test per byte
 #pragma unroll
-                for (uint32_t i = 0; i < 4; ++i) {
-                    if (i) mi = mi + 1u == xo ? 0u : mi + 1u;
-                    ad[i] = (q + mi) & (kRing - 1);
-                }
-                ova = ad[0] | (ad[1] << 16);
-                ovb = ad[2] | (ad[3] << 16);
+            for (uint32_t i = 0; i < 4; ++i) {
+                if (i) mi = mi + 1u == xo ? 0u : mi + 1u;
+                ad[i] = (q + mi) & (kRing - 1);
             }
+            ova = ad[0] | (ad[1] << 16);
+            ovb = ad[2] | (ad[3] << 16);
         }
-        uint64_t pending = __ballot(valid);
-        uint64_t done = ~pending;
-        for (int round = 0; pending; ++round) {
-            if (round > 64) return false;
-            const bool ready = ((pending >> lane) & 1ull) != 0 && (need & ~done) == 0ull;
+        // Rounds.  Round 0 writes every piece with no producer in this pass; then a pending piece is
+        // ready once none of its producers is pending (every valid piece not pending is written).
+        const uint32_t w = sp >> 2;
+        const uint32_t ra0 = lbase + (w & lmask), ra1 = lbase + ((w + 1u) & lmask);
+        bool ready = valid && !dep;
+        uint64_t pending = depm;
+        for (int round = 0;; ++round) {
             // stage (literal) or ring (near copy): one unaligned 4-byte read, all lanes
-            const uint32_t w = sp >> 2;
-            const uint32_t lo = lds32[lbase + (w & lmask)];
-            const uint32_t hi = lds32[lbase + ((w + 1u) & lmask)];
-            uint32_t val = gl ? gval : __builtin_amdgcn_alignbyte(hi, lo, sp & 3u);
-            if (has_ov && __ballot(ready && overlap)) {
-                if (ready && overlap) {
-                    val = (uint32_t)ring8[ova & 0xFFFFu] | ((uint32_t)ring8[ova >> 16] << 8) | ((uint32_t)ring8[ovb & 0xFFFFu] << 16) |
-                          ((uint32_t)ring8[ovb >> 16] << 24);
-                }
+            uint32_t lo = lds32[ra0];
+            uint32_t hi = lds32[ra1];
+            asm volatile("" : "+v"(lo), "+v"(hi));  // read on every lane: no exec-mask branch around the reads
+            uint32_t val = gl ? (tiny ? gtiny : gval >> gsh) : __builtin_amdgcn_alignbyte(hi, lo, sp & 3u);
+            if (has_ov) {
+                const uint32_t ov = (uint32_t)ring8[ova & 0xFFFFu] | ((uint32_t)ring8[ova >> 16] << 8) |
+                                    ((uint32_t)ring8[ovb & 0xFFFFu] << 16) | ((uint32_t)ring8[ovb >> 16] << 24);
+                val = overlap ? ov : val;
             }
             // one masked atomic write per lane: the piece's bytes, or nothing (mask 0)
             const uint32_t m = ready ? bmask : 0u;
             asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(waddr), "v"(m), "v"((val << sh) & m) : "memory");
-            const uint64_t rb = __ballot(ready);
-            pending &= ~rb;
-            done |= rb;
+            if (!pending) break;
+            if (round >= 64) return false;
+            ready = ((pending >> lane) & 1ull) != 0 && (need & pending) == 0ull;
+            pending &= ~__ballot(ready);
         }
         // Flush at the END of the pass, its bytes final (round 3; was at the start, flush_to(ps)): the
         // flush's stores then precede the next pass's far-copy loads by a pass of work, so the wait

@@ -28,7 +28,7 @@ import re
 import struct
 from dataclasses import dataclass, field
 
-from .handlers import Batcher, EmbeddedChannel, SnappyFrameDecoder, SnappyFrameEncoder
+from .handlers import DecoderException, Batcher, EmbeddedChannel, SnappyFrameDecoder, SnappyFrameEncoder
 
 SNAPPY = "snappy"  # HttpHeaderValues.SNAPPY (HttpHeaderValues.java:124-126)
 
@@ -166,14 +166,28 @@ class _Ordered:
         self.q.append([ticket, build])
 
     def poll(self) -> list:
-        """Messages whose turn has come (a running job stops the release; never blocks)."""
+        """Messages whose turn has come (a running job stops the release; never blocks).
+
+        A job that failed (a corrupted body) raises its DecoderException once, after its entry has
+        left the queue: ``e.messages`` holds what this poll released before it plus the contents the
+        job decoded before the failure (its LastHttpContent is not released: the reference's exception
+        leaves HttpContentDecoder.decode before finishDecode).  The messages queued behind it come out
+        on the next polls; the body's later contents decode to nothing, as the corrupted decoder skips
+        its input (SnappyFrameDecoder.java:86-89), and its LastHttpContent still ends the message."""
         out = []
         while self.q:
             t, m = self.q[0]
             if t is not None:
                 if not self.b.poll(t):
                     break
-                m = m(self.b.result(t))
+                self.q.popleft()
+                try:
+                    r = self.b.result(t)
+                except DecoderException as e:
+                    e.messages = out + [x for x in m(list(getattr(e, "decoded", []))) if not isinstance(x, LastHttpContent)]
+                    raise
+                out.extend(m(r))
+                continue
             self.q.popleft()
             out.extend(m if isinstance(m, list) else [m])
         return out

@@ -143,3 +143,44 @@ def test_nonblocking_snappy_http_bodies(oracle):
         assert dec_body == b"".join(parts)
         assert din[k] == http.LastHttpContent(b"", {"t": "1"})
         assert din[k + 1].headers == {"content-length": "3"} and din[k + 2] == http.LastHttpContent(b"abc")
+
+
+@pytest.mark.gpu
+def test_nonblocking_snappy_http_corrupted_body_then_next_message(oracle):
+    """A corrupted snappy body raises its DecompressionException once: the contents
+    decoded before the failure come with it, the body's later contents decode to nothing and its
+    LastHttpContent still ends the message, and the next message on the same channel comes out."""
+    from netty_amd.handlers import Batcher, DecompressionException
+    b = Batcher()
+    good = oracle.textgen_chunk(3, 40000)
+    framed, _ = oracle.snappy_frame_encode(good)
+    c2 = 10 + 4 + int.from_bytes(framed[11:14], "little")  # the second chunk's header
+    bad = bytearray(framed)
+    bad[c2 + 8 + 20] ^= 0xFF  # damage the second chunk's payload
+    first = bytes(bad[:c2 - 3])  # the stream identifier and most of the first chunk
+    dec = http.SnappyHttpBodyDecoder(b, validate_checksums=True)
+    dec.read(http.HttpMessage({"content-encoding": "snappy"}))
+    dec.read(http.HttpContent(first))
+    dec.read(http.HttpContent(bytes(bad[len(first):])))
+    dec.read(http.HttpContent(b"more bytes after the failure"))
+    dec.read(http.LastHttpContent(b"", {"t": "x"}))
+    dec.read(http.HttpMessage({"content-length": "3"}))
+    dec.read(http.LastHttpContent(b"abc"))
+    b.flush()
+    import time
+    got, err, t0 = [], None, time.time()
+    while sum(isinstance(m, http.LastHttpContent) for m in got) < 2:
+        try:
+            got += dec.poll()
+        except DecompressionException as e:
+            assert err is None, "the failure is raised once"
+            err = e
+            got += e.messages
+        assert time.time() - t0 < 60
+    assert err is not None and "checksum" in str(err)
+    assert isinstance(got[0], http.HttpMessage)
+    body = b"".join(m.content for m in got[1:] if type(m) is http.HttpContent)
+    assert good.startswith(body) and len(body) >= 32767  # the first chunk's message came out
+    lasts = [m for m in got if isinstance(m, http.LastHttpContent)]
+    assert lasts[0].trailers == {"t": "x"} and lasts[1] == http.LastHttpContent(b"abc")
+    assert got[-3].headers == {"content-length": "3"}
