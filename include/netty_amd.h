@@ -383,6 +383,14 @@ int32_t nx_batcher_set_flush_bytes(nx_batcher* b, size_t bytes);
  * encoders' tables; a quarter of that, and so on down to 1 024, when the device cannot spare it).
  * nx_batcher_new itself reserves nothing (a decode-only batcher never holds encoder tables). */
 int32_t nx_batcher_reserve(nx_batcher* b, uint32_t kinds);
+/* Pinned host arenas (the staging copy of submitted bytes and the mapped result memory) grow inside
+ * submit when a batch outgrows them.  nx_batcher_reserve_arenas sizes them up front: at least
+ * `nbatches` batch objects with staging_bytes / out_bytes each, so that submits of a server whose
+ * auto-flush threshold stays below staging_bytes never allocate (ByteToMessageDecoder.java:286-341
+ * runs on the event loop).  nx_batcher_arena_stats reports the allocations made so far (growth
+ * included), the pinned bytes held and the number of batch objects. */
+int32_t nx_batcher_reserve_arenas(nx_batcher* b, uint32_t nbatches, size_t staging_bytes, size_t out_bytes);
+int32_t nx_batcher_arena_stats(nx_batcher* b, uint64_t* allocs, uint64_t* bytes, uint32_t* batches);
 
 /* The FastLZ, LZF and LZ4 handlers as batcher jobs, with the Snappy jobs' contract (one launch per
  * codec kernel per flush for every job of every channel; results applied in submission order per

@@ -389,10 +389,15 @@ using nx::fr::SnappyAction;
 
 namespace {
 
+struct ArenaCount {  // the batcher's pinned arenas: allocations made (growth included) and bytes held
+    uint64_t allocs = 0, bytes = 0;
+};
+
 struct Pinned {  // hipHostMalloc'd, mapped into the device address space; grows keeping its bytes
     uint8_t* h = nullptr;
     uint8_t* d = nullptr;
     size_t cap = 0;
+    ArenaCount* cnt = nullptr;
     bool ensure(size_t n, size_t keep) {
         if (n <= cap) return true;
         size_t c = cap ? cap : (1u << 20);
@@ -407,6 +412,10 @@ struct Pinned {  // hipHostMalloc'd, mapped into the device address space; grows
         }
         if (h && keep) memcpy(nh, h, keep < cap ? keep : cap);
         if (h) (void)hipHostFree(h);
+        if (cnt) {
+            cnt->allocs += 1;
+            cnt->bytes += c - cap;
+        }
         h = nh;
         d = nd;
         cap = c;
@@ -414,6 +423,7 @@ struct Pinned {  // hipHostMalloc'd, mapped into the device address space; grows
     }
     ~Pinned() {
         if (h) (void)hipHostFree(h);
+        if (cnt) cnt->bytes -= cap;
     }
 };
 
@@ -586,6 +596,7 @@ struct nx_batcher {
     uint64_t launches = 0, chunks = 0, flushes = 0;
     uint64_t applied = 0;     // batches applied, in flush order (Batch::seq < applied)
     size_t flush_bytes = 0;   // auto-flush threshold on a batch's input bytes (0 = only explicit flushes)
+    ArenaCount arena;         // pinned staging / result arenas of all batches
     std::vector<std::pair<Job*, Batch*>> cont;  // re-walked jobs to queue again (found by apply())
     bool kick = false;        // the collecting batch holds a re-walked job: launch it at the next poll/wait
 };
@@ -606,6 +617,7 @@ Batch* reuse_or_new_batch(nx_batcher* b) {
         delete x;
         return nullptr;
     }
+    x->staging.cnt = x->out.cnt = &b->arena;
     b->all.push_back(x);
     return x;
 }
@@ -1968,6 +1980,37 @@ extern "C" int32_t nx_batcher_set_flush_bytes(nx_batcher* b, size_t bytes) {
     if (!b) return NX_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(b->mu);
     b->flush_bytes = bytes;
+    return NX_OK;
+}
+
+// Size the pinned arenas now: at least `nbatches` batch objects, each with a staging arena of
+// staging_bytes and a result arena of out_bytes, so that submits (on the event loops) never call
+// hipHostMalloc / hipHostFree once batches stay within those sizes (set the auto-flush threshold
+// below staging_bytes).
+extern "C" int32_t nx_batcher_reserve_arenas(nx_batcher* b, uint32_t nbatches, size_t staging_bytes, size_t out_bytes) {
+    if (!b) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    std::vector<Batch*> made;
+    while (b->all.size() < nbatches) {
+        Batch* x = new Batch();
+        if (hipEventCreateWithFlags(&x->ev, hipEventDisableTiming) != hipSuccess) {
+            delete x;
+            return NX_ERR_HIP;
+        }
+        x->staging.cnt = x->out.cnt = &b->arena;
+        b->all.push_back(x);
+    }
+    for (Batch* x : b->all)  // an in-flight batch's arenas are in use: sized when it is reused
+        if (!x->inflight && (!x->staging.ensure(staging_bytes, x->st_used) || !x->out.ensure(out_bytes, x->out_used))) return NX_ERR_HIP;
+    return NX_OK;
+}
+
+extern "C" int32_t nx_batcher_arena_stats(nx_batcher* b, uint64_t* allocs, uint64_t* bytes, uint32_t* batches) {
+    if (!b) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (allocs) *allocs = b->arena.allocs;
+    if (bytes) *bytes = b->arena.bytes;
+    if (batches) *batches = (uint32_t)b->all.size();
     return NX_OK;
 }
 

@@ -334,6 +334,18 @@ class Batcher:
         if r != 0:
             raise RuntimeError(f"nx_batcher_reserve: {_lib.status_string(r)}")
 
+    def reserve_arenas(self, nbatches: int, staging_bytes: int, out_bytes: int):
+        """Size the pinned arenas now (nx_batcher_reserve_arenas): submits then never allocate."""
+        r = _lib.load().nx_batcher_reserve_arenas(self._h, nbatches, staging_bytes, out_bytes)
+        if r != 0:
+            raise RuntimeError(f"nx_batcher_reserve_arenas: {_lib.status_string(r)}")
+
+    def arena_stats(self) -> dict:
+        a, n = C.c_uint64(0), C.c_uint64(0)
+        k = C.c_uint32(0)
+        _lib.load().nx_batcher_arena_stats(self._h, C.byref(a), C.byref(n), C.byref(k))
+        return {"allocs": a.value, "bytes": n.value, "batches": k.value}
+
     def _ticket(self, t, what):
         if t < 0:
             raise RuntimeError(f"{what}: {_lib.status_string(t)}")

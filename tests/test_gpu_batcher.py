@@ -432,3 +432,87 @@ def test_batcher_leftover_with_released_tickets(nx, oracle):
         t = b.submit_decode(other, oracle.snappy_frame_encode(data, started=_ > 0)[0])
         b.wait(t)
         assert b"".join(b.result(t)) == data
+
+
+def test_batcher_tiny_chunks_claiming_64k_keep_their_neighbours(oracle):
+    """the batcher packs decode slots by what a chunk can decode to (64 bytes per 3
+    compressed bytes), not by the 65536 its preamble may claim.  Tiny chunks claiming 65536, and
+    chunks that decode to exactly their bound, sit between ordinary ones in one flush: every
+    message equals the oracle's, so no slot overran into its neighbour."""
+    import random
+    import netty_amd as nx
+    from oracle import frame_decoders as F
+    rng = random.Random(77)
+    sid = bytes.fromhex("ff060000734e61507059")
+
+    def chunk(payload, crc_of):
+        return b"\x00" + (len(payload) + 4).to_bytes(3, "little") + oracle.snappy_checksum(crc_of).to_bytes(4, "little") + payload
+
+    b = nx.Batcher()
+    chans = []
+    for i in range(300):
+        parts = [sid]
+        for k in range(rng.randint(1, 4)):
+            kind = rng.randrange(3)
+            if kind == 0:  # preamble 65536, one 1-byte literal
+                v = bytes([rng.randrange(256)])
+                parts.append(chunk(b"\x80\x80\x04" + b"\x00" + v, v))
+            elif kind == 1:  # at the bound: literal 'a' then copy-2 tags of 64 bytes, offset 1
+                n = rng.randint(1, 40)
+                body = b"\x00a" + b"\xfe\x01\x00" * n
+                raw = b"a" * (1 + 64 * n)
+                pre = oracle.snappy_encode(raw)[:3]  # the varint of len(raw)
+                plen = 1 + (len(raw) >= 128) + (len(raw) >= 16384)
+                parts.append(chunk(pre[:plen] + body, raw))
+            else:
+                m = oracle.textgen_chunk(rng.randrange(1 << 20), rng.randint(1, 30000))
+                parts.append(oracle.snappy_frame_encode(m, started=True)[0])
+        stream = b"".join(parts)
+        chans.append((nx.SnappyFrameDecoder(True), stream, rng.random() < 0.5))
+    tickets = [b.submit_decode(d, s) for d, s, _ in chans]
+    b.flush()
+    for (d, s, _), t in zip(chans, tickets):
+        b.wait(t)
+        try:
+            got, err = b.result(t), None
+        except nx.DecoderException as e:
+            got, err = list(e.decoded), (type(e).__name__, str(e))
+        want = F.run(F.SnappyFrameDecoder(True), [s])
+        assert (got, err) == want
+
+
+def test_batcher_reserved_arenas_do_not_grow(oracle):
+    """with the pinned arenas sized up front (nx_batcher_reserve_arenas) and the
+    auto-flush threshold below them, rounds of submits / flushes after a warm-up allocate nothing."""
+    import random
+    import netty_amd as nx
+    rng = random.Random(3)
+    b = nx.Batcher()
+    b.reserve(1 << 4)  # the decoder's record workspace, up front
+    b.reserve_arenas(8, 8 << 20, 40 << 20)
+    b.set_flush_bytes(4 << 20)
+    streams = []
+    for i in range(48):
+        data = oracle.textgen_chunk(rng.randrange(1 << 20), rng.randint(20000, 200000))
+        streams.append((data, oracle.snappy_frame_encode(data)[0]))
+
+    def one_round():
+        decs = [nx.SnappyFrameDecoder(True) for _ in streams]
+        tickets = []
+        for d, (_, s) in zip(decs, streams):
+            q = len(s) // 2
+            tickets.append([b.submit_decode(d, s[:q]), b.submit_decode(d, s[q:])])
+        b.flush()
+        for (data, _), ts in zip(streams, tickets):
+            out = []
+            for t in ts:
+                b.wait(t)
+                out += b.result(t)
+            assert b"".join(out) == data
+
+    one_round()
+    before = b.arena_stats()
+    for _ in range(3):
+        one_round()
+    after = b.arena_stats()
+    assert after["allocs"] == before["allocs"], (before, after)

@@ -102,7 +102,7 @@ def test_lz4_encoder_jobs_equal_sync(nx, oracle, block_size):
     got = _run_jobs(b, chans)
     for (_, msgs), op, outs in zip(chans, ops, got):
         s = nx.Lz4FrameEncoder(block_size)
-        for m, o, k in zip(msgs, op, outs):
+        for m, k, o in zip(msgs, op, outs):
             want = s.encode(m)
             if k == 1:
                 want += s.flush()
