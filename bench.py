@@ -603,17 +603,21 @@ def device_info(torch, dev):
     return info
 
 
-def e2e_capi(channels: int, messages: int, timeout: float = 240.0):
+def e2e_capi(channels: int, messages: int, timeout: float = 240.0, dec_flush_mib: int = 256):
     """Host-to-host Snappy frame round trip through the asynchronous batcher C-ABI
     (netty_amd/tools/e2e_capi.cpp): `channels` SnappyFrameEncoder/Decoder pairs, `messages` 65535-byte
-    text messages each in registered host memory, one flush per direction.  Run as a child process
-    (its own HIP context); returns its JSON, or the failure."""
+    text messages each in registered host memory; encode in one flush, decode auto-flushed every
+    `dec_flush_mib` MiB (the batches rotate over four streams, so one batch's PCIe gather overlaps the
+    previous one's result writes).  Workspaces and pinned arenas are reserved before the timed rounds;
+    `arena_allocs_after_round0` counts pinned allocations after the first round (0: none on the submit
+    path).  Run as a child process (its own HIP context); returns its JSON, or the failure."""
     import subprocess
     exe = os.path.join(ROOT, "netty_amd", "e2e_capi")
     if not os.path.exists(exe):
         return {"error": "netty_amd/e2e_capi not built (make -C netty_amd)"}
     try:
-        r = subprocess.run([exe, str(channels), str(messages), "65535", "3"], capture_output=True, text=True, timeout=timeout)
+        r = subprocess.run([exe, str(channels), str(messages), "65535", "3", "0", str(dec_flush_mib)], capture_output=True, text=True,
+                           timeout=timeout)
     except subprocess.TimeoutExpired:
         return {"error": f"timed out after {timeout}s"}
     try:
@@ -622,7 +626,7 @@ def e2e_capi(channels: int, messages: int, timeout: float = 240.0):
         return {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
     d["path"] = ("pooled-direct-ByteBuf stand-in (registered host memory) -> nx_snappy_frame_encoder_submit x N -> one flush "
                  "-> framed bytes in mapped pinned memory -> (network: copied, untimed, into a registered receive buffer) -> "
-                 "nx_snappy_frame_decoder_submit_registered x N -> one flush -> messages; decode_copied_*: the same through "
+                 "nx_snappy_frame_decoder_submit_registered x N (auto-flush every decode_flush_mib) -> messages; decode_copied_*: the same through "
                  "nx_snappy_frame_decoder_submit (payloads copied at submit)")
     return d
 

@@ -713,9 +713,9 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
 // tags instead of one per tag for whichever lane happens to cross a block.
 constexpr int kParseBlock = 256;
 constexpr int kWinDw = 17;
-// PF: after each reload the lane also loads the window that follows into registers, so the next
-// reload (usually that window: tags advance through the stream) waits for nothing.
-template <uint32_t NB, bool PF = false>  // window of NB 16-byte blocks; LDS stride 4 * NB + 1 dwords (conflict-free)
+// (Round 4: a register prefetch of the following window at each reload measured 1.5 % slower end to
+// end, 54.7 vs 53.9 ms per 262 144 frames on one box, and was removed.)
+template <uint32_t NB>  // window of NB 16-byte blocks; LDS stride 4 * NB + 1 dwords (conflict-free)
 struct BurstWinT {
     static constexpr uint32_t kBytes = 16u * NB;
     static constexpr int kStride = 4 * (int)NB + 1;
@@ -723,15 +723,12 @@ struct BurstWinT {
     uint32_t pad, end;      // chunk start - origin; chunk end, origin-relative
     uint32_t base;          // window = origin-relative [base, base + kBytes)
     uint32_t* w;            // this lane's LDS window
-    v4u pf[PF ? NB : 1];    // the prefetched following window
-    uint32_t pfbase;        // its base (0xFFFFFFFF: none)
     __device__ __forceinline__ void init(const uint8_t* in, uint32_t length, uint32_t* lds) {
         origin = reinterpret_cast<const uint8_t*>((uintptr_t)in & ~(uintptr_t)15);
         pad = (uint32_t)((uintptr_t)in & 15u);
         end = pad + length;
         base = 0xFFFFFF00u;
         w = lds;
-        pfbase = 0xFFFFFFFFu;
     }
     // are the (up to) 5 header bytes at chunk position p in the window?
     __device__ __forceinline__ bool has(uint32_t p) const {
@@ -746,15 +743,10 @@ struct BurstWinT {
         base = (p + pad) & ~15u;
         const uint32_t last = (end - 1u) & ~15u;
         v4u x[NB];
-        if (PF && base == pfbase) {
 #pragma unroll
-            for (uint32_t k = 0; k < NB; ++k) x[k] = pf[PF ? k : 0];
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < NB; ++k) {
-                const uint32_t o = base + 16u * k;
-                x[k] = *(const gv4u*)(origin + (o <= last ? o : last));
-            }
+        for (uint32_t k = 0; k < NB; ++k) {
+            const uint32_t o = base + 16u * k;
+            x[k] = *(const gv4u*)(origin + (o <= last ? o : last));
         }
 #pragma unroll
         for (uint32_t k = 0; k < NB; ++k) {
@@ -762,17 +754,6 @@ struct BurstWinT {
             w[4 * k + 1] = x[k].y;
             w[4 * k + 2] = x[k].z;
             w[4 * k + 3] = x[k].w;
-        }
-        if (PF) {
-            const uint32_t nb = base + kBytes;
-            pfbase = nb <= last ? nb : 0xFFFFFFFFu;
-            if (nb <= last) {
-#pragma unroll
-                for (uint32_t k = 0; k < NB; ++k) {
-                    const uint32_t o = nb + 16u * k;
-                    pf[PF ? k : 0] = *(const gv4u*)(origin + (o <= last ? o : last));
-                }
-            }
         }
     }
     // 8 bytes at chunk position p, has(p) (bytes at or past the chunk end are unspecified)
@@ -783,10 +764,7 @@ struct BurstWinT {
         return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
     }
 };
-#ifndef NX_PARSE_PF
-#define NX_PARSE_PF 1
-#endif
-using BurstWin = BurstWinT<4, NX_PARSE_PF != 0>;
+using BurstWin = BurstWinT<4>;
 static_assert(BurstWin::kStride == kWinDw, "k_parse window stride");
 
 // Record writer: a lane's records gather 16 at a time in its LDS queue row and leave as one 64-byte

@@ -25,7 +25,10 @@ static double now() { return std::chrono::duration<double>(std::chrono::steady_c
 int main(int argc, char** argv) {
     const int C = argc > 1 ? atoi(argv[1]) : 256, M = argc > 2 ? atoi(argv[2]) : 256, S = argc > 3 ? atoi(argv[3]) : 65535;
     const int R = argc > 4 ? atoi(argv[4]) : 3;
+    // auto-flush thresholds per direction (0 = one flush): decoding overlaps the next batch's gather
+    // from the mapped receive pages with the previous batch's result writes over PCIe
     const size_t flush_mib = argc > 5 ? (size_t)atol(argv[5]) : 0;
+    const size_t dec_flush_mib = argc > 6 ? (size_t)atol(argv[6]) : flush_mib;
     const size_t N = (size_t)C * M, U = N * (size_t)S;
     uint8_t* in = (uint8_t*)aligned_alloc(4096, (U + 4095) / 4096 * 4096);
     static nx_textgen_tables tg;
@@ -38,7 +41,12 @@ int main(int argc, char** argv) {
         return 1;
     }
     nx_batcher* b = nx_batcher_new();
-    if (b && flush_mib) nx_batcher_set_flush_bytes(b, flush_mib << 20);
+    // the device workspaces and pinned arenas up front, as a server would at start-up: no submit allocates
+    if (b && (nx_batcher_reserve(b, (1u << NX_WS_SNAPPY_ENC) | (1u << NX_WS_DEC_RECORDS)) != NX_OK ||
+              (dec_flush_mib && nx_batcher_reserve_arenas(b, 8, (dec_flush_mib + 64) << 20, (4 * dec_flush_mib + 64) << 20) != NX_OK))) {
+        printf("{\"error\": \"batcher reservation failed\"}\n");
+        return 1;
+    }
     std::vector<nx_snappy_frame_encoder*> enc(C);
     std::vector<nx_snappy_frame_decoder*> dec(C), dec2(C);
     for (int c = 0; c < C; ++c) {
@@ -81,7 +89,10 @@ int main(int argc, char** argv) {
             nx_batcher_release(b, tk[i]);
         }
     };
+    uint64_t arena_allocs_round0 = 0;
     for (int r = 0; r < R; ++r) {
+        if (r == 1) nx_batcher_arena_stats(b, &arena_allocs_round0, nullptr, nullptr);
+        nx_batcher_set_flush_bytes(b, flush_mib << 20);
         const double t0 = now();
         for (int m = 0; m < M; ++m)
             for (int c = 0; c < C; ++c) {
@@ -116,6 +127,7 @@ int main(int argc, char** argv) {
             nx_batcher_release(b, et[i]);
         }
         // decode: registered cumulations (no copy at submit)
+        nx_batcher_set_flush_bytes(b, dec_flush_mib << 20);
         const double t2 = now();
         for (int m = 0; m < M; ++m)
             for (int c = 0; c < C; ++c) {
@@ -154,17 +166,20 @@ int main(int argc, char** argv) {
         }
         comp_total = comp;
     }
-    uint64_t fl = 0, la = 0, ch = 0;
+    uint64_t fl = 0, la = 0, ch = 0, arena_allocs = 0, arena_bytes = 0;
     nx_batcher_stats(b, &fl, &la, &ch);
+    nx_batcher_arena_stats(b, &arena_allocs, &arena_bytes, nullptr);
     const double g = (double)U / (1 << 30);
     printf("{\"channels\": %d, \"messages_per_channel\": %d, \"message_bytes\": %d, \"uncompressed_bytes\": %zu, "
            "\"compressed_bytes\": %.0f, \"encode_gib_s\": %.3f, \"decode_gib_s\": %.3f, \"round_trip_gib_s\": %.3f, "
            "\"decode_copied_gib_s\": %.3f, \"encode_s\": %.4f, \"decode_s\": %.4f, \"decode_copied_s\": %.4f, "
            "\"phases_s\": {\"encode_submit\": %.4f, \"encode_flush_wait\": %.4f, \"decode_submit\": %.4f, "
            "\"decode_flush_wait\": %.4f, \"decode_copied_submit\": %.4f, \"decode_copied_flush_wait\": %.4f}, "
-           "\"flush_mib\": %zu, \"flushes\": %llu, \"launches\": %llu, \"verified\": %s}\n",
+           "\"flush_mib\": %zu, \"decode_flush_mib\": %zu, \"flushes\": %llu, \"launches\": %llu, "
+           "\"arena_allocs_after_round0\": %llu, \"pinned_arena_mib\": %.0f, \"verified\": %s}\n",
            C, M, S, U, comp_total, g / best_e, g / best_d, g / (best_e + best_d), g / best_dc, best_e, best_d, best_dc, ph[0], ph[1],
-           ph[2], ph[3], ph[4], ph[5], flush_mib, (unsigned long long)fl, (unsigned long long)la, ok ? "true" : "false");
+           ph[2], ph[3], ph[4], ph[5], flush_mib, dec_flush_mib, (unsigned long long)fl, (unsigned long long)la,
+           (unsigned long long)(R > 1 ? arena_allocs - arena_allocs_round0 : arena_allocs), arena_bytes / 1048576.0, ok ? "true" : "false");
     for (int c = 0; c < C; ++c) {
         nx_snappy_frame_encoder_free(enc[c]);
         nx_snappy_frame_decoder_free(dec[c]);

@@ -1,7 +1,8 @@
 """Per-frame pass / round counters of k_expand from a diagnostic build (scripts/mk_dec_stats.py
-adds them; the product library has no such symbol).
+adds them; the product library has no such symbol), or with --stamps the per-section shader-clock
+cycles of scripts/mk_dec_stamps.py's build.
 
-    python scripts/dec_stats.py [chunks]
+    python scripts/dec_stats.py [--stamps] [chunks]
 """
 import ctypes as C
 import json
@@ -16,7 +17,9 @@ def main():
     import torch
     from netty_amd import batch as B
     from netty_amd import _lib
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    args = [a for a in sys.argv[1:] if a != "--stamps"]
+    stamps = "--stamps" in sys.argv
+    n = int(args[0]) if args else 16384
     L = 65536
     dev = torch.device("cuda:0")
     src = torch.empty(n * L, dtype=torch.uint8, device=dev)
@@ -37,6 +40,17 @@ def main():
     assert lib.nx_dec_stats_read(buf) == 0
     names = ["windows", "passes", "rounds", "map_passes", "far_or_unstaged_passes", "overlap_passes", "-", "pieces"]
     ok = bool(torch.equal(dec, src)) and int((r["status"] != 0).sum()) == 0
+    if stamps:
+        names = ["map_records", "addresses_far_issue_producer_map", "overlap_addresses", "round0_incl_far_wait",
+                 "dependent_rounds", "flush_crc", "passes", "frame_total"]
+        per = {k: buf[i] / n for i, k in enumerate(names)}
+        tot = per["frame_total"]
+        frac = {k: round(v / tot, 4) for k, v in per.items() if k not in ("passes", "frame_total")}
+        frac["outside_passes"] = round(1 - sum(frac.values()), 4)
+        print(json.dumps({"chunks": n, "verified": ok, "cycles_per_frame": round(tot), "passes_per_frame": round(per["passes"], 1),
+                          "cycles_per_pass": {k: round(v / per["passes"], 1) for k, v in per.items() if k not in ("passes", "frame_total")},
+                          "fraction_of_frame": frac}))
+        return
     print(json.dumps({"chunks": n, "verified": ok, "per_frame": {k: round(buf[i] / n, 2) for i, k in enumerate(names) if k != "-"}}))
 
 

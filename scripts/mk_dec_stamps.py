@@ -1,0 +1,60 @@
+# Instrumented copy of snappy_decode.hip: per-section shader-clock stamps of k_expand's passes
+# (diagnostic build only; s_memtime, summed per wave and added to a device array per frame).
+#   python scripts/mk_dec_stamps.py netty_amd/csrc/snappy_decode.hip /tmp/stamps.hip
+#   scripts/build_dec_variant.sh stamps /tmp/stamps.hip && python scripts/dec_stats.py --stamps
+# Each stamp waits for the wave's outstanding LDS and scalar loads (s_memtime shares lgkmcnt), so
+# the sections are "issued and their LDS traffic complete"; the build runs slower than the product.
+import sys
+s = open(sys.argv[1]).read()
+
+
+def rep(a, b, n=1):
+    global s
+    assert s.count(a) == n, (a[:60], s.count(a))
+    s = s.replace(a, b)
+
+
+T = "__builtin_amdgcn_s_memtime()"
+rep("struct Window {\n", "__device__ unsigned long long g_dec_stats[8];\nstruct Window {\n")
+rep("uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr) {",
+    "uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr, unsigned long long* tm = nullptr) {")
+rep("    for (uint32_t P0 = P0s; P0 < Pend; P0 += 64u) {\n",
+    "    for (uint32_t P0 = P0s; P0 < Pend; P0 += 64u) {\n        unsigned long long t0 = %s, tq;\n" % T)
+# [0] piece -> record map, record reads, pass bounds
+rep("        const uint32_t pe = uni((uint32_t)__builtin_amdgcn_readlane((int)x1, (int)last));\n",
+    "        const uint32_t pe = uni((uint32_t)__builtin_amdgcn_readlane((int)x1, (int)last));\n"
+    "        tq = %s; tm[0] += tq - t0; t0 = tq;\n" % T)
+# [1] source addresses, far-load issue, producer map
+rep("        const bool has_ov = __ballot(valid && overlap) != 0ull;\n",
+    "        tq = %s; tm[1] += tq - t0; t0 = tq;\n        const bool has_ov = __ballot(valid && overlap) != 0ull;\n" % T)
+# [2] overlap addresses
+rep("        const uint32_t w = sp >> 2;\n",
+    "        tq = %s; tm[2] += tq - t0; t0 = tq;\n        const uint32_t w = sp >> 2;\n" % T)
+# [3] round 0 (includes the wait for far / unstaged loads), [4] dependent rounds
+rep("            if (!pending) break;\n            if (round >= 64) return false;\n",
+    "            if (round == 0) { tq = %s; tm[3] += tq - t0; t0 = tq; }\n"
+    "            if (!pending) break;\n            if (round >= 64) return false;\n" % T)
+# [5] flush (stores + CRC); [6] passes
+rep("        io.flush_to(pe);\n    }\n",
+    "        tq = %s; tm[4] += tq - t0; t0 = tq;\n        io.flush_to(pe);\n"
+    "        tq = %s; tm[5] += tq - t0; tm[6] += 1;\n    }\n" % (T, T))
+# [7] whole frame (window setup, finish and result included)
+rep("        uint32_t pdone = 0;\n        bool primed = false;\n",
+    "        uint32_t pdone = 0;\n        bool primed = false;\n"
+    "        unsigned long long tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};\n        const unsigned long long tf = %s;\n" % T)
+rep("lane, pdone, last, &nw)) {", "lane, pdone, last, &nw, tm)) {")
+rep("        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
+    "                     crc_out ? &crc_out[c] : nullptr);\n    }\n}\n",
+    "        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
+    "                     crc_out ? &crc_out[c] : nullptr);\n"
+    "        tm[7] = %s - tf;\n"
+    "        if (lane == 0) for (int q = 0; q < 8; ++q) atomicAdd(&g_dec_stats[q], tm[q]);\n    }\n}\n" % T)
+s += '''
+extern "C" int32_t nx_dec_stats_read(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nx::dec::g_dec_stats), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(nx::dec::g_dec_stats), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+'''
+open(sys.argv[2], "w").write(s)
