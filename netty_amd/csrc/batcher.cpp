@@ -89,14 +89,29 @@ struct DecRes {  // per action, written by k_dec_finish
 
 // Copy n bytes device -> mapped host with the whole wave: 16-byte stores at 16-byte-aligned
 // destinations (one PCIe write per lane), bytes at the ragged ends.
+//
+// The kernels that move bytes across PCIe (k_gather_host reads mapped host pages, the finish kernels
+// write the results into them) run on a capped grid, kPcieBlocks workgroups looping over the jobs:
+// their speed is the link's, not the CUs', and a grid of one wave per job held every CU for the
+// whole transfer, so the next batch's parse / expand / encode on another stream could not start
+// (round 4 e2e trace: k_parse 5.9 ms alone, 17-23 ms beside a full-grid k_dec_finish).
+constexpr uint32_t kPcieBlocks = 64;
+inline dim3 pcie_grid(uint32_t jobs) { return dim3(std::min((jobs + 3u) / 4u, kPcieBlocks)); }
 __device__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n, int lane) {
     typedef uint32_t v4 __attribute__((ext_vector_type(4)));
     typedef v4 __attribute__((aligned(1))) v4u;
     const uint32_t head = (uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u) < n ? (uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u) : n;
     if ((uint32_t)lane < head) dst[lane] = src[lane];
     const uint32_t nv = (n - head) >> 4;
-    for (uint32_t i = lane; i < nv; i += 64)
-        *reinterpret_cast<v4*>(dst + head + 16u * i) = *reinterpret_cast<const v4u*>(src + head + 16u * i);
+    uint32_t i = lane;
+    for (; i + 192u < nv; i += 256u) {  // 4 KiB per wave per step: four loads in flight, then four stores
+        v4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const v4u*>(src + head + 16u * (i + 64u * u));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) *reinterpret_cast<v4*>(dst + head + 16u * (i + 64u * u)) = x[u];
+    }
+    for (; i < nv; i += 64u) *reinterpret_cast<v4*>(dst + head + 16u * i) = *reinterpret_cast<const v4u*>(src + head + 16u * i);
     const uint32_t t = head + (nv << 4);
     if (t + (uint32_t)lane < n) dst[t + lane] = src[t + lane];
 }
@@ -112,13 +127,21 @@ __global__ void __launch_bounds__(256) k_gather_host(const GatherOp* __restrict_
     typedef uint32_t v4 __attribute__((ext_vector_type(4)));
     typedef v4 __attribute__((aligned(1))) v4u;
     const int lane = threadIdx.x & 63;
-    const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (k >= n) return;
-    const GatherOp g = ops[k];
-    uint8_t* d = din + g.dst;  // 16-byte aligned
-    const uint64_t nv = g.len >> 4;
-    for (uint64_t i = lane; i < nv; i += 64) *reinterpret_cast<v4*>(d + 16 * i) = *reinterpret_cast<const v4u*>(g.src + 16 * i);
-    for (uint64_t i = (nv << 4) + lane; i < g.len; i += 64) d[i] = g.src[i];
+    for (uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += gridDim.x * 4) {
+        const GatherOp g = ops[k];
+        uint8_t* d = din + g.dst;  // 16-byte aligned
+        const uint64_t nv = g.len >> 4;
+        uint64_t i = lane;
+        for (; i + 192u < nv; i += 256u) {  // four PCIe reads per lane in flight
+            v4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const v4u*>(g.src + 16 * (i + 64u * u));
+#pragma unroll
+            for (int u = 0; u < 4; ++u) *reinterpret_cast<v4*>(d + 16 * (i + 64u * u)) = x[u];
+        }
+        for (; i < nv; i += 64) *reinterpret_cast<v4*>(d + 16 * i) = *reinterpret_cast<const v4u*>(g.src + 16 * i);
+        for (uint64_t q = (nv << 4) + lane; q < g.len; q += 64) d[q] = g.src[q];
+    }
 }
 
 // one wave per encoder job: [stream identifier] then [type][len+4: u24 LE][masked crc LE][payload] per slice
@@ -129,35 +152,35 @@ __global__ void __launch_bounds__(256) k_enc_finish(const uint8_t* __restrict__ 
                                                     const EncJob* __restrict__ jobs, uint32_t njobs, uint8_t* __restrict__ out,
                                                     int64_t* __restrict__ res_len) {
     const int lane = threadIdx.x & 63;
-    const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (j >= njobs) return;
-    const EncJob J = jobs[j];
-    for (uint32_t s = J.s0; s < J.s0 + J.ns; ++s) {
-        if (sl[s].comp && est[s] != NX_OK) {
-            if (lane == 0) res_len[j] = est[s];
-            return;
+    for (uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6); j < njobs; j += gridDim.x * 4) [&] {
+        const EncJob J = jobs[j];
+        for (uint32_t s = J.s0; s < J.s0 + J.ns; ++s) {
+            if (sl[s].comp && est[s] != NX_OK) {
+                if (lane == 0) res_len[j] = est[s];
+                return;
+            }
         }
-    }
-    uint8_t* o = out + J.out_off;
-    uint64_t pos = 0;
-    if (J.stream_start) {  // ff 06 00 00 "sNaPpY" (SnappyFrameEncoder.java:52-54)
-        const uint64_t v = lane < 8 ? (0x50614e73000006ffull >> (8 * lane)) : (0x5970ull >> (8 * (lane - 8)));  // LE bytes
-        if (lane < 10) o[lane] = (uint8_t)v;
-        pos = 10;
-    }
-    for (uint32_t s = J.s0; s < J.s0 + J.ns; ++s) {
-        const EncSlice S = sl[s];
-        const uint32_t L = S.comp ? clen[s] : S.len;
-        const uint32_t cl = L + 4;  // setChunkLength (:126-132) / writeUnencodedChunk (:119-124)
-        const uint32_t c = crc[s];
-        if (lane < 8) {
-            const uint32_t b = lane == 0 ? (S.comp ? 0u : 1u) : lane < 4 ? (cl >> (8 * (lane - 1))) & 0xFF : (c >> (8 * (lane - 4))) & 0xFF;
-            o[pos + lane] = (uint8_t)b;
+        uint8_t* o = out + J.out_off;
+        uint64_t pos = 0;
+        if (J.stream_start) {  // ff 06 00 00 "sNaPpY" (SnappyFrameEncoder.java:52-54)
+            const uint64_t v = lane < 8 ? (0x50614e73000006ffull >> (8 * lane)) : (0x5970ull >> (8 * (lane - 8)));  // LE bytes
+            if (lane < 10) o[lane] = (uint8_t)v;
+            pos = 10;
         }
-        wave_copy(o + pos + 8, S.comp ? slots + S.slot_off : din + S.in_off, L, lane);
-        pos += 8 + L;
-    }
-    if (lane == 0) res_len[j] = (int64_t)pos;
+        for (uint32_t s = J.s0; s < J.s0 + J.ns; ++s) {
+            const EncSlice S = sl[s];
+            const uint32_t L = S.comp ? clen[s] : S.len;
+            const uint32_t cl = L + 4;  // setChunkLength (:126-132) / writeUnencodedChunk (:119-124)
+            const uint32_t c = crc[s];
+            if (lane < 8) {
+                const uint32_t b = lane == 0 ? (S.comp ? 0u : 1u) : lane < 4 ? (cl >> (8 * (lane - 1))) & 0xFF : (c >> (8 * (lane - 4))) & 0xFF;
+                o[pos + lane] = (uint8_t)b;
+            }
+            wave_copy(o + pos + 8, S.comp ? slots + S.slot_off : din + S.in_off, L, lane);
+            pos += 8 + L;
+        }
+        if (lane == 0) res_len[j] = (int64_t)pos;
+    }();
 }
 
 // Bytes a Snappy block of clen bytes can decode to: at most 64 per 3 input bytes (a copy-2 tag; a
@@ -179,36 +202,36 @@ __global__ void __launch_bounds__(256) k_dec_finish(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ ucrc, uint8_t* __restrict__ out,
                                                     DecRes* __restrict__ res) {
     const int lane = threadIdx.x & 63;
-    const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (j >= njobs) return;
-    const DecJob J = jobs[j];
-    uint64_t pos = J.out_off;
-    for (uint32_t a = J.a0; a < J.a0 + J.na; ++a) {
-        const DecAct A = acts[a];
-        DecRes R{pos, 0, NX_OK, 0, 0};
-        if (A.kind == 1) {
-            R.crc = ucrc[A.chunk];
-            R.len = A.len;
-            if (J.validate && R.crc != A.crc) R.status = NX_ERR_SNAPPY_CRC_MISMATCH;  // (:171-175)
-            else wave_copy(out + pos, din + A.in_off, A.len, lane);
-        } else {
-            R.status = dstat[A.chunk];
-            // the decode launch verifies CRCs when any decoder of the batch validates; a decoder
-            // built without validateChecksums ignores them (:205-216)
-            if (R.status == NX_ERR_SNAPPY_CRC_MISMATCH && !J.validate) R.status = NX_OK;
-            R.len = dlen[A.chunk];
-            R.crc = dcrc[A.chunk];
-            R.cons = dcons[A.chunk];
-            if (R.status == NX_ERR_SNAPPY_LITERAL_LEN_INVALID && R.cons >= 4u) {  // the literal's length field, for the message
-                const uint8_t* f = din + A.in_off + R.cons - 4u;
-                R.crc = f[0] | (f[1] << 8) | (f[2] << 16) | ((uint32_t)f[3] << 24);
+    for (uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6); j < njobs; j += gridDim.x * 4) [&] {
+        const DecJob J = jobs[j];
+        uint64_t pos = J.out_off;
+        for (uint32_t a = J.a0; a < J.a0 + J.na; ++a) {
+            const DecAct A = acts[a];
+            DecRes R{pos, 0, NX_OK, 0, 0};
+            if (A.kind == 1) {
+                R.crc = ucrc[A.chunk];
+                R.len = A.len;
+                if (J.validate && R.crc != A.crc) R.status = NX_ERR_SNAPPY_CRC_MISMATCH;  // (:171-175)
+                else wave_copy(out + pos, din + A.in_off, A.len, lane);
+            } else {
+                R.status = dstat[A.chunk];
+                // the decode launch verifies CRCs when any decoder of the batch validates; a decoder
+                // built without validateChecksums ignores them (:205-216)
+                if (R.status == NX_ERR_SNAPPY_CRC_MISMATCH && !J.validate) R.status = NX_OK;
+                R.len = dlen[A.chunk];
+                R.crc = dcrc[A.chunk];
+                R.cons = dcons[A.chunk];
+                if (R.status == NX_ERR_SNAPPY_LITERAL_LEN_INVALID && R.cons >= 4u) {  // the literal's length field, for the message
+                    const uint8_t* f = din + A.in_off + R.cons - 4u;
+                    R.crc = f[0] | (f[1] << 8) | (f[2] << 16) | ((uint32_t)f[3] << 24);
+                }
+                if (R.status == NX_OK) wave_copy(out + pos, slots + dslot[A.chunk], R.len, lane);
             }
-            if (R.status == NX_OK) wave_copy(out + pos, slots + dslot[A.chunk], R.len, lane);
+            if (lane == 0) res[a] = R;
+            if (R.status != NX_OK) break;
+            pos += R.len;
         }
-        if (lane == 0) res[a] = R;
-        if (R.status != NX_OK) break;
-        pos += R.len;
-    }
+    }();
 }
 
 // ---------------------------------------------------------------- FastLZ / LZF / LZ4 jobs
@@ -267,113 +290,113 @@ __global__ void __launch_bounds__(256) k_alt_finish(const uint8_t* __restrict__ 
                                                     const AltPiece* __restrict__ pcs, const AltJobD* __restrict__ jobs, uint32_t njobs,
                                                     AltArrays R, uint8_t* __restrict__ out, AltRes* __restrict__ res) {
     const int lane = threadIdx.x & 63;
-    const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (j >= njobs) return;
-    const AltJobD J = jobs[j];
-    uint64_t pos = J.out_off;
-    for (uint32_t k = J.p0; k < J.p0 + J.np; ++k) {
-        const AltPiece P = pcs[k];
-        AltRes r{pos, 0, NX_OK, 0, 0};
-        if (P.kind >= AK_DEC_FLZ && P.aux) r.cks = R.dcks[P.aux - 1];
-        uint8_t* o = out + pos;
-        switch (P.kind) {
-            case AK_FLZ_ENC: {  // FastLzFrameEncoder.java:115-168
-                const bool cks = (P.aux & 1u) != 0;
-                const int32_t st = R.flz_st[P.res];
-                if (st != NX_OK) {
-                    r.status = st;
-                    break;
-                }
-                const uint32_t clen = R.flz_clen[P.res];
-                const bool comp = P.len >= 32u && clen < P.len;  // MIN_LENGTH_TO_COMPRESSION, :150-158
-                const uint32_t hdr = 4u + (cks ? 4u : 0u) + (comp ? 4u : 2u);
-                if (lane == 0) {
-                    o[0] = 'F';
-                    o[1] = 'L';
-                    o[2] = 'Z';
-                    o[3] = (uint8_t)((comp ? 1u : 0u) | (cks ? 0x10u : 0u));
-                    uint32_t q = 4;
-                    if (cks) {
-                        const uint32_t a = R.flz_adler[P.res];
-                        o[4] = (uint8_t)(a >> 24);
-                        o[5] = (uint8_t)(a >> 16);
-                        o[6] = (uint8_t)(a >> 8);
-                        o[7] = (uint8_t)a;
-                        q = 8;
+    for (uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6); j < njobs; j += gridDim.x * 4) [&] {
+        const AltJobD J = jobs[j];
+        uint64_t pos = J.out_off;
+        for (uint32_t k = J.p0; k < J.p0 + J.np; ++k) {
+            const AltPiece P = pcs[k];
+            AltRes r{pos, 0, NX_OK, 0, 0};
+            if (P.kind >= AK_DEC_FLZ && P.aux) r.cks = R.dcks[P.aux - 1];
+            uint8_t* o = out + pos;
+            switch (P.kind) {
+                case AK_FLZ_ENC: {  // FastLzFrameEncoder.java:115-168
+                    const bool cks = (P.aux & 1u) != 0;
+                    const int32_t st = R.flz_st[P.res];
+                    if (st != NX_OK) {
+                        r.status = st;
+                        break;
                     }
-                    if (comp) {
-                        o[q] = (uint8_t)(clen >> 8);
-                        o[q + 1] = (uint8_t)clen;
-                        q += 2;
+                    const uint32_t clen = R.flz_clen[P.res];
+                    const bool comp = P.len >= 32u && clen < P.len;  // MIN_LENGTH_TO_COMPRESSION, :150-158
+                    const uint32_t hdr = 4u + (cks ? 4u : 0u) + (comp ? 4u : 2u);
+                    if (lane == 0) {
+                        o[0] = 'F';
+                        o[1] = 'L';
+                        o[2] = 'Z';
+                        o[3] = (uint8_t)((comp ? 1u : 0u) | (cks ? 0x10u : 0u));
+                        uint32_t q = 4;
+                        if (cks) {
+                            const uint32_t a = R.flz_adler[P.res];
+                            o[4] = (uint8_t)(a >> 24);
+                            o[5] = (uint8_t)(a >> 16);
+                            o[6] = (uint8_t)(a >> 8);
+                            o[7] = (uint8_t)a;
+                            q = 8;
+                        }
+                        if (comp) {
+                            o[q] = (uint8_t)(clen >> 8);
+                            o[q + 1] = (uint8_t)clen;
+                            q += 2;
+                        }
+                        o[q] = (uint8_t)(P.len >> 8);
+                        o[q + 1] = (uint8_t)P.len;
                     }
-                    o[q] = (uint8_t)(P.len >> 8);
-                    o[q + 1] = (uint8_t)P.len;
-                }
-                if (comp) wave_copy(o + hdr, aslots + P.slot, clen, lane);
-                else wave_copy(o + hdr, din + P.src, P.len, lane);
-                r.len = hdr + (comp ? clen : P.len);
-                break;
-            }
-            case AK_LZF_ENC:
-            case AK_LZ4_ENC: {
-                const int32_t st = P.kind == AK_LZF_ENC ? R.lzf_st[P.res] : R.lz4_st[P.res];
-                if (st != NX_OK) {
-                    r.status = st;
+                    if (comp) wave_copy(o + hdr, aslots + P.slot, clen, lane);
+                    else wave_copy(o + hdr, din + P.src, P.len, lane);
+                    r.len = hdr + (comp ? clen : P.len);
                     break;
                 }
-                r.len = P.kind == AK_LZF_ENC ? R.lzf_olen[P.res] : R.lz4_olen[P.res];
-                wave_copy(o, aslots + P.slot, r.len, lane);
-                break;
-            }
-            case AK_LZF_RAW:  // LZFChunk.appendNonCompressed: 'Z' 'V' 0 len(BE16) bytes
-                if (lane == 0) {
-                    o[0] = 'Z';
-                    o[1] = 'V';
-                    o[2] = 0;
-                    o[3] = (uint8_t)(P.len >> 8);
-                    o[4] = (uint8_t)P.len;
-                }
-                wave_copy(o + 5, din + P.src, P.len, lane);
-                r.len = 5u + P.len;
-                break;
-            case AK_LZ4_END:  // magic, token = BLOCK_TYPE_NON_COMPRESSED | level, then 12 zero bytes
-                if (lane < 21) o[lane] = lane < 8 ? (uint8_t)"LZ4Block"[lane] : (lane == 8 ? (uint8_t)(0x10u | P.aux) : 0);
-                r.len = 21;
-                break;
-            case AK_RAW:
-            case AK_DEC_RAW:
-                wave_copy(o, din + P.src, P.len, lane);
-                r.len = P.len;
-                break;
-            case AK_DEC_FLZ: {  // FastLzFrameDecoder.java:154-165: decompress() must return originalLength
-                const int32_t v = R.dflz_r[P.res];
-                if (v < 0 || (uint32_t)v != P.olen) {
-                    r.status = v < 0 ? v : NX_ERR_FASTLZ_LENGTH_MISMATCH;
-                    r.len = (uint32_t)v;  // the value, for the message
+                case AK_LZF_ENC:
+                case AK_LZ4_ENC: {
+                    const int32_t st = P.kind == AK_LZF_ENC ? R.lzf_st[P.res] : R.lz4_st[P.res];
+                    if (st != NX_OK) {
+                        r.status = st;
+                        break;
+                    }
+                    r.len = P.kind == AK_LZF_ENC ? R.lzf_olen[P.res] : R.lz4_olen[P.res];
+                    wave_copy(o, aslots + P.slot, r.len, lane);
                     break;
                 }
-                wave_copy(o, aslots + P.slot, P.olen, lane);
-                r.len = P.olen;
-                break;
-            }
-            case AK_DEC_LZF:
-            case AK_DEC_LZ4: {
-                const int32_t st = P.kind == AK_DEC_LZF ? R.dlzf_st[P.res] : R.dlz4_st[P.res];
-                if (st != NX_OK) {
-                    r.status = st;
+                case AK_LZF_RAW:  // LZFChunk.appendNonCompressed: 'Z' 'V' 0 len(BE16) bytes
+                    if (lane == 0) {
+                        o[0] = 'Z';
+                        o[1] = 'V';
+                        o[2] = 0;
+                        o[3] = (uint8_t)(P.len >> 8);
+                        o[4] = (uint8_t)P.len;
+                    }
+                    wave_copy(o + 5, din + P.src, P.len, lane);
+                    r.len = 5u + P.len;
+                    break;
+                case AK_LZ4_END:  // magic, token = BLOCK_TYPE_NON_COMPRESSED | level, then 12 zero bytes
+                    if (lane < 21) o[lane] = lane < 8 ? (uint8_t)"LZ4Block"[lane] : (lane == 8 ? (uint8_t)(0x10u | P.aux) : 0);
+                    r.len = 21;
+                    break;
+                case AK_RAW:
+                case AK_DEC_RAW:
+                    wave_copy(o, din + P.src, P.len, lane);
+                    r.len = P.len;
+                    break;
+                case AK_DEC_FLZ: {  // FastLzFrameDecoder.java:154-165: decompress() must return originalLength
+                    const int32_t v = R.dflz_r[P.res];
+                    if (v < 0 || (uint32_t)v != P.olen) {
+                        r.status = v < 0 ? v : NX_ERR_FASTLZ_LENGTH_MISMATCH;
+                        r.len = (uint32_t)v;  // the value, for the message
+                        break;
+                    }
+                    wave_copy(o, aslots + P.slot, P.olen, lane);
+                    r.len = P.olen;
                     break;
                 }
-                wave_copy(o, aslots + P.slot, P.olen, lane);
-                r.len = P.olen;
-                break;
+                case AK_DEC_LZF:
+                case AK_DEC_LZ4: {
+                    const int32_t st = P.kind == AK_DEC_LZF ? R.dlzf_st[P.res] : R.dlz4_st[P.res];
+                    if (st != NX_OK) {
+                        r.status = st;
+                        break;
+                    }
+                    wave_copy(o, aslots + P.slot, P.olen, lane);
+                    r.len = P.olen;
+                    break;
+                }
+                default:
+                    r.status = NX_ERR_INTERNAL;
             }
-            default:
-                r.status = NX_ERR_INTERNAL;
+            if (lane == 0) res[k] = r;
+            if (r.status != NX_OK) break;
+            pos += r.len;
         }
-        if (lane == 0) res[k] = r;
-        if (r.status != NX_OK) break;
-        pos += r.len;
-    }
+    }();
 }
 
 }  // namespace bt
@@ -947,7 +970,7 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         if (!bt->gops.ensure(sizeof(nx::bt::GatherOp) * ng) ||
             hipMemcpyAsync(bt->gops.p, ops.data(), sizeof(nx::bt::GatherOp) * ng, hipMemcpyHostToDevice, s) != hipSuccess)
             return NX_ERR_HIP;
-        hipLaunchKernelGGL(nx::bt::k_gather_host, dim3((ng + 3) / 4), dim3(256), 0, s, bt->gops.as<const nx::bt::GatherOp>(), ng, din);
+        hipLaunchKernelGGL(nx::bt::k_gather_host, nx::bt::pcie_grid(ng), dim3(256), 0, s, bt->gops.as<const nx::bt::GatherOp>(), ng, din);
         if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
         b->launches += 1;
     }
@@ -959,7 +982,7 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         r = nx_snappy_encode_batch(din, (const uint64_t*)(A + o_ein), (const uint32_t*)(A + o_elen), slots, (const uint64_t*)(A + o_eslot),
                                    (uint32_t*)(D + o_eclen), (int32_t*)(D + o_est), nes, s);
         if (r != NX_OK) return r;
-        hipLaunchKernelGGL(nx::bt::k_enc_finish, dim3((nej + 3) / 4), dim3(256), 0, s, din, slots, (const EncSlice*)(A + o_esl),
+        hipLaunchKernelGGL(nx::bt::k_enc_finish, nx::bt::pcie_grid(nej), dim3(256), 0, s, din, slots, (const EncSlice*)(A + o_esl),
                            (const uint32_t*)(D + o_eclen), (const int32_t*)(D + o_est), (const uint32_t*)(D + o_ecrc),
                            (const EncJob*)(A + o_ejob), nej, bt->out.d, (int64_t*)(bt->out.d + bt->res_enc));
         if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
@@ -980,7 +1003,7 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
             if (r != NX_OK) return r;
             b->launches += 1;
         }
-        hipLaunchKernelGGL(nx::bt::k_dec_finish, dim3((ndj + 3) / 4), dim3(256), 0, s, din, dslots, (const uint64_t*)(A + o_dslot),
+        hipLaunchKernelGGL(nx::bt::k_dec_finish, nx::bt::pcie_grid(ndj), dim3(256), 0, s, din, dslots, (const uint64_t*)(A + o_dslot),
                            (const DecAct*)(A + o_dact),
                            (const DecJob*)(A + o_djob), ndj, (const uint32_t*)(D + o_dlen), (const uint32_t*)(D + o_dcons),
                            (const int32_t*)(D + o_dst), (const uint32_t*)(D + o_dcrc), (const uint32_t*)(D + o_ducrc), bt->out.d,
@@ -1046,7 +1069,7 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
                                   (const uint32_t*)(D + o_lolen), (const int32_t*)(D + o_lst), (const uint32_t*)(D + o_zolen),
                                   (const int32_t*)(D + o_zst), (const int32_t*)(D + o_dfr), (const int32_t*)(D + o_dlst),
                                   (const int32_t*)(D + o_dzst), dcks};
-        hipLaunchKernelGGL(nx::bt::k_alt_finish, dim3((naj + 3) / 4), dim3(256), 0, s, din, aslots, (const nx::bt::AltPiece*)(A + o_apc),
+        hipLaunchKernelGGL(nx::bt::k_alt_finish, nx::bt::pcie_grid(naj), dim3(256), 0, s, din, aslots, (const nx::bt::AltPiece*)(A + o_apc),
                            (const nx::bt::AltJobD*)(A + o_ajob), naj, R, bt->out.d, (nx::bt::AltRes*)(bt->out.d + bt->res_alt));
         if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
         b->launches += 1;
@@ -1279,6 +1302,7 @@ bool advance(nx_batcher* b, uint64_t upto, bool block) {
             if (x->inflight && x->seq == b->applied) bt = x;
         if (!bt) return false;  // unreachable: every launched batch stays in flight until applied
         const hipError_t e = block ? hipEventSynchronize(bt->ev) : hipEventQuery(bt->ev);
+        if (e == hipErrorNotReady) (void)hipGetLastError();  // not an error: keep it from the next launch check
         if (e != hipSuccess) return false;
         apply(b, bt);
         bt->inflight = false;

@@ -283,8 +283,10 @@ struct Window {
 // Pieces [0, P0s) are already produced.  `last`: run to the end, the final pass partial; otherwise
 // run only full 64-piece passes and report in *nw where the next window starts (k_expand slides its
 // 64-record window there, so no pass is cut short at a window's end; prodm must be a lane prefix).
+// `rn` (k_expand): the next window's records, loaded at the window's start; every pass takes delivery
+// of them once its rounds are done (see the passes loop).
 __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t E, bool prod, uint64_t prodm, uint32_t ostart,
-                            uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr) {
+                            uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr, uint32_t* rn = nullptr) {
     WaveLds& L = io.L;
     const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);
     const uint32_t* lds32 = L.ring;  // ring at dwords [0, 1024), stage at [1024, 1280)
@@ -304,7 +306,16 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
     // marks go to scratch[pbase - P0]; a tag whose first piece lies outside the pass writes the spare
     // slot scratch[64] instead, so the store needs no divergent branch
     uint32_t* const marks = L.scratch;
-    for (uint32_t P0 = P0s; P0 < Pend; P0 += 64u) {
+    // The next window's records (*rn) are waited for after the first pass's rounds, where the wait for
+    // that pass's far loads (issued after them) has already retired them.  Waited for at the slide
+    // instead, they cost a wait for the last pass's flush stores in every window: gfx950's vmcnt
+    // retires loads and stores in issue order and the compiler, unable to count the variable number
+    // of stores in between, waits for all of them.  The do-while gives every path one such wait, so
+    // the compiler sees the value delivered at the slide on all of them.
+    uint32_t P0 = P0s;
+    if (P0 >= Pend) {
+        if (rn) asm volatile("" : "+v"(*rn));
+    } else do {
         // piece -> tag: each tag marks its first piece, then a max-scan over the lanes
         L.scratch[lane] = 0u;
         wave_sync();
@@ -448,12 +459,13 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
             ready = ((pending >> lane) & 1ull) != 0 && (need & pending) == 0ull;
             pending &= ~__ballot(ready);
         }
+        if (rn) asm volatile("" : "+v"(*rn));
         // Flush at the END of the pass, its bytes final (round 3; was at the start, flush_to(ps)): the
         // flush's stores then precede the next pass's far-copy loads by a pass of work, so the wait
         // for those loads (gfx950's vmcnt also counts older stores) rarely waits on a fresh store.
         // Same blocks, one pass earlier; 58.8 -> 57.9 ms per 262 144 frames with the gval change below.
         io.flush_to(pe);
-    }
+    } while ((P0 += 64u) < Pend);
     if (!last) {
         if (Pend == Ptot) {  // the window is done: the next starts at its successor
             nw->rec = (uint32_t)__popcll(prodm);
@@ -949,6 +961,7 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
         uint32_t pdone = 0;
         bool primed = false;
         uint32_t r = (uint32_t)lane < N ? R[lane] : 0u;
+        asm volatile("" : "+v"(r));  // delivered here: at the window loop's head r then never waits on vmcnt (see expand_tags)
         for (uint32_t b = 0; b < N;) {
             const bool valid = b + (uint32_t)lane < N;
             const bool isc = (r >> 31) != 0u;
@@ -957,7 +970,7 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
             // in order, so a wait for `r` placed after the new load also waited for the new load
             // (a memory latency per window; 57.8 -> 57.0 ms per 262 144 frames).
             asm volatile("" ::"v"(len) : "memory");
-            const uint32_t rnext = b + 64u + (uint32_t)lane < N ? R[b + 64u + lane] : 0u;  // records [b + 64, b + 128)
+            uint32_t rnext = b + 64u + (uint32_t)lane < N ? R[b + 64u + lane] : 0u;  // records [b + 64, b + 128)
             const uint32_t x = r & 0x1FFFFFFu;
             const uint32_t incl = incl_scan(len);
             const uint32_t ostart = O + incl - len;
@@ -977,7 +990,7 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
             const uint32_t xv = isc ? (0x80000000u | x) : x;
             const bool last = b + 64u >= N;
             Window nw{0u, 0u, 0u};
-            if (!expand_tags(io, s.lds_base, O, E, valid, __ballot(valid), ostart, xv, lane, pdone, last, &nw)) {
+            if (!expand_tags(io, s.lds_base, O, E, valid, __ballot(valid), ostart, xv, lane, pdone, last, &nw, &rnext)) {
                 st = kGuardTrip + 2;
                 break;
             }
@@ -1414,10 +1427,11 @@ struct DecSlots {
     uint32_t* olen;
     uint32_t frames;
 };
-static DecSlots dec_slots(nx::SharedWs& W) {
+// slots [first, first + count) of the record workspace (a part lease)
+static DecSlots dec_slots(nx::SharedWs& W, size_t first, size_t count) {
     uint32_t* p = static_cast<uint32_t*>(W.p);
     const size_t f = W.slots;
-    return {p, p + f * nx::dec::kRecCap, p + f * nx::dec::kRecCap + f, (uint32_t)f};
+    return {p + first * nx::dec::kRecCap, p + f * nx::dec::kRecCap + first, p + f * nx::dec::kRecCap + f + first, (uint32_t)count};
 }
 
 // Dynamic-LDS limit of the wave kernels, set once per process.
@@ -1469,8 +1483,9 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
         return NX_OK;
     }
     nx::WsLease lease(nx::WsKind::DecRecords, dev, st);
-    NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::DecRecords, n, cus)));
-    const DecSlots W = dec_slots(lease.ws());
+    size_t first = 0, count = 0;
+    NX_HIP_CHECK(lease.acquire_part(nx::ws_want(nx::WsKind::DecRecords, n, cus), &first, &count));
+    const DecSlots W = dec_slots(lease.ws(), first, count);
     const uint32_t sb = n < W.frames ? n : W.frames;  // a held workspace caps the sub-batch
     for (uint32_t base = 0; base < n; base += sb) {
         const uint32_t m = n - base < sb ? n - base : sb;
@@ -1527,8 +1542,9 @@ extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off
     const hipStream_t st = (hipStream_t)stream;
     const uint64_t want = (uint64_t)cus * blocks_per_cu;
     nx::WsLease lease(nx::WsKind::DecRecords, dev, st);
-    NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::DecRecords, n, cus)));
-    const DecSlots Ws = dec_slots(lease.ws());
+    size_t first = 0, count = 0;
+    NX_HIP_CHECK(lease.acquire_part(nx::ws_want(nx::WsKind::DecRecords, n, cus), &first, &count));
+    const DecSlots Ws = dec_slots(lease.ws(), first, count);
     const DecSlots* W = &Ws;
     const uint32_t sb = n < W->frames ? n : W->frames;
     for (uint32_t base = 0; base < n; base += sb) {
@@ -1564,8 +1580,9 @@ int32_t nx::dec::decode_records(RecCodec codec, const uint8_t* in, const uint64_
     unsigned blocks_per_cu = (unsigned)(160 * 1024 / lds);
     if (blocks_per_cu < 1) blocks_per_cu = 1;
     nx::WsLease lease(nx::WsKind::DecRecords, dev, st);
-    NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::DecRecords, n, cus)));
-    const DecSlots W = dec_slots(lease.ws());
+    size_t first = 0, count = 0;
+    NX_HIP_CHECK(lease.acquire_part(nx::ws_want(nx::WsKind::DecRecords, n, cus), &first, &count));
+    const DecSlots W = dec_slots(lease.ws(), first, count);
     const uint32_t sb = n < W.frames ? n : W.frames;
     for (uint32_t base = 0; base < n; base += sb) {
         const uint32_t m = n - base < sb ? n - base : sb;

@@ -11,10 +11,18 @@ thread_local bool t_no_grow = false;
 // Free W (waits for its last use first: nothing may still read or write it).
 hipError_t ws_drop(SharedWs& W) {
     hipError_t e = hipSuccess;
-    if (W.p) {
-        if (W.used) e = hipEventSynchronize(W.ev);
-        const hipError_t f = hipFree(W.p);
+    for (const WsUse& u : W.uses) {
+        const hipError_t f = hipEventSynchronize(u.ev);
         if (e == hipSuccess) e = f;
+        W.spare.push_back(u.ev);
+    }
+    W.uses.clear();
+    W.cursor = 0;
+    if (W.p) {
+        const hipError_t f = W.used ? hipEventSynchronize(W.ev) : hipSuccess;
+        if (e == hipSuccess) e = f;
+        const hipError_t g = hipFree(W.p);
+        if (e == hipSuccess) e = g;
     }
     W.p = nullptr;
     W.slots = 0;
@@ -90,7 +98,33 @@ bool ws_no_grow() { return t_no_grow; }
 WsLease::WsLease(WsKind k, int dev, hipStream_t st) : k_(k), W_(shared_ws(k, dev)), lk_(W_.mu), st_(st) {}
 
 WsLease::~WsLease() {
-    if (acquired_) (void)ws_mark(W_, st_);  // the next user waits for this batch's launches
+    if (!acquired_) return;
+    if (part_) {  // the next users of slots [a_, b_) wait for this batch's launches
+        hipEvent_t ev = nullptr;
+        if (!W_.spare.empty()) {
+            ev = W_.spare.back();
+            W_.spare.pop_back();
+        } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            ev = nullptr;
+        }
+        if (ev && hipEventRecord(ev, st_) == hipSuccess) {
+            // uses inside [a_, b_) are covered: this stream waited for them before its launches
+            size_t k = 0;
+            for (const WsUse& u : W_.uses) {
+                if (u.a >= a_ && u.b <= b_) W_.spare.push_back(u.ev);
+                else W_.uses[k++] = u;
+            }
+            W_.uses.resize(k);
+            W_.uses.push_back({a_, b_, ev});
+            return;
+        }
+        if (ev) W_.spare.push_back(ev);
+        // no event: fall back to the whole-workspace mark below (every later user waits for it)
+    } else {
+        for (const WsUse& u : W_.uses) W_.spare.push_back(u.ev);  // this stream waited for all of them
+        W_.uses.clear();
+    }
+    (void)ws_mark(W_, st_);
 }
 
 hipError_t WsLease::acquire(size_t want) {
@@ -100,6 +134,42 @@ hipError_t WsLease::acquire(size_t want) {
         W_.kept = true;
     }
     acquired_ = true;
+    for (const WsUse& u : W_.uses) {
+        const hipError_t e = hipStreamWaitEvent(st_, u.ev, 0);
+        if (e != hipSuccess) return e;
+    }
+    return W_.used ? hipStreamWaitEvent(st_, W_.ev, 0) : hipSuccess;
+}
+
+hipError_t WsLease::acquire_part(size_t want, size_t* first, size_t* count) {
+    if (!W_.p || (!t_no_grow && W_.slots < want)) {
+        const hipError_t e = ws_grow(k_, W_, std::max(want, W_.slots), st_);
+        if (e != hipSuccess) return e;
+        W_.kept = true;
+    }
+    const size_t n = std::max<size_t>(1, std::min(want, W_.slots));
+    if (W_.cursor + n > W_.slots) W_.cursor = 0;
+    a_ = W_.cursor;
+    b_ = a_ + n;
+    W_.cursor = b_ == W_.slots ? 0 : b_;
+    acquired_ = true;
+    part_ = true;
+    *first = a_;
+    *count = n;
+    if (W_.uses.size() > 32) {  // forget the completed ones
+        size_t k = 0;
+        for (const WsUse& u : W_.uses) {
+            if (hipEventQuery(u.ev) == hipSuccess) W_.spare.push_back(u.ev);
+            else W_.uses[k++] = u;
+        }
+        (void)hipGetLastError();  // hipErrorNotReady is kept as the thread's last error: a launch check would see it
+        W_.uses.resize(k);
+    }
+    for (const WsUse& u : W_.uses) {
+        if (u.b <= a_ || u.a >= b_) continue;
+        const hipError_t e = hipStreamWaitEvent(st_, u.ev, 0);
+        if (e != hipSuccess) return e;
+    }
     return W_.used ? hipStreamWaitEvent(st_, W_.ev, 0) : hipSuccess;
 }
 

@@ -3,7 +3,11 @@
 //
 // Launches that use a workspace are ordered on the device: a batch waits (hipStreamWaitEvent) for
 // the event the previous batch recorded after its launches, so the host never blocks and any number
-// of streams (the batcher's four, every handle's own) share one allocation.  A workspace grows only
+// of streams (the batcher's four, every handle's own) share one allocation.  The decoder's record
+// slots are leased by PART (WsLease::acquire_part): a batch of m frames takes the next m slots of a
+// ring over the workspace and waits only for the earlier batches whose slots it reuses, so the
+// parse / expand of batches on different streams overlap (round 4: with one lease for the whole
+// workspace, a batcher's auto-flushed batches ran their decodes strictly one after another).  A workspace grows only
 // where growth is allowed: in the standalone batch entry points (nx_*_batch called directly) and at
 // set-up (nx_snappy_encoder_reserve, nx_batcher_new and the handle constructors, which hold it).
 // Batches submitted by a batcher or a handle run inside a NoGrowScope: they use the slots the owner
@@ -11,6 +15,7 @@
 // to let go frees it unless the standalone API grew it (then nx_workspaces_trim does).
 #pragma once
 #include <mutex>
+#include <vector>
 #include "nx_common.hpp"
 
 namespace nx {
@@ -28,8 +33,15 @@ constexpr WsSpec kWsSpec[] = {{8, 14, 16}, {8, 13, 16}, {8, 13, 8}, {8, 14, 8}, 
 constexpr size_t kDecSlotBytes = 16384u * 4u + 8u;  // records of one frame + its count and length
 constexpr uint32_t kDecMaxFrames = 262144;           // frames per parse/expand launch pair
 
+struct WsUse {  // an in-flight part lease: slots [a, b), done when ev completes
+    size_t a, b;
+    hipEvent_t ev;
+};
 struct SharedWs {
     std::mutex mu;
+    std::vector<WsUse> uses;        // part leases not yet known to be complete
+    std::vector<hipEvent_t> spare;  // their recycled events
+    size_t cursor = 0;              // next part lease starts here (wraps to 0)
     void* p = nullptr;
     size_t slots = 0;    // tables (lanes or waves) or frames
     uint32_t stamp = 0;  // encoders: last stamp used
@@ -63,6 +75,9 @@ class WsLease {
     // Grow to `want` slots when growth is allowed (blocking, set-up only), allocate if there is no
     // workspace yet, then order the stream after the previous user's launches.
     hipError_t acquire(size_t want);
+    // The same for min(want, slots) slots [*first, *first + *count) of the ring: the stream waits for
+    // the last whole-workspace user and for the part leases that overlap them.
+    hipError_t acquire_part(size_t want, size_t* first, size_t* count);
     SharedWs& ws() { return W_; }
 
   private:
@@ -71,6 +86,8 @@ class WsLease {
     std::unique_lock<std::mutex> lk_;
     hipStream_t st_;
     bool acquired_ = false;
+    bool part_ = false;
+    size_t a_ = 0, b_ = 0;
 };
 
 // Owners: hold at creation (grows to `units` now), unhold at destruction (the last one frees).

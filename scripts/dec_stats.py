@@ -32,7 +32,7 @@ def main():
     elen, est = B.snappy_encode(src, off, ln, enc, eoff)
     crc = B.crc32c_masked(src, off, ln)
     lib = C.CDLL(_lib.LIB_PATH)
-    buf = (C.c_ulonglong * 8)()
+    buf = (C.c_ulonglong * 16)()
     lib.nx_dec_stats_read(buf)  # reset
     dec = torch.empty_like(src)
     r = B.snappy_decode(enc, eoff, elen, dec, off, expected_crc=crc)
@@ -42,13 +42,17 @@ def main():
     ok = bool(torch.equal(dec, src)) and int((r["status"] != 0).sum()) == 0
     if stamps:
         names = ["map_records", "addresses_far_issue_producer_map", "overlap_addresses", "round0_incl_far_wait",
-                 "dependent_rounds", "flush_crc", "passes", "frame_total"]
+                 "dependent_rounds", "flush_crc", "passes", "frame_total", "window_setup", "expand_prologue", "window_slide",
+                 "finish_crc_result", "windows"]
         per = {k: buf[i] / n for i, k in enumerate(names)}
         tot = per["frame_total"]
-        frac = {k: round(v / tot, 4) for k, v in per.items() if k not in ("passes", "frame_total")}
-        frac["outside_passes"] = round(1 - sum(frac.values()), 4)
+        pas = names[:6]
+        frac = {k: round(per[k] / tot, 4) for k in pas + ["window_setup", "expand_prologue", "window_slide", "finish_crc_result"]}
+        frac["unaccounted"] = round(1 - sum(frac.values()), 4)
         print(json.dumps({"chunks": n, "verified": ok, "cycles_per_frame": round(tot), "passes_per_frame": round(per["passes"], 1),
-                          "cycles_per_pass": {k: round(v / per["passes"], 1) for k, v in per.items() if k not in ("passes", "frame_total")},
+                          "windows_per_frame": round(per["windows"], 1),
+                          "cycles_per_pass": {k: round(per[k] / per["passes"], 1) for k in pas},
+                          "cycles_per_window": {k: round(per[k] / per["windows"], 1) for k in ("window_setup", "expand_prologue", "window_slide")},
                           "fraction_of_frame": frac}))
         return
     print(json.dumps({"chunks": n, "verified": ok, "per_frame": {k: round(buf[i] / n, 2) for i, k in enumerate(names) if k != "-"}}))

@@ -15,11 +15,16 @@ def rep(a, b, n=1):
 
 
 T = "__builtin_amdgcn_s_memtime()"
-rep("struct Window {\n", "__device__ unsigned long long g_dec_stats[8];\nstruct Window {\n")
-rep("uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr) {",
-    "uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr, unsigned long long* tm = nullptr) {")
-rep("    for (uint32_t P0 = P0s; P0 < Pend; P0 += 64u) {\n",
-    "    for (uint32_t P0 = P0s; P0 < Pend; P0 += 64u) {\n        unsigned long long t0 = %s, tq;\n" % T)
+rep("struct Window {\n", "__device__ unsigned long long g_dec_stats[16];\nstruct Window {\n")
+rep("uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr, uint32_t* rn = nullptr) {",
+    "uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr, uint32_t* rn = nullptr, unsigned long long* tm = nullptr) {")
+# [9] expand_tags prologue (record table, piece bases)
+rep("    WaveLds& L = io.L;\n    const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);\n    const uint32_t* lds32 = L.ring;",
+    "    const unsigned long long te = %s;\n    WaveLds& L = io.L;\n    const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);\n    const uint32_t* lds32 = L.ring;" % T)
+rep("    uint32_t P0 = P0s;\n    if (P0 >= Pend) {",
+    "    tm[9] += %s - te;\n    uint32_t P0 = P0s;\n    if (P0 >= Pend) {" % T)
+rep("    } else do {\n",
+    "    } else do {\n        unsigned long long t0 = %s, tq;\n" % T)
 # [0] piece -> record map, record reads, pass bounds
 rep("        const uint32_t pe = uni((uint32_t)__builtin_amdgcn_readlane((int)x1, (int)last));\n",
     "        const uint32_t pe = uni((uint32_t)__builtin_amdgcn_readlane((int)x1, (int)last));\n"
@@ -35,25 +40,34 @@ rep("            if (!pending) break;\n            if (round >= 64) return false
     "            if (round == 0) { tq = %s; tm[3] += tq - t0; t0 = tq; }\n"
     "            if (!pending) break;\n            if (round >= 64) return false;\n" % T)
 # [5] flush (stores + CRC); [6] passes
-rep("        io.flush_to(pe);\n    }\n",
+rep("        io.flush_to(pe);\n    } while",
     "        tq = %s; tm[4] += tq - t0; t0 = tq;\n        io.flush_to(pe);\n"
-    "        tq = %s; tm[5] += tq - t0; tm[6] += 1;\n    }\n" % (T, T))
+    "        tq = %s; tm[5] += tq - t0; tm[6] += 1;\n    } while" % (T, T))
 # [7] whole frame (window setup, finish and result included)
 rep("        uint32_t pdone = 0;\n        bool primed = false;\n",
     "        uint32_t pdone = 0;\n        bool primed = false;\n"
-    "        unsigned long long tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};\n        const unsigned long long tf = %s;\n" % T)
-rep("lane, pdone, last, &nw)) {", "lane, pdone, last, &nw, tm)) {")
+    "        unsigned long long tm[16] = {};\n        const unsigned long long tf = %s;\n        unsigned long long tw, tw2;\n" % T)
+# [8] window setup, [10] slide, [12] windows
+rep("        for (uint32_t b = 0; b < N;) {\n            const bool valid = b + (uint32_t)lane < N;\n",
+    "        for (uint32_t b = 0; b < N;) {\n            tw = %s; tm[12] += 1;\n            const bool valid = b + (uint32_t)lane < N;\n" % T)
+rep("            Window nw{0u, 0u, 0u};\n            if (!expand_tags(",
+    "            Window nw{0u, 0u, 0u};\n            tm[8] += %s - tw;\n            if (!expand_tags(" % T)
+rep("lane, pdone, last, &nw, &rnext)) {", "lane, pdone, last, &nw, &rnext, tm)) {")
+rep("            if (last) {\n                O = E;\n                break;\n            }\n",
+    "            tw2 = %s;\n            if (last) {\n                O = E;\n                break;\n            }\n" % T)
+rep("            O = nw.O;\n        }\n",
+    "            O = nw.O;\n            tm[10] += %s - tw2;\n        }\n        const unsigned long long tfin = %s;\n" % (T, T))
 rep("        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
     "                     crc_out ? &crc_out[c] : nullptr);\n    }\n}\n",
     "        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
     "                     crc_out ? &crc_out[c] : nullptr);\n"
-    "        tm[7] = %s - tf;\n"
-    "        if (lane == 0) for (int q = 0; q < 8; ++q) atomicAdd(&g_dec_stats[q], tm[q]);\n    }\n}\n" % T)
+    "        tm[7] = %s - tf;\n        tm[11] = tm[7] + tf - tfin;\n"
+    "        if (lane == 0) for (int q = 0; q < 16; ++q) atomicAdd(&g_dec_stats[q], tm[q]);\n    }\n}\n" % T)
 s += '''
 extern "C" int32_t nx_dec_stats_read(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nx::dec::g_dec_stats), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nx::dec::g_dec_stats), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    unsigned long long z[16] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(nx::dec::g_dec_stats), z, sizeof z) == hipSuccess ? 0 : -1;
 }
 '''

@@ -94,8 +94,8 @@ def test_handle_message_beyond_its_reservation(nx, B, oracle):
 
 def test_batcher_large_flushes_on_all_streams_one_workspace(nx, B, oracle):
     """Eight flushes of 16 500 encoder slices each (two on each of the batcher's four streams, all in
-    flight together) and two 16 500-chunk decoder jobs: the workspaces reserved at nx_batcher_new are
-    the only ones (no growth during the flushes, device memory grows by less than one workspace),
+    flight together) and two 16 500-chunk decoder jobs: the workspaces reserved by nx_batcher_reserve
+    are the only ones (no growth during the flushes, device memory grows by less than one workspace),
     every job's bytes equal the oracle's, and nx_batcher_free returns the memory."""
     _collect(B)
     enc = nx.SnappyFrameEncoder()
@@ -104,6 +104,9 @@ def test_batcher_large_flushes_on_all_streams_one_workspace(nx, B, oracle):
     e0, eo0 = B.workspace_info(B.WS_SNAPPY_ENC)
     d0, do0 = B.workspace_info(B.WS_DEC_RECORDS)
     b = nx.Batcher()
+    # a batcher holds a workspace from its first submit that needs it, or from reserve()
+    assert B.workspace_info(B.WS_SNAPPY_ENC)[1] == eo0 and B.workspace_info(B.WS_DEC_RECORDS)[1] == do0
+    b.reserve((1 << B.WS_SNAPPY_ENC) | (1 << B.WS_DEC_RECORDS))
     e1, eo1 = B.workspace_info(B.WS_SNAPPY_ENC)
     d1, do1 = B.workspace_info(B.WS_DEC_RECORDS)
     assert (eo1, do1) == (eo0 + 1, do0 + 1)
@@ -143,3 +146,44 @@ def test_batcher_large_flushes_on_all_streams_one_workspace(nx, B, oracle):
     assert (eo3, do3) == (eo0 - 1, do0 - 1)  # the batcher's and the two handles' shares returned
     free3 = _free_bytes()
     assert free3 >= free0 - 64 * MiB, (free0 - free3) / MiB
+
+
+def test_record_part_leases_overlap_streams(nx, B, oracle):
+    """The decoder's record workspace is leased by part (a ring of frame slots): batches on different
+    streams take disjoint slots and run together, a batch that wraps onto slots still in use waits
+    for their batch.  Twelve decodes over four streams, launched back to back with no host sync,
+    against a 3000-slot workspace (three 1000-frame batches fit, the fourth reuses the first's
+    slots): every frame decodes to its source bytes."""
+    _collect(B)
+    _, owners = B.workspace_info(B.WS_DEC_RECORDS)
+    if owners:
+        pytest.skip("a live handle of another test holds the workspace")
+    dev = torch.device("cuda:0")
+    L = 4096
+    src = torch.empty(3000 * L, dtype=torch.uint8, device=dev)
+    B.textgen(src, 0, 3000, L)
+    off = torch.arange(3000, dtype=torch.int64, device=dev) * L
+    ln = torch.full((3000,), L, dtype=torch.int32, device=dev)
+    cap = (B.snappy_max_compressed_length(L) + 15) // 16 * 16
+    enc = torch.empty(3000 * cap, dtype=torch.uint8, device=dev)
+    eoff = torch.arange(3000, dtype=torch.int64, device=dev) * cap
+    elen, est = B.snappy_encode(src, off, ln, enc, eoff)
+    dec = torch.zeros_like(src)
+    r = B.snappy_decode(enc, eoff, elen, dec, off)  # grows the workspace to 3000 slots
+    torch.cuda.synchronize()
+    assert int((est != 0).sum()) == 0 and int((r["status"] != 0).sum()) == 0 and torch.equal(dec, src)
+    assert B.workspace_info(B.WS_DEC_RECORDS)[0] >= 3000 * 16384 * 4
+    streams = [torch.cuda.Stream(dev) for _ in range(4)]
+    outs = []
+    for k in range(12):
+        part = slice(1000 * (k % 3), 1000 * (k % 3 + 1))
+        o = torch.zeros_like(src)
+        with torch.cuda.stream(streams[k % 4]):
+            res = B.snappy_decode(enc, eoff[part], elen[part], o, off[part])
+        outs.append((part, o, res, streams[k % 4]))
+    torch.cuda.synchronize()
+    for part, o, res, s in outs:
+        a, b = part.start * L, part.stop * L
+        assert int((res["status"] != 0).sum()) == 0
+        assert torch.equal(o[a:b], src[a:b]), part
+    B.workspaces_trim()
