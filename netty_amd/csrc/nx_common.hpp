@@ -33,6 +33,11 @@ struct CrcTables {
 // pointer as an argument: no cross-TU device symbols, so no -fgpu-rdc).
 int crc_tables_init();                 // host: build + upload (idempotent). Returns NX_OK / NX_ERR_HIP.
 const CrcTables* crc_tables_dev();     // device pointer for the current device
+// Masked CRC32C of decoded frames out[off[i] .. + len[i]) after a decode launch: crc_out[i] (if set)
+// and, where status[i] is NX_OK and expect is set, NX_ERR_SNAPPY_CRC_MISMATCH on a mismatch; frames
+// whose status is `skip` are left alone (crc32c.hip).
+int32_t crc32c_verify_launch(const uint8_t* out, const uint64_t* off, const uint32_t* len, int32_t* status, const uint32_t* expect,
+                             uint32_t* crc_out, uint32_t n, int32_t skip, hipStream_t st);
 // host helpers (also used by the host handler layer)
 uint32_t host_crc32c(const uint8_t* p, size_t n);
 uint32_t host_mask(uint32_t c);

@@ -67,15 +67,36 @@ constexpr int kTabBytes = kTabWords * 4;
 
 struct WaveLds {
     uint32_t ring[kRing / 4];    // dword 0 .. 1023
-    uint32_t stage[kStage / 4];  // dword 1024 .. 1279
     // tag records {start (absolute output position), x (bit31 = copy; low 31 bits = literal source
     // position or copy offset)}; the start of record r+1 is the end of record r (sentinel after the last)
     uint32_t tagw[2 * 64 + 2];
     uint32_t scratch[65];        // parse: tag-start marks; expand: first-piece marks (+ a spare slot), then byte -> piece map
     uint32_t pad[1];
+    uint32_t stage[kStage / 4];  // last: a kernel without the stage allocates offsetof(WaveLds, stage) per wave
 };
-static_assert(sizeof(WaveLds) % 16 == 0, "keep per-wave LDS 16-byte aligned");
+constexpr uint32_t kStageDw = offsetof(WaveLds, stage) / 4;
+static_assert(sizeof(WaveLds) % 16 == 0 && offsetof(WaveLds, stage) % 16 == 0, "keep per-wave LDS 16-byte aligned");
 static_assert(2 * (kTabBytes + kWaves * sizeof(WaveLds)) <= 160 * 1024, "two workgroups per CU");
+
+// k_expand without the compressed-input stage (NX_EXPAND_STAGE=0): literal pieces read the chunk
+// from HBM like far copies, and the 1 KiB per wave it frees raises the waves per workgroup.
+#ifndef NX_EXPAND_STAGE
+#define NX_EXPAND_STAGE 1
+#endif
+constexpr bool kExpandStaged = NX_EXPAND_STAGE != 0;
+constexpr size_t kExpandWaveLds = kExpandStaged ? sizeof(WaveLds) : offsetof(WaveLds, stage);
+// k_expand without the fused CRC32C (NX_EXPAND_CRC=0): no CRC tables in LDS (8 KiB per workgroup
+// more for waves); the verify runs as its own pass over the decoded frames (k_crc32c_verify).
+#ifndef NX_EXPAND_CRC
+#define NX_EXPAND_CRC 1
+#endif
+constexpr bool kExpandCrc = NX_EXPAND_CRC != 0;
+constexpr size_t kExpandTabBytes = kExpandCrc ? kTabBytes : 0;
+#ifndef NX_EXPAND_WAVES
+#define NX_EXPAND_WAVES (NX_EXPAND_STAGE ? 12 : (NX_EXPAND_CRC ? 14 : 16))
+#endif
+constexpr int kExpandWaves = NX_EXPAND_WAVES;
+static_assert(2 * (kExpandTabBytes + kExpandWaves * kExpandWaveLds) <= 160 * 1024, "two k_expand workgroups per CU");
 
 typedef uint32_t __attribute__((aligned(1))) u32u;
 typedef __attribute__((address_space(1))) const uint8_t gu8;
@@ -286,10 +307,11 @@ struct Window {
 // `rn` (k_expand): the next window's records, loaded at the window's start; every pass takes delivery
 // of them once its rounds are done (see the passes loop).
 __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t E, bool prod, uint64_t prodm, uint32_t ostart,
-                            uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr, uint32_t* rn = nullptr) {
+                            uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr, uint32_t* rn = nullptr,
+                            bool staged = true) {
     WaveLds& L = io.L;
     const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);
-    const uint32_t* lds32 = L.ring;  // ring at dwords [0, 1024), stage at [1024, 1280)
+    const uint32_t* lds32 = L.ring;  // ring at dwords [0, 1024), stage at [kStageDw, kStageDw + 256)
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(prodm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)prodm, 0u));
     if (prod) *reinterpret_cast<uint2*>(&L.tagw[2 * rank]) = make_uint2(ostart, xv);
     if (lane == 0) L.tagw[2 * (uint32_t)__popcll(prodm)] = E;  // sentinel: end of the last tag
@@ -355,10 +377,10 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
         const uint32_t pin = xo + (x0 - tstart);  // literal: input position
         // LDS read: dwords lbase + ((sp >> 2) [+1] & lmask); selects, not a divergent branch
         const uint32_t sp = lit ? pin + io.a : x0 - xo;
-        const bool gl = lit ? (sp - io.sbase) > (uint32_t)(kStage - 8)                        // outside the stage: HBM
+        const bool gl = lit ? (!staged || (sp - io.sbase) > (uint32_t)(kStage - 8))          // outside the stage: HBM
                             : (!overlap && pe > (uint32_t)kRing && sp < pe - (uint32_t)kRing);  // far copy
-        const uint32_t lbase = lit ? (uint32_t)(kRing / 4) : 0u;
-        const uint32_t lmask = lit ? (uint32_t)(kStage / 4 - 1) : (uint32_t)(kRing / 4 - 1);
+        const uint32_t lbase = lit && staged ? kStageDw : 0u;
+        const uint32_t lmask = lit && staged ? (uint32_t)(kStage / 4 - 1) : (uint32_t)(kRing / 4 - 1);
         const uint32_t nbytes = x1 - x0;
         const uint32_t sh = 8u * (x0 & 3u);
         const uint32_t bmask = (nbytes >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nbytes)) - 1u)) << sh;
@@ -672,7 +694,8 @@ struct WaveSetup {
     uint32_t lds_base;
     uint32_t wave;
 };
-__device__ __forceinline__ WaveSetup wave_setup(uint8_t* smem, const CrcTables* __restrict__ tabs, bool do_crc) {
+__device__ __forceinline__ WaveSetup wave_setup(uint8_t* smem, const CrcTables* __restrict__ tabs, bool do_crc,
+                                                size_t wave_lds = sizeof(WaveLds), size_t tab_bytes = kTabBytes) {
     WaveSetup s;
     s.sT = reinterpret_cast<uint32_t*>(smem);  // T8[0..3]
     s.sSH = s.sT + 4 * 256;                    // SH[5] = shift by 512 B
@@ -685,7 +708,7 @@ __device__ __forceinline__ WaveSetup wave_setup(uint8_t* smem, const CrcTables* 
     // and everything derived from it (the frame, its pointers, sizes, positions) would otherwise
     // live in VGPRs with exec-masked control flow
     s.wave = uni(threadIdx.x >> 6);
-    s.L = reinterpret_cast<WaveLds*>(smem + kTabBytes + s.wave * sizeof(WaveLds));
+    s.L = reinterpret_cast<WaveLds*>(smem + tab_bytes + s.wave * wave_lds);
     // LDS byte address of L for the inline-asm atomics: the low 32 bits of a flat pointer into the
     // LDS aperture are the LDS offset
     s.lds_base = (uint32_t)(uintptr_t)s.L;
@@ -936,17 +959,17 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
 // =====================================================================================
 // k_expand: one wave per frame executes the frame's records
 // =====================================================================================
-__global__ void __launch_bounds__(kWaves * 64, 6)
+__global__ void __launch_bounds__(kExpandWaves * 64, kExpandStaged ? 6 : 2)
     k_expand(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
              uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ rec,
              const uint32_t* __restrict__ nrec, uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
              const uint32_t* __restrict__ expect, uint32_t* __restrict__ crc_out, uint32_t n, const CrcTables* __restrict__ tabs) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const bool do_crc = (expect != nullptr) || (crc_out != nullptr);
-    const WaveSetup s = wave_setup(smem, tabs, do_crc);
+    const bool do_crc = kExpandCrc && ((expect != nullptr) || (crc_out != nullptr));
+    const WaveSetup s = wave_setup(smem, tabs, do_crc, kExpandWaveLds, kExpandTabBytes);
     const int lane = threadIdx.x & 63;
-    const uint32_t nw = gridDim.x * kWaves;
-    for (uint32_t c = blockIdx.x * kWaves + s.wave; c < n; c += nw) {
+    const uint32_t nw = gridDim.x * kExpandWaves;
+    for (uint32_t c = blockIdx.x * kExpandWaves + s.wave; c < n; c += nw) {
         int32_t st = (int32_t)uni((uint32_t)status[c]);
         if (st == kNeedFused) continue;
         const uint32_t N = uni(nrec[c]);
@@ -976,7 +999,7 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
             const uint32_t ostart = O + incl - len;
             const uint32_t E = O + uni((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
             // the stage follows the first literal of the batch (literal positions are monotone)
-            const uint64_t litm = __ballot(valid && !isc);
+            const uint64_t litm = kExpandStaged ? __ballot(valid && !isc) : 0ull;
             if (litm) {
                 const uint32_t w = uni((uint32_t)__builtin_amdgcn_readlane((int)x, __ffsll((long long)litm) - 1));
                 if (!primed) {
@@ -990,7 +1013,7 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
             const uint32_t xv = isc ? (0x80000000u | x) : x;
             const bool last = b + 64u >= N;
             Window nw{0u, 0u, 0u};
-            if (!expand_tags(io, s.lds_base, O, E, valid, __ballot(valid), ostart, xv, lane, pdone, last, &nw, &rnext)) {
+            if (!expand_tags(io, s.lds_base, O, E, valid, __ballot(valid), ostart, xv, lane, pdone, last, &nw, &rnext, kExpandStaged)) {
                 st = kGuardTrip + 2;
                 break;
             }
@@ -1009,8 +1032,8 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
         }
         if (st == kGuardTrip + 2) O = Ofin;  // unreachable on a consistent record stream
         const uint32_t crc = io.finish(O, &tabs->NS[0][0][0]);
-        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],
-                     crc_out ? &crc_out[c] : nullptr);
+        write_result(lane, crc, st, do_crc && expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],
+                     do_crc && crc_out ? &crc_out[c] : nullptr);
     }
 }
 
@@ -1434,13 +1457,16 @@ static DecSlots dec_slots(nx::SharedWs& W, size_t first, size_t count) {
     return {p + first * nx::dec::kRecCap, p + f * nx::dec::kRecCap + first, p + f * nx::dec::kRecCap + f + first, (uint32_t)count};
 }
 
-// Dynamic-LDS limit of the wave kernels, set once per process.
+constexpr size_t kExpandLds = nx::dec::kExpandTabBytes + nx::dec::kExpandWaves * nx::dec::kExpandWaveLds;
+
+// Dynamic-LDS limit of the wave kernels, set once per process (`lds`: k_decode_fused's).
 static hipError_t wave_kernel_attrs(size_t lds) {
     static std::once_flag once;
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [&] {
-        for (const void* k : {(const void*)nx::dec::k_decode_fused, (const void*)nx::dec::k_expand})
-            if (attr_err == hipSuccess) attr_err = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_err = hipFuncSetAttribute((const void*)nx::dec::k_decode_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (attr_err == hipSuccess)
+            attr_err = hipFuncSetAttribute((const void*)nx::dec::k_expand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kExpandLds);
     });
     return attr_err;
 }
@@ -1448,12 +1474,15 @@ static hipError_t wave_kernel_attrs(size_t lds) {
 // one launch of the record expander over m frames
 static hipError_t launch_expand(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
                                 const uint32_t* rec, const uint32_t* nrec, uint32_t* out_len, int32_t* status, const uint32_t* expect,
-                                uint32_t* crc_out, uint32_t m, int cus, size_t lds, unsigned blocks_per_cu, hipStream_t st) {
+                                uint32_t* crc_out, uint32_t m, int cus, hipStream_t st) {
     using namespace nx::dec;
-    const uint64_t want = (uint64_t)cus * blocks_per_cu, need = (m + kWaves - 1) / kWaves;
-    hipLaunchKernelGGL(k_expand, dim3((unsigned)(need < want ? need : want)), dim3(kWaves * 64), lds, st, in, in_off, in_len, out,
-                       out_off, rec, nrec, out_len, status, expect, crc_out, m, nx::crc_tables_dev());
-    return hipGetLastError();
+    const uint64_t want = (uint64_t)cus * (160 * 1024 / kExpandLds), need = (m + kExpandWaves - 1) / kExpandWaves;
+    hipLaunchKernelGGL(k_expand, dim3((unsigned)(need < want ? need : want)), dim3(kExpandWaves * 64), kExpandLds, st, in, in_off, in_len,
+                       out, out_off, rec, nrec, out_len, status, expect, crc_out, m, nx::crc_tables_dev());
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess || kExpandCrc) return e;
+    return nx::crc32c_verify_launch(out, out_off, out_len, status, expect, crc_out, m, kNeedFused, st) == NX_OK ? hipSuccess
+                                                                                                           : hipErrorLaunchFailure;
 }
 
 static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
@@ -1495,7 +1524,7 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
         NX_HIP_CHECK(hipGetLastError());
         NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W.rec, W.nrec, out_len + base, status + base,
                                    expected_masked_crc ? expected_masked_crc + base : nullptr, crc_out ? crc_out + base : nullptr, m,
-                                   cus, lds, blocks_per_cu, st));
+                                   cus, st));
         // frames k_parse could not slot (more than kRecCap records, or input >= 32 MiB)
         hipLaunchKernelGGL(k_decode_fused, dim3(wave_grid(m)), dim3(kWaves * 64), lds, st, in, in_off + base, in_len + base, out,
                            out_off + base, out_cap ? out_cap + base : nullptr, out_len + base, consumed ? consumed + base : nullptr,
@@ -1556,7 +1585,7 @@ extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off
         (void)need;
         (void)want;
         NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W->rec, W->nrec, W->olen, status + base, nullptr,
-                                   nullptr, m, cus, lds, blocks_per_cu, st));
+                                   nullptr, m, cus, st));
         hipLaunchKernelGGL(k_lz4_serial, dim3((m + 255) / 256), dim3(256), 0, st, in, in_off + base, in_len + base, out_len + base,
                            out, out_off + base, status + base, m);
         NX_HIP_CHECK(hipGetLastError());
@@ -1595,7 +1624,7 @@ int32_t nx::dec::decode_records(RecCodec codec, const uint8_t* in, const uint64_
                                status + base, m);
         NX_HIP_CHECK(hipGetLastError());
         NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W.rec, W.nrec, W.olen, status + base, nullptr,
-                                   nullptr, m, cus, lds, blocks_per_cu, st));
+                                   nullptr, m, cus, st));
         NX_HIP_CHECK(after(base, m, W.olen, ctx, st));
     }
     return NX_OK;

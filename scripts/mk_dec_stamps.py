@@ -16,8 +16,8 @@ def rep(a, b, n=1):
 
 T = "__builtin_amdgcn_s_memtime()"
 rep("struct Window {\n", "__device__ unsigned long long g_dec_stats[16];\nstruct Window {\n")
-rep("uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr, uint32_t* rn = nullptr) {",
-    "uint32_t xv, int lane, uint32_t P0s = 0u, bool last = true, Window* nw = nullptr, uint32_t* rn = nullptr, unsigned long long* tm = nullptr) {")
+rep("                            bool staged = true) {",
+    "                            bool staged = true, unsigned long long* tm = nullptr) {")
 # [9] expand_tags prologue (record table, piece bases)
 rep("    WaveLds& L = io.L;\n    const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);\n    const uint32_t* lds32 = L.ring;",
     "    const unsigned long long te = %s;\n    WaveLds& L = io.L;\n    const uint8_t* ring8 = reinterpret_cast<const uint8_t*>(L.ring);\n    const uint32_t* lds32 = L.ring;" % T)
@@ -52,15 +52,15 @@ rep("        for (uint32_t b = 0; b < N;) {\n            const bool valid = b + 
     "        for (uint32_t b = 0; b < N;) {\n            tw = %s; tm[12] += 1;\n            const bool valid = b + (uint32_t)lane < N;\n" % T)
 rep("            Window nw{0u, 0u, 0u};\n            if (!expand_tags(",
     "            Window nw{0u, 0u, 0u};\n            tm[8] += %s - tw;\n            if (!expand_tags(" % T)
-rep("lane, pdone, last, &nw, &rnext)) {", "lane, pdone, last, &nw, &rnext, tm)) {")
+rep("lane, pdone, last, &nw, &rnext, kExpandStaged)) {", "lane, pdone, last, &nw, &rnext, kExpandStaged, tm)) {")
 rep("            if (last) {\n                O = E;\n                break;\n            }\n",
     "            tw2 = %s;\n            if (last) {\n                O = E;\n                break;\n            }\n" % T)
 rep("            O = nw.O;\n        }\n",
     "            O = nw.O;\n            tm[10] += %s - tw2;\n        }\n        const unsigned long long tfin = %s;\n" % (T, T))
-rep("        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
-    "                     crc_out ? &crc_out[c] : nullptr);\n    }\n}\n",
-    "        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
-    "                     crc_out ? &crc_out[c] : nullptr);\n"
+rep("        write_result(lane, crc, st, do_crc && expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
+    "                     do_crc && crc_out ? &crc_out[c] : nullptr);\n    }\n}\n",
+    "        write_result(lane, crc, st, do_crc && expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
+    "                     do_crc && crc_out ? &crc_out[c] : nullptr);\n"
     "        tm[7] = %s - tf;\n        tm[11] = tm[7] + tf - tfin;\n"
     "        if (lane == 0) for (int q = 0; q < 16; ++q) atomicAdd(&g_dec_stats[q], tm[q]);\n    }\n}\n" % T)
 s += '''
