@@ -43,7 +43,7 @@ def main():
     if stamps:
         names = ["map_records", "addresses_far_issue_producer_map", "overlap_addresses", "round0_incl_far_wait",
                  "dependent_rounds", "flush_crc", "passes", "frame_total", "window_setup", "expand_prologue", "window_slide",
-                 "finish_crc_result", "windows"]
+                 "finish_crc_result", "windows", "parse_reload", "parse_tags", "parse_total"]
         per = {k: buf[i] / n for i, k in enumerate(names)}
         tot = per["frame_total"]
         pas = names[:6]
@@ -53,7 +53,8 @@ def main():
                           "windows_per_frame": round(per["windows"], 1),
                           "cycles_per_pass": {k: round(per[k] / per["passes"], 1) for k in pas},
                           "cycles_per_window": {k: round(per[k] / per["windows"], 1) for k in ("window_setup", "expand_prologue", "window_slide")},
-                          "fraction_of_frame": frac}))
+                          "fraction_of_frame": frac,
+                          "k_parse_cycles_per_wave": {k: round(buf[13 + i] / (n / 64)) for i, k in enumerate(("reload", "tag_loop", "total"))}}))
         return
     print(json.dumps({"chunks": n, "verified": ok, "per_frame": {k: round(buf[i] / n, 2) for i, k in enumerate(names) if k != "-"}}))
 

@@ -63,6 +63,21 @@ rep("        write_result(lane, crc, st, do_crc && expect != nullptr, expect ? e
     "                     do_crc && crc_out ? &crc_out[c] : nullptr);\n"
     "        tm[7] = %s - tf;\n        tm[11] = tm[7] + tf - tfin;\n"
     "        if (lane == 0) for (int q = 0; q < 16; ++q) atomicAdd(&g_dec_stats[q], tm[q]);\n    }\n}\n" % T)
+# k_parse: [13] burst-reload cycles, [14] tag-loop cycles, [15] whole-kernel cycles, per wave
+_k0 = s.index("k_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,")
+_k1 = s.index("__global__", _k0)
+_pre, s, _post = s[:_k0], s[_k0:_k1], s[_k1:]
+rep("    uint32_t ip = 0, op = 0;\n    int32_t st = NX_OK;\n    bool run = false;\n",
+    "    uint32_t ip = 0, op = 0;\n    int32_t st = NX_OK;\n    bool run = false;\n"
+    "    const unsigned long long tp0 = %s;\n    unsigned long long tpr = 0, tpi = 0, tpa, tpb;\n" % T)
+rep("        if (run && !win.has(ip)) win.load(ip);  // burst reload: one wait for the whole wave\n        while (run && win.has(ip)) {\n",
+    "        tpa = %s;\n        if (run && !win.has(ip)) win.load(ip);  // burst reload: one wait for the whole wave\n"
+    "        tpb = %s; tpr += tpb - tpa;\n        while (run && win.has(ip)) {\n" % (T, T))
+rep("            run = ip < in_len;\n        }\n    }\n    if (st == kNeedFused) {\n",
+    "            run = ip < in_len;\n        }\n        tpi += %s - tpb;\n    }\n"
+    "    if ((threadIdx.x & 63) == 0) { atomicAdd(&g_dec_stats[13], tpr); atomicAdd(&g_dec_stats[14], tpi); atomicAdd(&g_dec_stats[15], %s - tp0); }\n"
+    "    if (st == kNeedFused) {\n" % (T, T))
+s = _pre + s + _post
 s += '''
 extern "C" int32_t nx_dec_stats_read(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
