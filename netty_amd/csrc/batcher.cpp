@@ -814,6 +814,7 @@ bool rewalk(nx_batcher* b, Batch* bt, Job* j, uint64_t q) {
 
 // Launch everything `bt` collected (batcher lock held).
 int32_t launch_inner(nx_batcher* b, Batch* bt) {
+    NX_CLEAR_STALE_ERROR();
     const hipStream_t s = b->s[b->flushes % kStreams];
     const nx::NoGrowScope no_grow;  // the workspaces reserved at nx_batcher_new: a flush never allocates them
     const uint32_t nes = (uint32_t)bt->esl.size(), nej = (uint32_t)bt->ejob.size(), nda = (uint32_t)bt->dact.size();
@@ -962,7 +963,7 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
     uint8_t* aslots = reinterpret_cast<uint8_t*>(((uintptr_t)(dslots + dslot_bytes) + 15) & ~(uintptr_t)15);
     uint8_t* D = aslots + bt->aslots;
     D = reinterpret_cast<uint8_t*>(((uintptr_t)D + 15) & ~(uintptr_t)15);
-    if (hipMemcpyAsync(din, bt->staging.h, bt->st_used, hipMemcpyHostToDevice, s) != hipSuccess) return NX_ERR_HIP;
+    NX_HIP_CHECK(hipMemcpyAsync(din, bt->staging.h, bt->st_used, hipMemcpyHostToDevice, s));
     if (!bt->direct.empty()) {  // registered inputs: one gather launch reading the mapped host pages
         const uint32_t ng = (uint32_t)bt->direct.size();
         std::vector<nx::bt::GatherOp> ops(ng);
@@ -971,7 +972,7 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
             hipMemcpyAsync(bt->gops.p, ops.data(), sizeof(nx::bt::GatherOp) * ng, hipMemcpyHostToDevice, s) != hipSuccess)
             return NX_ERR_HIP;
         hipLaunchKernelGGL(nx::bt::k_gather_host, nx::bt::pcie_grid(ng), dim3(256), 0, s, bt->gops.as<const nx::bt::GatherOp>(), ng, din);
-        if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
+        NX_HIP_CHECK(hipGetLastError());
         b->launches += 1;
     }
     const uint8_t* A = din + st_arr;
@@ -985,7 +986,7 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         hipLaunchKernelGGL(nx::bt::k_enc_finish, nx::bt::pcie_grid(nej), dim3(256), 0, s, din, slots, (const EncSlice*)(A + o_esl),
                            (const uint32_t*)(D + o_eclen), (const int32_t*)(D + o_est), (const uint32_t*)(D + o_ecrc),
                            (const EncJob*)(A + o_ejob), nej, bt->out.d, (int64_t*)(bt->out.d + bt->res_enc));
-        if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
+        NX_HIP_CHECK(hipGetLastError());
         b->launches += 3;
         b->chunks += nes;
     }
@@ -1008,7 +1009,7 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
                            (const DecJob*)(A + o_djob), ndj, (const uint32_t*)(D + o_dlen), (const uint32_t*)(D + o_dcons),
                            (const int32_t*)(D + o_dst), (const uint32_t*)(D + o_dcrc), (const uint32_t*)(D + o_ducrc), bt->out.d,
                            (DecRes*)(bt->out.d + bt->res_dec));
-        if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
+        NX_HIP_CHECK(hipGetLastError());
         b->launches += 1;
         b->chunks += ndc + ndu;
     }
@@ -1071,11 +1072,11 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
                                   (const int32_t*)(D + o_dzst), dcks};
         hipLaunchKernelGGL(nx::bt::k_alt_finish, nx::bt::pcie_grid(naj), dim3(256), 0, s, din, aslots, (const nx::bt::AltPiece*)(A + o_apc),
                            (const nx::bt::AltJobD*)(A + o_ajob), naj, R, bt->out.d, (nx::bt::AltRes*)(bt->out.d + bt->res_alt));
-        if (hipGetLastError() != hipSuccess) return NX_ERR_HIP;
+        NX_HIP_CHECK(hipGetLastError());
         b->launches += 1;
         b->chunks += nfe + nle + nze + nfd + nld + nzd;
     }
-    if (hipEventRecord(bt->ev, s) != hipSuccess) return NX_ERR_HIP;
+    NX_HIP_CHECK(hipEventRecord(bt->ev, s));
     bt->inflight = true;
     bt->seq = b->flushes;
     b->flushes += 1;

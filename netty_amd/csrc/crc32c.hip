@@ -231,46 +231,13 @@ __global__ void __launch_bounds__(256) k_crc32c_masked(const uint8_t* __restrict
     }
 }
 
-// Decoded frames (k_expand built without its fused CRC): one wave per frame, as k_crc32c_masked.
-__global__ void __launch_bounds__(256) k_crc32c_verify(const uint8_t* __restrict__ out, const uint64_t* __restrict__ off,
-                                                       const uint32_t* __restrict__ len, int32_t* __restrict__ status,
-                                                       const uint32_t* __restrict__ expect, uint32_t* __restrict__ crc_out,
-                                                       uint32_t n, int32_t skip, const CrcTables* __restrict__ tabs) {
-    __shared__ uint32_t sT[8 * 256];
-    __shared__ uint32_t sSH[7 * 1024];
-    for (int i = threadIdx.x; i < 8 * 256; i += blockDim.x) sT[i] = (&tabs->T8[0][0])[i];
-    for (int i = threadIdx.x; i < 7 * 1024; i += blockDim.x) sSH[i] = (&tabs->SH[3][0][0])[i];
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const uint32_t waves_per_block = blockDim.x / 64;
-    for (uint32_t c = blockIdx.x * waves_per_block + (threadIdx.x >> 6); c < n; c += gridDim.x * waves_per_block) {
-        const int32_t st = (int32_t)__builtin_amdgcn_readfirstlane(status[c]);
-        if (st == skip) continue;
-        const uint32_t m = mask_checksum(wave_crc32c(sT, sSH, tabs->XI, out + off[c], len[c], lane));
-        if (lane == 0) {
-            if (crc_out) crc_out[c] = m;
-            if (expect && st == NX_OK && m != expect[c]) status[c] = NX_ERR_SNAPPY_CRC_MISMATCH;
-        }
-    }
-}
-
-int32_t crc32c_verify_launch(const uint8_t* out, const uint64_t* off, const uint32_t* len, int32_t* status, const uint32_t* expect,
-                             uint32_t* crc_out, uint32_t n, int32_t skip, hipStream_t st) {
-    if (n == 0 || (!expect && !crc_out)) return NX_OK;
-    if (crc_tables_init() != NX_OK) return NX_ERR_HIP;
-    unsigned grid = n / 4 + 1;
-    if (grid > 2048) grid = 2048;
-    hipLaunchKernelGGL(k_crc32c_verify, dim3(grid), dim3(256), 0, st, out, off, len, status, expect, crc_out, n, skip, crc_tables_dev());
-    NX_HIP_CHECK(hipGetLastError());
-    return NX_OK;
-}
-
 }  // namespace nx
 
 using namespace nx;
 
 extern "C" int32_t nx_crc32c_masked_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len,
                                           uint32_t* masked_out, uint32_t n, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!in || !off || !len || !masked_out) return NX_ERR_INVALID_ARG;
     if (crc_tables_init() != NX_OK) return NX_ERR_HIP;

@@ -492,6 +492,7 @@ static_assert(nx::kWsSpec[(int)nx::WsKind::FastLzEnc].entry_bytes == sizeof(uint
 extern "C" int32_t nx_fastlz_compress_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                             const uint64_t* out_off, uint32_t* out_len, const int32_t* level,
                                             const int32_t* u16_limit, int32_t* status, uint32_t n, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
     int dev = 0, cus = 256;
@@ -544,6 +545,7 @@ hipError_t flz_dec_after(uint32_t base, uint32_t m, const uint32_t* olen, void* 
 extern "C" int32_t nx_fastlz_decompress_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                               const uint32_t* in_avail, uint8_t* out, const uint64_t* out_off,
                                               const uint32_t* out_len_limit, int32_t* result, uint32_t n, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len_limit || !result) return NX_ERR_INVALID_ARG;
     FlzDecCtx ctx{in, in_off, in_len, in_avail, out, out_off, out_len_limit, result};
@@ -553,6 +555,7 @@ extern "C" int32_t nx_fastlz_decompress_batch(const uint8_t* in, const uint64_t*
 
 extern "C" int32_t nx_adler32_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t* out, uint32_t n,
                                     void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!in || !off || !len || !out) return NX_ERR_INVALID_ARG;
     unsigned grid = n / 4 + 1;

@@ -217,6 +217,7 @@ extern "C" size_t nx_lz4_max_compressed_length(size_t n) { return n + n / 255 + 
 // (Lz4FrameEncoder.java:259-275); in_len[i] <= 2^25 (MAX_BLOCK_SIZE, Lz4Constants.java / :175-178).
 extern "C" int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                        const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
     int dev = 0, cus = 256;

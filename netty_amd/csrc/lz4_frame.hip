@@ -273,6 +273,7 @@ __global__ void __launch_bounds__(256) k_frame_scan(const uint8_t* __restrict__ 
 
 extern "C" int32_t nx_xxhash32_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t seed,
                                      uint32_t* out, uint32_t n, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!in || !off || !len || !out) return NX_ERR_INVALID_ARG;
     hipLaunchKernelGGL(nx::lz4f::k_xxhash32, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, in, off, len, seed,
@@ -284,6 +285,7 @@ extern "C" int32_t nx_xxhash32_batch(const uint8_t* in, const uint64_t* off, con
 extern "C" int32_t nx_lz4_frame_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                              uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
                                              int32_t compression_level, int32_t* status, uint32_t n, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status || compression_level < 0 ||
         compression_level > 15)
@@ -306,6 +308,7 @@ extern "C" int32_t nx_lz4_frame_scan_batch(const uint8_t* in, const uint64_t* in
                                            uint32_t* comp_len, uint32_t* decomp_len, uint32_t* checksum,
                                            uint32_t* block_stream, uint32_t* block_seq, uint32_t* counts, uint32_t cap,
                                            uint32_t n, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (!counts || (n && (!in || !in_off || !in_len || !state || !consumed || !status)) ||
         (cap && (!data_off || !comp_len || !decomp_len || !checksum || !block_stream || !block_seq)))
         return NX_ERR_INVALID_ARG;

@@ -244,6 +244,7 @@ static_assert(nx::kWsSpec[(int)nx::WsKind::LzfEnc].entry_bytes == sizeof(uint64_
 
 extern "C" int32_t nx_lzf_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                        const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
     int dev = 0, cus = 256;
@@ -295,6 +296,7 @@ hipError_t lzf_dec_after(uint32_t base, uint32_t m, const uint32_t*, void* ctx, 
 extern "C" int32_t nx_lzf_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                        const uint64_t* out_off, const uint32_t* out_len, int32_t* status, uint32_t n,
                                        void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
     LzfDecCtx ctx{in, in_off, in_len, out, out_off, out_len, status};

@@ -3,15 +3,28 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include "../../include/netty_amd_status.h"
 
 #define NX_WAVE 64
 
-#define NX_HIP_CHECK(x)                                  \
-    do {                                                 \
-        hipError_t _e = (x);                             \
-        if (_e != hipSuccess) return NX_ERR_HIP;         \
+// A failing HIP call returns NX_ERR_HIP; with NX_HIP_DEBUG set in the environment the call site and
+// HIP's error string go to stderr (diagnostics only).
+#define NX_HIP_CHECK(x)                                                      \
+    do {                                                                     \
+        hipError_t _e = (x);                                                 \
+        if (_e != hipSuccess) return nx_hip_fail(_e, __FILE__, __LINE__);    \
     } while (0)
+// Launch checks read hipGetLastError(), which also returns an error any earlier HIP call of this
+// thread left behind (an expected failure the caller already handled, a NotReady from a query):
+// the kernel-launching entry points clear it first, so a check reports only their own launches.
+#define NX_CLEAR_STALE_ERROR() ((void)hipGetLastError())
+inline int32_t nx_hip_fail(hipError_t e, const char* file, int line) {
+    static const bool dbg = getenv("NX_HIP_DEBUG") != nullptr;
+    if (dbg) fprintf(stderr, "netty_amd: %s:%d: %s\n", file, line, hipGetErrorString(e));
+    return NX_ERR_HIP;
+}
 
 namespace nx {
 
@@ -33,11 +46,6 @@ struct CrcTables {
 // pointer as an argument: no cross-TU device symbols, so no -fgpu-rdc).
 int crc_tables_init();                 // host: build + upload (idempotent). Returns NX_OK / NX_ERR_HIP.
 const CrcTables* crc_tables_dev();     // device pointer for the current device
-// Masked CRC32C of decoded frames out[off[i] .. + len[i]) after a decode launch: crc_out[i] (if set)
-// and, where status[i] is NX_OK and expect is set, NX_ERR_SNAPPY_CRC_MISMATCH on a mismatch; frames
-// whose status is `skip` are left alone (crc32c.hip).
-int32_t crc32c_verify_launch(const uint8_t* out, const uint64_t* off, const uint32_t* len, int32_t* status, const uint32_t* expect,
-                             uint32_t* crc_out, uint32_t n, int32_t skip, hipStream_t st);
 // host helpers (also used by the host handler layer)
 uint32_t host_crc32c(const uint8_t* p, size_t n);
 uint32_t host_mask(uint32_t c);

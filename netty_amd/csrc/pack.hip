@@ -40,6 +40,7 @@ __global__ void __launch_bounds__(256) k_pack(const uint8_t* __restrict__ src, c
 
 extern "C" int32_t nx_pack_batch(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, uint8_t* dst,
                                  const uint64_t* dst_off, uint32_t n, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!src || !src_off || !len || !dst || !dst_off) return NX_ERR_INVALID_ARG;
     hipLaunchKernelGGL(nx::pk::k_pack, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, src, src_off, len, dst, dst_off, n);

@@ -78,25 +78,29 @@ constexpr uint32_t kStageDw = offsetof(WaveLds, stage) / 4;
 static_assert(sizeof(WaveLds) % 16 == 0 && offsetof(WaveLds, stage) % 16 == 0, "keep per-wave LDS 16-byte aligned");
 static_assert(2 * (kTabBytes + kWaves * sizeof(WaveLds)) <= 160 * 1024, "two workgroups per CU");
 
-// k_expand without the compressed-input stage (NX_EXPAND_STAGE=0): literal pieces read the chunk
-// from HBM like far copies, and the 1 KiB per wave it frees raises the waves per workgroup.
+// k_expand's shape (round 4, `scripts/ab_dec.sh`, one box, ms per 262 144 frames incl. k_parse):
+// * no compressed-input stage: literal pieces read the chunk from HBM like far copies (they are
+//   issued with them, before the producer map); the stage's block loads and their waits cost more
+//   than they saved: 12 waves/WG x 2, staged 53.8 -> unstaged 50.5;
+// * 8 waves per workgroup, three workgroups per CU (24 waves, 6 per SIMD): 49.8.  Time follows the
+//   busiest SIMD: 6+6+6+6 waves beat 8+8+4+4 (6-wave WGs x 4: 60.8), 4+4+3+3 x 2 (14-wave WGs:
+//   59.2), 8 per SIMD (16-wave WGs without CRC tables: 59.1) and 4 per SIMD (8 x 2: 55.9);
+// * the CRC32C stays fused: a separate verify pass over the output was slower (56.5 vs 50.5);
+// * one piece per lane: 128-piece passes with two pieces per lane (halving the passes and their
+//   scalar control) were bit-exact but slower, 56.7 vs 49.9: the kernel is issue-bound (PMC: each
+//   wave issues 36 % of its cycles, stalls on issue 27 %), and the longer dependency chains of
+//   128-piece passes cost more rounds than the shared control saved.
+// NX_EXPAND_STAGE=1 / NX_EXPAND_WAVES=n rebuild the alternatives for A/B runs.
 #ifndef NX_EXPAND_STAGE
-#define NX_EXPAND_STAGE 1
+#define NX_EXPAND_STAGE 0
 #endif
 constexpr bool kExpandStaged = NX_EXPAND_STAGE != 0;
 constexpr size_t kExpandWaveLds = kExpandStaged ? sizeof(WaveLds) : offsetof(WaveLds, stage);
-// k_expand without the fused CRC32C (NX_EXPAND_CRC=0): no CRC tables in LDS (8 KiB per workgroup
-// more for waves); the verify runs as its own pass over the decoded frames (k_crc32c_verify).
-#ifndef NX_EXPAND_CRC
-#define NX_EXPAND_CRC 1
-#endif
-constexpr bool kExpandCrc = NX_EXPAND_CRC != 0;
-constexpr size_t kExpandTabBytes = kExpandCrc ? kTabBytes : 0;
 #ifndef NX_EXPAND_WAVES
-#define NX_EXPAND_WAVES (NX_EXPAND_STAGE ? 12 : (NX_EXPAND_CRC ? 14 : 16))
+#define NX_EXPAND_WAVES (NX_EXPAND_STAGE ? 12 : 8)
 #endif
 constexpr int kExpandWaves = NX_EXPAND_WAVES;
-static_assert(2 * (kExpandTabBytes + kExpandWaves * kExpandWaveLds) <= 160 * 1024, "two k_expand workgroups per CU");
+static_assert(kTabBytes + kExpandWaves * kExpandWaveLds <= 160 * 1024 / (NX_EXPAND_STAGE ? 2 : 3), "k_expand workgroups per CU");
 
 typedef uint32_t __attribute__((aligned(1))) u32u;
 typedef __attribute__((address_space(1))) const uint8_t gu8;
@@ -695,7 +699,7 @@ struct WaveSetup {
     uint32_t wave;
 };
 __device__ __forceinline__ WaveSetup wave_setup(uint8_t* smem, const CrcTables* __restrict__ tabs, bool do_crc,
-                                                size_t wave_lds = sizeof(WaveLds), size_t tab_bytes = kTabBytes) {
+                                                size_t wave_lds = sizeof(WaveLds)) {
     WaveSetup s;
     s.sT = reinterpret_cast<uint32_t*>(smem);  // T8[0..3]
     s.sSH = s.sT + 4 * 256;                    // SH[5] = shift by 512 B
@@ -708,7 +712,7 @@ __device__ __forceinline__ WaveSetup wave_setup(uint8_t* smem, const CrcTables* 
     // and everything derived from it (the frame, its pointers, sizes, positions) would otherwise
     // live in VGPRs with exec-masked control flow
     s.wave = uni(threadIdx.x >> 6);
-    s.L = reinterpret_cast<WaveLds*>(smem + tab_bytes + s.wave * wave_lds);
+    s.L = reinterpret_cast<WaveLds*>(smem + kTabBytes + s.wave * wave_lds);
     // LDS byte address of L for the inline-asm atomics: the low 32 bits of a flat pointer into the
     // LDS aperture are the LDS offset
     s.lds_base = (uint32_t)(uintptr_t)s.L;
@@ -959,14 +963,14 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
 // =====================================================================================
 // k_expand: one wave per frame executes the frame's records
 // =====================================================================================
-__global__ void __launch_bounds__(kExpandWaves * 64, kExpandStaged ? 6 : 2)
+__global__ void __launch_bounds__(kExpandWaves * 64, kExpandStaged ? 6 : 3)
     k_expand(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
              uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ rec,
              const uint32_t* __restrict__ nrec, uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
              const uint32_t* __restrict__ expect, uint32_t* __restrict__ crc_out, uint32_t n, const CrcTables* __restrict__ tabs) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const bool do_crc = kExpandCrc && ((expect != nullptr) || (crc_out != nullptr));
-    const WaveSetup s = wave_setup(smem, tabs, do_crc, kExpandWaveLds, kExpandTabBytes);
+    const bool do_crc = (expect != nullptr) || (crc_out != nullptr);
+    const WaveSetup s = wave_setup(smem, tabs, do_crc, kExpandWaveLds);
     const int lane = threadIdx.x & 63;
     const uint32_t nw = gridDim.x * kExpandWaves;
     for (uint32_t c = blockIdx.x * kExpandWaves + s.wave; c < n; c += nw) {
@@ -1032,8 +1036,8 @@ __global__ void __launch_bounds__(kExpandWaves * 64, kExpandStaged ? 6 : 2)
         }
         if (st == kGuardTrip + 2) O = Ofin;  // unreachable on a consistent record stream
         const uint32_t crc = io.finish(O, &tabs->NS[0][0][0]);
-        write_result(lane, crc, st, do_crc && expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],
-                     do_crc && crc_out ? &crc_out[c] : nullptr);
+        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],
+                     crc_out ? &crc_out[c] : nullptr);
     }
 }
 
@@ -1457,7 +1461,7 @@ static DecSlots dec_slots(nx::SharedWs& W, size_t first, size_t count) {
     return {p + first * nx::dec::kRecCap, p + f * nx::dec::kRecCap + first, p + f * nx::dec::kRecCap + f + first, (uint32_t)count};
 }
 
-constexpr size_t kExpandLds = nx::dec::kExpandTabBytes + nx::dec::kExpandWaves * nx::dec::kExpandWaveLds;
+constexpr size_t kExpandLds = nx::dec::kTabBytes + nx::dec::kExpandWaves * nx::dec::kExpandWaveLds;
 
 // Dynamic-LDS limit of the wave kernels, set once per process (`lds`: k_decode_fused's).
 static hipError_t wave_kernel_attrs(size_t lds) {
@@ -1476,18 +1480,21 @@ static hipError_t launch_expand(const uint8_t* in, const uint64_t* in_off, const
                                 const uint32_t* rec, const uint32_t* nrec, uint32_t* out_len, int32_t* status, const uint32_t* expect,
                                 uint32_t* crc_out, uint32_t m, int cus, hipStream_t st) {
     using namespace nx::dec;
-    const uint64_t want = (uint64_t)cus * (160 * 1024 / kExpandLds), need = (m + kExpandWaves - 1) / kExpandWaves;
+#ifdef NX_EXPAND_BLOCKS_PER_CU
+    const uint64_t per_cu = NX_EXPAND_BLOCKS_PER_CU;
+#else
+    const uint64_t per_cu = 160 * 1024 / kExpandLds;
+#endif
+    const uint64_t want = (uint64_t)cus * per_cu, need = (m + kExpandWaves - 1) / kExpandWaves;
     hipLaunchKernelGGL(k_expand, dim3((unsigned)(need < want ? need : want)), dim3(kExpandWaves * 64), kExpandLds, st, in, in_off, in_len,
                        out, out_off, rec, nrec, out_len, status, expect, crc_out, m, nx::crc_tables_dev());
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess || kExpandCrc) return e;
-    return nx::crc32c_verify_launch(out, out_off, out_len, status, expect, crc_out, m, kNeedFused, st) == NX_OK ? hipSuccess
-                                                                                                           : hipErrorLaunchFailure;
+    return hipGetLastError();
 }
 
 static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
                             const uint32_t* out_cap, uint32_t* out_len, uint32_t* consumed, int32_t* status,
                             const uint32_t* expected_masked_crc, uint32_t* crc_out, uint32_t n, void* stream, bool fused_only) {
+    NX_CLEAR_STALE_ERROR();
     using namespace nx::dec;
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
@@ -1539,6 +1546,7 @@ extern "C" int32_t nx_snappy_decode_batch(const uint8_t* in, const uint64_t* in_
                                           const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len,
                                           uint32_t* consumed, int32_t* status, const uint32_t* expected_masked_crc,
                                           uint32_t* crc_out, uint32_t n, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     return decode_batch(in, in_off, in_len, out, out_off, out_cap, out_len, consumed, status, expected_masked_crc, crc_out, n, stream,
                         false);
 }
@@ -1557,6 +1565,7 @@ extern "C" int32_t nx_snappy_decode_batch_fused(const uint8_t* in, const uint64_
 extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                        const uint64_t* out_off, const uint32_t* out_len, int32_t* status, uint32_t n,
                                        void* stream) {
+    NX_CLEAR_STALE_ERROR();
     using namespace nx::dec;
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status) return NX_ERR_INVALID_ARG;
@@ -1598,6 +1607,7 @@ int32_t nx::dec::decode_records(RecCodec codec, const uint8_t* in, const uint64_
                                 const uint32_t* lim,
                                 uint8_t* out, const uint64_t* out_off, int32_t* status, uint32_t n, hipStream_t st, RecAfter after,
                                 void* ctx) {
+    NX_CLEAR_STALE_ERROR();
     static_assert(kNeedSerial == kNeedFused, "one marker for the serial fallback");
     if (n == 0) return NX_OK;
     if (nx::crc_tables_init() != NX_OK) return NX_ERR_HIP;

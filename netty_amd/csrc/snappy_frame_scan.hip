@@ -154,6 +154,7 @@ extern "C" int32_t nx_snappy_frame_scan_batch(const uint8_t* in, const uint64_t*
                                               uint32_t* data_len, uint32_t* masked_crc, uint32_t* chunk_stream,
                                               uint32_t* chunk_seq, uint32_t* counts, uint32_t cap, uint32_t n,
                                               void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (!counts || (n && (!in || !in_off || !in_len || !state || !consumed || !status)) ||
         (cap && (!data_off || !data_len || !masked_crc || !chunk_stream || !chunk_seq)))
         return NX_ERR_INVALID_ARG;

@@ -61,6 +61,7 @@ int g_dev = -1;
 }  // namespace
 
 extern "C" int32_t nx_textgen_device(uint8_t* out, uint64_t first_chunk, uint32_t n_chunks, uint32_t chunk_len, void* stream) {
+    NX_CLEAR_STALE_ERROR();
     if (n_chunks == 0) return NX_OK;
     if (!out) return NX_ERR_INVALID_ARG;
     int dev = 0;

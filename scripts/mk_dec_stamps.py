@@ -57,10 +57,10 @@ rep("            if (last) {\n                O = E;\n                break;\n  
     "            tw2 = %s;\n            if (last) {\n                O = E;\n                break;\n            }\n" % T)
 rep("            O = nw.O;\n        }\n",
     "            O = nw.O;\n            tm[10] += %s - tw2;\n        }\n        const unsigned long long tfin = %s;\n" % (T, T))
-rep("        write_result(lane, crc, st, do_crc && expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
-    "                     do_crc && crc_out ? &crc_out[c] : nullptr);\n    }\n}\n",
-    "        write_result(lane, crc, st, do_crc && expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
-    "                     do_crc && crc_out ? &crc_out[c] : nullptr);\n"
+rep("        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
+    "                     crc_out ? &crc_out[c] : nullptr);\n    }\n}\n",
+    "        write_result(lane, crc, st, expect != nullptr, expect ? expect[c] : 0u, O, 0u, &out_len[c], nullptr, &status[c],\n"
+    "                     crc_out ? &crc_out[c] : nullptr);\n"
     "        tm[7] = %s - tf;\n        tm[11] = tm[7] + tf - tfin;\n"
     "        if (lane == 0) for (int q = 0; q < 16; ++q) atomicAdd(&g_dec_stats[q], tm[q]);\n    }\n}\n" % T)
 # k_parse: [13] burst-reload cycles, [14] tag-loop cycles, [15] whole-kernel cycles, per wave

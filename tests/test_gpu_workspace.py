@@ -174,10 +174,12 @@ def test_record_part_leases_overlap_streams(nx, B, oracle):
     assert int((est != 0).sum()) == 0 and int((r["status"] != 0).sum()) == 0 and torch.equal(dec, src)
     assert B.workspace_info(B.WS_DEC_RECORDS)[0] >= 3000 * 16384 * 4
     streams = [torch.cuda.Stream(dev) for _ in range(4)]
+    bufs = [torch.zeros_like(src) for _ in range(12)]
+    torch.cuda.synchronize()  # the zero fills (default stream) are done before the side streams write
     outs = []
     for k in range(12):
         part = slice(1000 * (k % 3), 1000 * (k % 3 + 1))
-        o = torch.zeros_like(src)
+        o = bufs[k]
         with torch.cuda.stream(streams[k % 4]):
             res = B.snappy_decode(enc, eoff[part], elen[part], o, off[part])
         outs.append((part, o, res, streams[k % 4]))
