@@ -74,6 +74,7 @@ _SIGS = {
     "nx_batcher_reserve": (i32, [vp, C.c_uint32]),
     "nx_batcher_reserve_arenas": (i32, [vp, C.c_uint32, sz, sz]),
     "nx_batcher_arena_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(C.c_uint32)]),
+    "nx_batcher_dma_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64)]),
     "nx_fastlz_frame_encoder_submit": (i64, [vp, vp, vp, sz, sz]),
     "nx_lzf_encoder_submit": (i64, [vp, vp, vp, sz]),
     "nx_lz4_frame_encoder_submit": (i64, [vp, vp, vp, sz, i32]),

@@ -72,7 +72,10 @@ struct DecAct {  // one UNCOMPRESSED_DATA (kind 1) or COMPRESSED_DATA (kind 2) c
     uint32_t kind;
     uint32_t chunk;   // kind 2: index into the decode batch; kind 1: index into the uncompressed-CRC batch
     uint32_t crc;     // stored masked CRC32C
+    uint32_t cap;     // bytes reserved for its message: kind 2 the preamble's length (capped by the bound)
+    uint32_t pad;
 };
+constexpr uint64_t kSpilled = ~0ull;  // DecRes::off of a message longer than its chunk's preamble said
 struct DecJob {
     uint64_t out_off;
     uint32_t a0, na;
@@ -95,7 +98,11 @@ struct DecRes {  // per action, written by k_dec_finish
 // their speed is the link's, not the CUs', and a grid of one wave per job held every CU for the
 // whole transfer, so the next batch's parse / expand / encode on another stream could not start
 // (round 4 e2e trace: k_parse 5.9 ms alone, 17-23 ms beside a full-grid k_dec_finish).
-constexpr uint32_t kPcieBlocks = 64;
+#ifndef NX_PCIE_BLOCKS
+#define NX_PCIE_BLOCKS 64
+#endif
+constexpr uint32_t kPcieBlocks = NX_PCIE_BLOCKS;
+constexpr uint64_t kDmaOutMin = 64ull << 20;  // launch_inner: result arenas at least this large may go by DMA
 inline dim3 pcie_grid(uint32_t jobs) { return dim3(std::min((jobs + 3u) / 4u, kPcieBlocks)); }
 __device__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n, int lane) {
     typedef uint32_t v4 __attribute__((ext_vector_type(4)));
@@ -225,11 +232,14 @@ __global__ void __launch_bounds__(256) k_dec_finish(const uint8_t* __restrict__ 
                     const uint8_t* f = din + A.in_off + R.cons - 4u;
                     R.crc = f[0] | (f[1] << 8) | (f[2] << 16) | ((uint32_t)f[3] << 24);
                 }
-                if (R.status == NX_OK) wave_copy(out + pos, slots + dslot[A.chunk], R.len, lane);
+                // a chunk that decodes past its preamble's length (Java allows it up to 65 536 bytes,
+                // SnappyFrameDecoder.java:203) has no room here: apply() copies it from the slot
+                if (R.status == NX_OK && R.len > A.cap) R.off = kSpilled;
+                else if (R.status == NX_OK) wave_copy(out + pos, slots + dslot[A.chunk], R.len, lane);
             }
             if (lane == 0) res[a] = R;
             if (R.status != NX_OK) break;
-            pos += R.len;
+            if (R.off != kSpilled) pos += R.len;
         }
     }();
 }
@@ -529,6 +539,13 @@ struct Batch {
     AltList flz_e, lzf_e, lz4_e, flz_d, lzf_d, lz4_d;
     Pinned out;  // mapped result arena: job outputs, then the result records
     uint64_t out_used = 0, res_enc = 0, res_dec = 0, res_alt = 0;
+    // Bytes the finish kernels are known to write into `out`: decoded messages (lengths from the
+    // chunks' preambles).  Encoder outputs are not counted (they fill ~half of their bound-sized
+    // reservation).  When the known bytes fill most of a large arena the finish kernels write a device
+    // mirror instead and one DMA copy moves it (launch_inner).
+    uint64_t est_out = 0;
+    nx::h::DevBuf dout;
+    std::vector<uint64_t> dslot_off;  // decode slot of each compressed chunk (device, from slots + eslots)
     std::vector<Job*> jobs;
     nx::h::DevBuf din, slots, gops;
     hipEvent_t ev = nullptr;
@@ -555,6 +572,8 @@ struct Batch {
         du_len.clear();
         du_direct.clear();
         out_used = res_enc = res_dec = res_alt = 0;
+        est_out = 0;
+        dslot_off.clear();
         apc.clear();
         ajob.clear();
         aslots = 0;
@@ -606,7 +625,10 @@ const uint8_t* registered_device_ptr(const uint8_t* p, size_t n) {
 }
 }  // namespace
 
-constexpr int kStreams = 4;
+#ifndef NX_BATCHER_STREAMS
+#define NX_BATCHER_STREAMS 4
+#endif
+constexpr int kStreams = NX_BATCHER_STREAMS;
 struct nx_batcher {
     std::mutex mu;
     hipStream_t s[kStreams] = {};
@@ -617,6 +639,7 @@ struct nx_batcher {
     std::unordered_map<uint64_t, std::pair<Batch*, Job*>> tickets;
     uint64_t next_ticket = 1;
     uint64_t launches = 0, chunks = 0, flushes = 0;
+    uint64_t dma_flushes = 0, dma_bytes = 0;
     uint64_t applied = 0;     // batches applied, in flush order (Batch::seq < applied)
     size_t flush_bytes = 0;   // auto-flush threshold on a batch's input bytes (0 = only explicit flushes)
     ArenaCount arena;         // pinned staging / result arenas of all batches
@@ -678,10 +701,22 @@ void unwalk(Job* j) {  // the job no longer needs its walked bytes kept
 // Queue decoder job j's walked actions into batch bt.  Payloads are copied from S (host bytes the
 // walk ran over), or, with dS (the device address of S in registered memory), gathered from there at
 // flush.  On failure the batch's arrays go back to their sizes at entry (its other jobs stay valid).
+// Snappy.decode's preamble (readPreamble, Snappy.java:404-420): the declared length, for sizing
+// estimates only (65 536, the frame decoder's cap, when it is malformed or absent)
+inline uint32_t snappy_declared_len(const uint8_t* p, size_t n) {
+    uint32_t v = 0;
+    for (size_t i = 0; i < n && i < 4; ++i) {
+        v |= (uint32_t)(p[i] & 0x7f) << (7 * i);
+        if ((p[i] & 0x80) == 0) return v < 65536u ? v : 65536u;
+    }
+    return 65536u;
+}
+
 int32_t enqueue_dec(Batch* bt, Job* j, const uint8_t* S, size_t walked, const uint8_t* dS, int64_t staged = -1) {
     const size_t n_act = bt->dact.size(), n_dc = bt->dc_off.size(), n_du = bt->du_off.size(), n_dir = bt->direct.size();
-    const uint64_t dir_used = bt->direct_used;
+    const uint64_t dir_used = bt->direct_used, est0 = bt->est_out;
     auto fail = [&](int32_t code) -> int32_t {
+        bt->est_out = est0;
         bt->dact.resize(n_act);
         bt->dact_direct.resize(n_act);
         bt->dc_off.resize(n_dc);
@@ -719,7 +754,7 @@ int32_t enqueue_dec(Batch* bt, Job* j, const uint8_t* S, size_t walked, const ui
         }
         const uint8_t dir = dS ? 1 : 0;
         bt->dact_direct.push_back(dir);
-        DecAct A{off, a.dlen, 0, 0, a.crc};
+        DecAct A{off, a.dlen, 0, 0, a.crc, a.dlen, 0};
         if (a.kind == SAct::Comp) {
             A.kind = 2;
             A.chunk = (uint32_t)bt->dc_off.size();
@@ -728,7 +763,11 @@ int32_t enqueue_dec(Batch* bt, Job* j, const uint8_t* S, size_t walked, const ui
             bt->dc_crc.push_back(a.crc);
             bt->dc_direct.push_back(dir);
             if (j->dec->validate) bt->dc_validate = true;
-            out_need += nx::bt::snappy_decoded_bound(a.dlen);
+            // the message's room: the preamble's length (never more than the bound); a chunk that
+            // decodes longer (malformed, yet Java keeps it) spills (k_dec_finish, apply)
+            A.cap = std::min<uint32_t>(snappy_declared_len(S + a.data, a.dlen), nx::bt::snappy_decoded_bound(a.dlen));
+            out_need += A.cap;
+            bt->est_out += A.cap;
         } else {
             A.kind = 1;
             A.chunk = (uint32_t)bt->du_off.size();
@@ -736,6 +775,7 @@ int32_t enqueue_dec(Batch* bt, Job* j, const uint8_t* S, size_t walked, const ui
             bt->du_len.push_back(a.dlen);
             bt->du_direct.push_back(dir);
             out_need += a.dlen;
+            bt->est_out += a.dlen;
         }
         bt->dact.push_back(A);
     }
@@ -920,6 +960,7 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         dslot[i] = dslot_bytes;
         dslot_bytes += nx::bt::dec_slot_bytes(bt->dc_len[i]);
     }
+    bt->dslot_off = dslot;
     auto cp = [&](uint64_t off, const void* src, size_t n) {
         if (n) memcpy(h + off, src, n);
     };
@@ -956,6 +997,15 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         if (!bt->reserve_out(sizeof(nx::bt::AltRes) * nap + 8, &bt->res_alt)) return NX_ERR_HIP;
     }
     if (!bt->reserve_out(8ull * nej + 8, &bt->res_enc) || !bt->reserve_out(sizeof(DecRes) * nda + 8, &bt->res_dec)) return NX_ERR_HIP;
+    // Where the finish kernels write: straight into the mapped arena (their stores cross PCIe), or,
+    // when the expected bytes fill most of a large arena (decoded messages: lengths known from the
+    // preambles), into a device mirror that one DMA copy then moves.  The copy engine does not hold
+    // CUs or flood the memory system with partial writes while the next batch parses (round 4 e2e:
+    // the finish kernel's host writes ran at 53 GB/s and slowed a concurrent k_parse 2-3x).
+    const uint64_t est = bt->est_out + 8ull * nej + sizeof(DecRes) * nda + sizeof(nx::bt::AltRes) * (naj ? bt->apc.size() : 0);
+    const bool dma_out = bt->out_used >= nx::bt::kDmaOutMin && est * 5 >= bt->out_used * 4;
+    if (dma_out && !bt->dout.ensure(bt->out_used)) return NX_ERR_HIP;
+    uint8_t* const ob = dma_out ? bt->dout.as<uint8_t>() : bt->out.d;
     if (!bt->din.ensure(d0 + bt->direct_used + 16) || !bt->slots.ensure(bt->eslots + dslot_bytes + bt->aslots + Ld.at + 128)) return NX_ERR_HIP;
     uint8_t* din = bt->din.as<uint8_t>();
     uint8_t* slots = bt->slots.as<uint8_t>();
@@ -985,7 +1035,7 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         if (r != NX_OK) return r;
         hipLaunchKernelGGL(nx::bt::k_enc_finish, nx::bt::pcie_grid(nej), dim3(256), 0, s, din, slots, (const EncSlice*)(A + o_esl),
                            (const uint32_t*)(D + o_eclen), (const int32_t*)(D + o_est), (const uint32_t*)(D + o_ecrc),
-                           (const EncJob*)(A + o_ejob), nej, bt->out.d, (int64_t*)(bt->out.d + bt->res_enc));
+                           (const EncJob*)(A + o_ejob), nej, ob, (int64_t*)(ob + bt->res_enc));
         NX_HIP_CHECK(hipGetLastError());
         b->launches += 3;
         b->chunks += nes;
@@ -1007,8 +1057,8 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         hipLaunchKernelGGL(nx::bt::k_dec_finish, nx::bt::pcie_grid(ndj), dim3(256), 0, s, din, dslots, (const uint64_t*)(A + o_dslot),
                            (const DecAct*)(A + o_dact),
                            (const DecJob*)(A + o_djob), ndj, (const uint32_t*)(D + o_dlen), (const uint32_t*)(D + o_dcons),
-                           (const int32_t*)(D + o_dst), (const uint32_t*)(D + o_dcrc), (const uint32_t*)(D + o_ducrc), bt->out.d,
-                           (DecRes*)(bt->out.d + bt->res_dec));
+                           (const int32_t*)(D + o_dst), (const uint32_t*)(D + o_dcrc), (const uint32_t*)(D + o_ducrc), ob,
+                           (DecRes*)(ob + bt->res_dec));
         NX_HIP_CHECK(hipGetLastError());
         b->launches += 1;
         b->chunks += ndc + ndu;
@@ -1071,10 +1121,15 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
                                   (const int32_t*)(D + o_zst), (const int32_t*)(D + o_dfr), (const int32_t*)(D + o_dlst),
                                   (const int32_t*)(D + o_dzst), dcks};
         hipLaunchKernelGGL(nx::bt::k_alt_finish, nx::bt::pcie_grid(naj), dim3(256), 0, s, din, aslots, (const nx::bt::AltPiece*)(A + o_apc),
-                           (const nx::bt::AltJobD*)(A + o_ajob), naj, R, bt->out.d, (nx::bt::AltRes*)(bt->out.d + bt->res_alt));
+                           (const nx::bt::AltJobD*)(A + o_ajob), naj, R, ob, (nx::bt::AltRes*)(ob + bt->res_alt));
         NX_HIP_CHECK(hipGetLastError());
         b->launches += 1;
         b->chunks += nfe + nle + nze + nfd + nld + nzd;
+    }
+    if (dma_out) {
+        NX_HIP_CHECK(hipMemcpyAsync(bt->out.h, ob, bt->out_used, hipMemcpyDeviceToHost, s));
+        b->dma_flushes += 1;
+        b->dma_bytes += bt->out_used;
     }
     NX_HIP_CHECK(hipEventRecord(bt->ev, s));
     bt->inflight = true;
@@ -1225,7 +1280,19 @@ void apply(nx_batcher* b, Batch* bt) {
                 failed = true;
                 break;
             }
-            j->msgs.push_back({bt->out.h + R.off, (size_t)R.len});
+            if (R.off == nx::bt::kSpilled) {  // longer than its preamble said: from the decode slot (rare, blocking)
+                j->owned.emplace_back(R.len);
+                const uint8_t* src = bt->slots.as<uint8_t>() + bt->eslots + bt->dslot_off[A.chunk];
+                if (hipMemcpy(j->owned.back().data(), src, R.len, hipMemcpyDeviceToHost) != hipSuccess) {
+                    j->status = NX_ERR_HIP;
+                    j->err = nx_status_string(NX_ERR_HIP);
+                    failed = true;
+                    break;
+                }
+                j->msgs.push_back({j->owned.back().data(), (size_t)R.len});
+            } else {
+                j->msgs.push_back({bt->out.h + R.off, (size_t)R.len});
+            }
             if (A.kind == 2 && J.validate && R.cons < A.len) {  // validating-mode leftover (:206-212)
                 moved = rewalk(b, bt, j, j->s_base + act.data + R.cons);
                 break;
@@ -2036,6 +2103,14 @@ extern "C" int32_t nx_batcher_arena_stats(nx_batcher* b, uint64_t* allocs, uint6
     if (allocs) *allocs = b->arena.allocs;
     if (bytes) *bytes = b->arena.bytes;
     if (batches) *batches = (uint32_t)b->all.size();
+    return NX_OK;
+}
+
+extern "C" int32_t nx_batcher_dma_stats(nx_batcher* b, uint64_t* dma_flushes, uint64_t* dma_bytes) {
+    if (!b) return NX_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (dma_flushes) *dma_flushes = b->dma_flushes;
+    if (dma_bytes) *dma_bytes = b->dma_bytes;
     return NX_OK;
 }
 

@@ -443,7 +443,9 @@ class Batcher:
     def stats(self) -> dict:
         f, l_, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
         _lib.load().nx_batcher_stats(self._h, C.byref(f), C.byref(l_), C.byref(c))
-        return {"flushes": f.value, "launches": l_.value, "chunks": c.value}
+        df, db = C.c_uint64(0), C.c_uint64(0)
+        _lib.load().nx_batcher_dma_stats(self._h, C.byref(df), C.byref(db))
+        return {"flushes": f.value, "launches": l_.value, "chunks": c.value, "dma_flushes": df.value, "dma_bytes": db.value}
 
     @staticmethod
     def register(ptr: int, n: int):

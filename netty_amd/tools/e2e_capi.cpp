@@ -169,6 +169,8 @@ int main(int argc, char** argv) {
     uint64_t fl = 0, la = 0, ch = 0, arena_allocs = 0, arena_bytes = 0;
     nx_batcher_stats(b, &fl, &la, &ch);
     nx_batcher_arena_stats(b, &arena_allocs, &arena_bytes, nullptr);
+    uint64_t dma_fl = 0, dma_by = 0;
+    nx_batcher_dma_stats(b, &dma_fl, &dma_by);
     const double g = (double)U / (1 << 30);
     printf("{\"channels\": %d, \"messages_per_channel\": %d, \"message_bytes\": %d, \"uncompressed_bytes\": %zu, "
            "\"compressed_bytes\": %.0f, \"encode_gib_s\": %.3f, \"decode_gib_s\": %.3f, \"round_trip_gib_s\": %.3f, "
@@ -176,9 +178,9 @@ int main(int argc, char** argv) {
            "\"phases_s\": {\"encode_submit\": %.4f, \"encode_flush_wait\": %.4f, \"decode_submit\": %.4f, "
            "\"decode_flush_wait\": %.4f, \"decode_copied_submit\": %.4f, \"decode_copied_flush_wait\": %.4f}, "
            "\"flush_mib\": %zu, \"decode_flush_mib\": %zu, \"flushes\": %llu, \"launches\": %llu, "
-           "\"arena_allocs_after_round0\": %llu, \"pinned_arena_mib\": %.0f, \"verified\": %s}\n",
+           "\"dma_flushes\": %llu, \"arena_allocs_after_round0\": %llu, \"pinned_arena_mib\": %.0f, \"verified\": %s}\n",
            C, M, S, U, comp_total, g / best_e, g / best_d, g / (best_e + best_d), g / best_dc, best_e, best_d, best_dc, ph[0], ph[1],
-           ph[2], ph[3], ph[4], ph[5], flush_mib, dec_flush_mib, (unsigned long long)fl, (unsigned long long)la,
+           ph[2], ph[3], ph[4], ph[5], flush_mib, dec_flush_mib, (unsigned long long)fl, (unsigned long long)la, (unsigned long long)dma_fl,
            (unsigned long long)(R > 1 ? arena_allocs - arena_allocs_round0 : arena_allocs), arena_bytes / 1048576.0, ok ? "true" : "false");
     for (int c = 0; c < C; ++c) {
         nx_snappy_frame_encoder_free(enc[c]);

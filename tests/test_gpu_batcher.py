@@ -516,3 +516,59 @@ def test_batcher_reserved_arenas_do_not_grow(oracle):
         one_round()
     after = b.arena_stats()
     assert after["allocs"] == before["allocs"], (before, after)
+
+
+def test_batcher_large_decode_results_by_dma(oracle):
+    """A flush whose decoded messages fill most of a large result arena (>= 64 MiB) goes to host
+    memory by one DMA copy from a device mirror (nx_batcher_dma_stats) instead of the finish kernel's
+    mapped stores; the messages are the same, and a flush of small chunks (whose result reservation
+    is mostly headroom) keeps the mapped path."""
+    import random
+    import netty_amd as nx
+    rng = random.Random(11)
+    b = nx.Batcher()
+    chans = []
+    for i in range(8):  # 8 channels x ~9.4 MiB of 64 KiB-chunk streams: ~75 MiB of messages
+        data = b"".join(oracle.textgen_chunk(rng.randrange(1 << 20), 65536) for _ in range(150))
+        chans.append((nx.SnappyFrameDecoder(i % 2 == 0), data, oracle.snappy_frame_encode(data)[0]))
+    tickets = [(b.submit_decode(d, s), data) for d, data, s in chans]
+    b.flush()
+    for t, data in tickets:
+        b.wait(t)
+        assert b"".join(b.result(t)) == data
+    st = b.stats()
+    assert st["dma_flushes"] == 1 and st["dma_bytes"] >= 64 << 20, st
+    # small chunks: bound-sized reservations, few bytes written -> mapped stores
+    small = [(nx.SnappyFrameDecoder(True), oracle.textgen_chunk(i, 200)) for i in range(300)]
+    ts = [(b.submit_decode(d, oracle.snappy_frame_encode(x)[0]), x) for d, x in small]
+    b.flush()
+    for t, x in ts:
+        b.wait(t)
+        assert b"".join(b.result(t)) == x
+    assert b.stats()["dma_flushes"] == 1
+
+
+def test_batcher_chunk_longer_than_its_preamble(oracle):
+    """A compressed chunk whose preamble declares fewer bytes than its tags produce: the reference
+    decodes it anyway (the output buffer grows to 65 536, SnappyFrameDecoder.java:203, Snappy.java:
+    328 only ensures the declared size).  The batcher reserves the declared length for the message,
+    so this one spills and is copied from its decode slot at apply; the messages equal the
+    synchronous decoder's and the oracle's."""
+    import netty_amd as nx
+    from oracle import frame_decoders as F
+    x = oracle.textgen_chunk(77, 3000)
+    block = oracle.snappy_encode(x)
+    assert block[:2] == bytes([0xB8, 0x17])  # varint(3000)
+    lying = bytes([10]) + block[2:]          # declares 10 bytes, decodes to 3000
+    good = oracle.textgen_chunk(78, 5000)
+    stream = STREAM_ID + _chunk(0, lying, oracle.snappy_checksum(x)) + oracle.snappy_frame_encode(good, started=True)[0]
+    for validate in (True, False):
+        want = F.run(F.SnappyFrameDecoder(validate), [stream])
+        assert want == ([x, good], None)
+        b = nx.Batcher()
+        d = nx.SnappyFrameDecoder(validate)
+        t = b.submit_decode(d, stream)
+        b.flush()
+        b.wait(t)
+        assert b.result(t) == [x, good]
+        assert nx.SnappyFrameDecoder(validate).channel_read(stream) == [x, good]
