@@ -586,20 +586,12 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
 
 # ---------------------------------------------------------------------------------------- extra legs
 def device_info(torch, dev):
-    """What the box is: device properties and the power cap (the encoder's speed differs by ~15 %
-    between boxes of this pool; recorded so runs can be compared)."""
-    import subprocess
+    """What the box is: device properties (the encoder's speed differs by up to ~15 % between boxes of
+    this pool; recorded so runs can be compared).  No rocm-smi: it is a Python script, and a child
+    process of a GPU-initialised program may not exec an interpreter on this pool."""
     p = torch.cuda.get_device_properties(dev)
     info = {"name": p.name, "arch": p.gcnArchName, "cus": p.multi_processor_count, "hbm_gib": round(p.total_memory / 2**30, 1),
             "pci_bus_id": getattr(p, "pci_bus_id", None)}
-    try:
-        r = subprocess.run(["rocm-smi", "--showmaxpower", "--showmemorypartition", "--showcomputepartition"], capture_output=True,
-                           text=True, timeout=30)
-        keep = [ln.split(":", 1)[1].strip() if ":" in ln else ln for ln in r.stdout.splitlines()
-                if "GPU[" in ln and ("Power" in ln or "Partition" in ln)]
-        info["rocm_smi"] = keep
-    except (OSError, subprocess.SubprocessError):
-        info["rocm_smi"] = None
     return info
 
 
