@@ -15,6 +15,8 @@ mkdir -p "$out"
 if [ -f "$src" ]; then cp "$src" "$out/$FILE"; else git show "$src:netty_amd/csrc/$FILE" > "$out/$FILE"; fi
 cp netty_amd/csrc/*.hpp "$out/"
 make -s -C netty_amd >/dev/null
+# (snappy_decode.hip: the Makefile's phi-folding flags come first; flags given here follow them)
+[ "$FILE" = snappy_decode.hip ] && set -- -mllvm -phi-node-folding-threshold=16 -mllvm -two-entry-phi-node-folding-threshold=32 "$@"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -munsafe-fp-atomics "$@" \
     -I netty_amd/csrc -x hip -c "$out/$FILE" -o "$out/$stem.o"
 objs=$(ls netty_amd/build/*.o | grep -v "/$stem.o\$")
