@@ -76,3 +76,39 @@ extern "C" int32_t nx_memcpy_d2h(void* dst, const void* src, size_t bytes, void*
 extern "C" int32_t nx_stream_sync(void* stream) {
     return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? NX_OK : NX_ERR_HIP;
 }
+
+// Diagnostics only: with NX_SEGV_TRACE set when the library loads, a segmentation fault prints the
+// native call stack (addresses resolve with addr2line against this library) before the previous
+// handler (Python's faulthandler under pytest) runs.
+#include <execinfo.h>
+#include <signal.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+namespace {
+struct sigaction g_prev_segv;
+void nx_segv_trace(int sig, siginfo_t* si, void* ctx) {
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    const char hdr[] = "netty_amd: SIGSEGV, native stack:\n";
+    (void)!write(2, hdr, sizeof hdr - 1);
+    backtrace_symbols_fd(frames, n, 2);
+    sigaction(SIGSEGV, &g_prev_segv, nullptr);
+    if (g_prev_segv.sa_flags & SA_SIGINFO) {
+        if (g_prev_segv.sa_sigaction) g_prev_segv.sa_sigaction(sig, si, ctx);
+    } else if (g_prev_segv.sa_handler != SIG_DFL && g_prev_segv.sa_handler != SIG_IGN) {
+        g_prev_segv.sa_handler(sig);
+    }
+    raise(sig);
+}
+struct SegvTraceInit {
+    SegvTraceInit() {
+        if (!getenv("NX_SEGV_TRACE")) return;
+        struct sigaction sa;
+        memset(&sa, 0, sizeof sa);
+        sa.sa_sigaction = nx_segv_trace;
+        sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+        sigaction(SIGSEGV, &sa, &g_prev_segv);
+    }
+} g_segv_trace_init;
+}  // namespace
