@@ -103,6 +103,8 @@ struct DecRes {  // per action, written by k_dec_finish
 #endif
 constexpr uint32_t kPcieBlocks = NX_PCIE_BLOCKS;
 constexpr uint64_t kDmaOutMin = 64ull << 20;  // launch_inner: result arenas at least this large may go by DMA
+constexpr uint64_t kGatherStageMax = 8ull << 20;  // launch_inner: staging arenas up to this size move by k_gather_host
+constexpr uint64_t kGatherPiece = 64ull << 10;    // ... in ops of this many bytes
 inline dim3 pcie_grid(uint32_t jobs) { return dim3(std::min((jobs + 3u) / 4u, kPcieBlocks)); }
 __device__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n, int lane) {
     typedef uint32_t v4 __attribute__((ext_vector_type(4)));
@@ -547,7 +549,8 @@ struct Batch {
     nx::h::DevBuf dout;
     std::vector<uint64_t> dslot_off;  // decode slot of each compressed chunk (device, from slots + eslots)
     std::vector<Job*> jobs;
-    nx::h::DevBuf din, slots, gops;
+    nx::h::DevBuf din, slots;
+    Pinned gops;  // k_gather_host's op list, read by the kernel from pinned memory
     hipEvent_t ev = nullptr;
     uint64_t seq = 0;  // flush order
     bool inflight = false, done = false;
@@ -663,7 +666,7 @@ Batch* reuse_or_new_batch(nx_batcher* b) {
         delete x;
         return nullptr;
     }
-    x->staging.cnt = x->out.cnt = &b->arena;
+    x->staging.cnt = x->out.cnt = x->gops.cnt = &b->arena;
     b->all.push_back(x);
     return x;
 }
@@ -1013,15 +1016,29 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
     uint8_t* aslots = reinterpret_cast<uint8_t*>(((uintptr_t)(dslots + dslot_bytes) + 15) & ~(uintptr_t)15);
     uint8_t* D = aslots + bt->aslots;
     D = reinterpret_cast<uint8_t*>(((uintptr_t)D + 15) & ~(uintptr_t)15);
-    NX_HIP_CHECK(hipMemcpyAsync(din, bt->staging.h, bt->st_used, hipMemcpyHostToDevice, s));
-    if (!bt->direct.empty()) {  // registered inputs: one gather launch reading the mapped host pages
-        const uint32_t ng = (uint32_t)bt->direct.size();
-        std::vector<nx::bt::GatherOp> ops(ng);
-        for (uint32_t k = 0; k < ng; ++k) ops[k] = {bt->direct[k].dsrc, d0 + bt->direct[k].din_off, bt->direct[k].len};
-        if (!bt->gops.ensure(sizeof(nx::bt::GatherOp) * ng) ||
-            hipMemcpyAsync(bt->gops.p, ops.data(), sizeof(nx::bt::GatherOp) * ng, hipMemcpyHostToDevice, s) != hipSuccess)
-            return NX_ERR_HIP;
-        hipLaunchKernelGGL(nx::bt::k_gather_host, nx::bt::pcie_grid(ng), dim3(256), 0, s, bt->gops.as<const nx::bt::GatherOp>(), ng, din);
+    // Host -> device.  Registered inputs (and a small staging arena) move in one gather launch that
+    // reads the mapped pages, its op list itself read from pinned memory: no copy-engine work.  The
+    // copy engines run the batches' result copies in order, and a descriptor copy queued behind the
+    // previous batch's 500 MB result copy held this batch's gather (and, for an op list in pageable
+    // memory, the submitting thread) until that copy ended (round 4 e2e trace).  A large staging
+    // arena (payloads copied at submit) still goes by one DMA copy.
+    const bool dma_in = bt->direct.empty() && bt->st_used > nx::bt::kGatherStageMax;
+    if (dma_in) {
+        NX_HIP_CHECK(hipMemcpyAsync(din, bt->staging.h, bt->st_used, hipMemcpyHostToDevice, s));
+    } else if (bt->st_used || !bt->direct.empty()) {
+        const uint64_t piece = nx::bt::kGatherPiece;
+        const uint32_t nst = (uint32_t)((bt->st_used + piece - 1) / piece);
+        const uint32_t ng = nst + (uint32_t)bt->direct.size();
+        if (!bt->gops.ensure(sizeof(nx::bt::GatherOp) * ng, 0)) return NX_ERR_HIP;
+        nx::bt::GatherOp* ops = reinterpret_cast<nx::bt::GatherOp*>(bt->gops.h);
+        for (uint32_t k = 0; k < nst; ++k) {
+            const uint64_t o = (uint64_t)k * piece;
+            ops[k] = {bt->staging.d + o, o, std::min<uint64_t>(piece, bt->st_used - o)};
+        }
+        for (uint32_t k = 0; k < (uint32_t)bt->direct.size(); ++k)
+            ops[nst + k] = {bt->direct[k].dsrc, d0 + bt->direct[k].din_off, bt->direct[k].len};
+        hipLaunchKernelGGL(nx::bt::k_gather_host, nx::bt::pcie_grid(ng), dim3(256), 0, s,
+                           reinterpret_cast<const nx::bt::GatherOp*>(bt->gops.d), ng, din);
         NX_HIP_CHECK(hipGetLastError());
         b->launches += 1;
     }
@@ -2089,11 +2106,13 @@ extern "C" int32_t nx_batcher_reserve_arenas(nx_batcher* b, uint32_t nbatches, s
             delete x;
             return NX_ERR_HIP;
         }
-        x->staging.cnt = x->out.cnt = &b->arena;
+        x->staging.cnt = x->out.cnt = x->gops.cnt = &b->arena;
         b->all.push_back(x);
     }
     for (Batch* x : b->all)  // an in-flight batch's arenas are in use: sized when it is reused
-        if (!x->inflight && (!x->staging.ensure(staging_bytes, x->st_used) || !x->out.ensure(out_bytes, x->out_used))) return NX_ERR_HIP;
+        if (!x->inflight && (!x->staging.ensure(staging_bytes, x->st_used) || !x->out.ensure(out_bytes, x->out_used) ||
+                             !x->gops.ensure(1u << 20, 0)))
+            return NX_ERR_HIP;
     return NX_OK;
 }
 
