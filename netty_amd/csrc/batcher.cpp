@@ -11,11 +11,13 @@
 //           advances in call order; the chunk payloads are copied into a pinned staging arena
 //           (MessageToByteEncoder releases `in` when encode() returns, :109), or, for an encoder input
 //           the caller registered with nx_host_register and keeps alive, DMA'd straight from it.
-//   flush   one H2D copy of the staging arena, then ONE launch per kernel for every job of every
-//           channel: CRC32C + Snappy.encode of all encoder slices, Snappy.decode (+ CRC verify) of all
-//           compressed chunks, CRC32C of uncompressed chunks, and a finish kernel that writes each
-//           job's result — framed encoder output, or the decoder's messages — straight into mapped
-//           pinned host memory (only the result bytes cross PCIe; no D2H of capacity-sized slots).
+//   flush   the staging arena and registered inputs to the device (one gather launch reading the
+//           mapped pages; a large staging arena by one DMA copy), then ONE launch per kernel for every
+//           job of every channel: CRC32C + Snappy.encode of all encoder slices, Snappy.decode (+ CRC
+//           verify) of all compressed chunks, CRC32C of uncompressed chunks, and a finish kernel that
+//           writes each job's result — framed encoder output, or the decoder's messages — straight
+//           into mapped pinned host memory, or into a device mirror moved by one DMA copy when the
+//           decoded messages fill most of a large result arena (only result bytes cross PCIe).
 //   poll    hipEventQuery: 1 when the job's batch is done (never blocks); wait() blocks (tests).
 //   streams flushes go round-robin to kStreams HIP streams, so one batch's host gather / result
 //           writes (PCIe) overlap the next batch's kernels; results are still APPLIED in flush order
