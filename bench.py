@@ -608,15 +608,22 @@ def e2e_capi(channels: int, messages: int, timeout: float = 240.0, dec_flush_mib
     exe = os.path.join(ROOT, "netty_amd", "e2e_capi")
     if not os.path.exists(exe):
         return {"error": "netty_amd/e2e_capi not built (make -C netty_amd)"}
+    # 16 hardware queues for the child's HIP streams (HIP's default is 4): with 4, the batcher's four
+    # streams share queues with the null stream and a batch's kernels wait behind another stream's
+    # result copy (round 4, one box, three runs each: decode 25.4-27.1 GiB/s with 4, 28.2-28.7 with
+    # 16; profiles/r04/s4/e2e_hwq.log).  A caller's own setting wins.
+    env = dict(os.environ)
+    env.setdefault("GPU_MAX_HW_QUEUES", "16")
     try:
         r = subprocess.run([exe, str(channels), str(messages), "65535", "3", "0", str(dec_flush_mib)], capture_output=True, text=True,
-                           timeout=timeout)
+                           timeout=timeout, env=env)
     except subprocess.TimeoutExpired:
         return {"error": f"timed out after {timeout}s"}
     try:
         d = json.loads(r.stdout.strip().splitlines()[-1])
     except (ValueError, IndexError):
         return {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+    d["gpu_max_hw_queues"] = int(env["GPU_MAX_HW_QUEUES"])
     d["path"] = ("pooled-direct-ByteBuf stand-in (registered host memory) -> nx_snappy_frame_encoder_submit x N -> one flush "
                  "-> framed bytes in mapped pinned memory -> (network: copied, untimed, into a registered receive buffer) -> "
                  "nx_snappy_frame_decoder_submit_registered x N (auto-flush every decode_flush_mib) -> messages; decode_copied_*: the same through "
