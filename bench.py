@@ -411,11 +411,11 @@ def encoder_placement():
     import ctypes
     from netty_amd import _lib
     L = _lib.load()
-    ms = (ctypes.c_float * 16)()
+    ms = (ctypes.c_float * 32)()
     n, pick = ctypes.c_int32(0), ctypes.c_int32(-1)
-    if L.nx_snappy_encode_placement(ms, 16, ctypes.byref(n), ctypes.byref(pick)) != 0:
+    if L.nx_snappy_encode_placement(ms, 32, ctypes.byref(n), ctypes.byref(pick)) != 0:
         return None
-    return {"note": "k_ws_probe ms per candidate workspace (256 dependent exchanges per lane), two draws of up to six; the encoder keeps the fastest",
+    return {"note": "k_ws_probe ms per candidate workspace (256 dependent exchanges per lane), four draws of up to six; the encoder keeps the fastest",
             "probe_ms": [round(ms[k], 3) for k in range(n.value)], "pick": pick.value}
 
 
@@ -611,9 +611,10 @@ def e2e_capi(channels: int, messages: int, timeout: float = 240.0, dec_flush_mib
     # 16 hardware queues for the child's HIP streams (HIP's default is 4): with 4, the batcher's four
     # streams share queues with the null stream and a batch's kernels wait behind another stream's
     # result copy (round 4, one box, three runs each: decode 25.4-27.1 GiB/s with 4, 28.2-28.7 with
-    # 16; profiles/r04/s4/e2e_hwq.log).  A caller's own setting wins.
+    # 16; profiles/r04/s4/e2e_hwq.log).  A caller's setting of 16 or more is kept.
     env = dict(os.environ)
-    env.setdefault("GPU_MAX_HW_QUEUES", "16")
+    if int(env.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:  # (the GPU boxes export HIP's default, 4)
+        env["GPU_MAX_HW_QUEUES"] = "16"
     try:
         r = subprocess.run([exe, str(channels), str(messages), "65535", "3", "0", str(dec_flush_mib)], capture_output=True, text=True,
                            timeout=timeout, env=env)

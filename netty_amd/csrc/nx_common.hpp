@@ -176,7 +176,7 @@ __global__ void __launch_bounds__(256) k_ws_probe(E* __restrict__ ws, uint32_t p
 }
 constexpr size_t kPlaceMinBytes = (size_t)2 << 30;  // smaller workspaces (handler / batcher sizes): allocated directly
 constexpr int kPlaceCandidates = 6;  // drawn at once (each while the others are held, so each lands elsewhere)
-constexpr int kPlaceRounds = 2;      // draws; the best so far is held through the next draw
+constexpr int kPlaceRounds = 4;      // draws; the best so far is held through the next draw
 constexpr uint32_t kPlaceSteps = 256;
 
 // Allocate a zeroed workspace of `lanes` tables of 2^lg entries each.  A large one is the fastest of
@@ -184,8 +184,9 @@ constexpr uint32_t kPlaceSteps = 256;
 // candidates stay allocated while the next is drawn, so each lands elsewhere; between draws all but
 // the best so far are freed, and the next draw lands on other placements again (a box whose first six
 // candidates were all slow, profiles/r03/s6, left the encoder ~4 % slower; scripts/experiments/
-// placement_redraw.py shows later draws reaching the fast placements).  A candidate is only drawn
-// while 8 GiB stay free.
+// placement_redraw.py shows later draws reaching the fast placements; round 4: a box whose twelve
+// candidates in two draws held no fast one ran the encoder at 55.3 GiB/s against 57.0-57.8 elsewhere,
+// profiles/r04/s5, so four draws of six).  A candidate is only drawn while 8 GiB stay free.
 struct PlacementReport {
     int n = 0;      // candidates probed (0: allocated directly, below kPlaceMinBytes)
     int pick = -1;  // the one kept

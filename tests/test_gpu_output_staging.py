@@ -171,10 +171,10 @@ def test_encoder_workspace_placement_report(dev, B, oracle):
     s.synchronize()
     assert int((st != 0).sum()) == 0
     L = _lib.load()
-    ms = (ctypes.c_float * 16)()
+    ms = (ctypes.c_float * 32)()
     n, pick = ctypes.c_int32(0), ctypes.c_int32(-1)
-    assert L.nx_snappy_encode_placement(ms, 16, ctypes.byref(n), ctypes.byref(pick)) == 0
-    assert 1 <= n.value <= 12 and 0 <= pick.value < n.value  # two draws of up to six
+    assert L.nx_snappy_encode_placement(ms, 32, ctypes.byref(n), ctypes.byref(pick)) == 0
+    assert 1 <= n.value <= 24 and 0 <= pick.value < n.value  # four draws of up to six
     probe = [ms[k] for k in range(n.value)]
     assert all(p > 0 for p in probe)
     assert probe[pick.value] == min(probe)
