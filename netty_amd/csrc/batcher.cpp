@@ -1830,7 +1830,7 @@ extern "C" int64_t nx_lzf_decoder_submit(nx_lzf_decoder* d, nx_batcher* b, const
 
 extern "C" int64_t nx_lz4_frame_decoder_submit(nx_lz4_frame_decoder* d, nx_batcher* b, const uint8_t* in, size_t n,
                                                size_t* consumed) {
-    if (!d) return NX_ERR_INVALID_ARG;
+    if (!d || !b || (!in && n) || !consumed) return NX_ERR_INVALID_ARG;
     if (d->st.state == 2 && !d->corrupted && !d->parse_failed) {  // FINISHED: everything is skipped (:250-254)
         std::lock_guard<std::mutex> lk(b->mu);
         Batch* bt = collecting(b);
@@ -2111,9 +2111,13 @@ extern "C" int32_t nx_batcher_reserve_arenas(nx_batcher* b, uint32_t nbatches, s
         x->staging.cnt = x->out.cnt = x->gops.cnt = &b->arena;
         b->all.push_back(x);
     }
-    for (Batch* x : b->all)  // an in-flight batch's arenas are in use: sized when it is reused
-        if (!x->inflight && (!x->staging.ensure(staging_bytes, x->st_used) || !x->out.ensure(out_bytes, x->out_used) ||
-                             !x->gops.ensure(1u << 20, 0)))
+    // A batch that holds jobs is left alone: an in-flight batch's arenas are being written, and the
+    // results of an applied batch whose tickets are not all released (nx_batcher_result's messages),
+    // or the staged bytes a collecting batch's jobs point into, live in its arenas; growing one
+    // frees the old buffer under them.  Such a batch is sized when it is reused (reset, then staged).
+    for (Batch* x : b->all)
+        if (!x->inflight && x->live == 0 && x->jobs.empty() &&
+            (!x->staging.ensure(staging_bytes, x->st_used) || !x->out.ensure(out_bytes, x->out_used) || !x->gops.ensure(1u << 20, 0)))
             return NX_ERR_HIP;
     return NX_OK;
 }
