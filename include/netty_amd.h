@@ -69,6 +69,7 @@ int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const 
 #define NX_WS_FASTLZ_ENC 2
 #define NX_WS_LZF_ENC 3
 #define NX_WS_DEC_RECORDS 4
+#define NX_WS_LZ4HC_ENC 5
 int32_t nx_snappy_encoder_reserve(uint32_t max_chunks, void* stream);
 int32_t nx_workspaces_trim(void);
 int32_t nx_workspace_info(int32_t kind, uint64_t* bytes, int32_t* owners);
@@ -94,13 +95,23 @@ int32_t nx_snappy_decode_batch(const uint8_t* in, const uint64_t* in_off, const 
                                uint32_t n, void* stream);
 
 /* Same contract as nx_snappy_decode_batch, single-kernel variant: each wave parses its frame's tag
- * stream itself (speculative 64-byte windows) and expands it (cross-check of the parse/expand pair,
- * and the path nx_snappy_decode_batch takes for frames of more than 16384 output-producing tags). */
+ * stream itself (speculative 64-byte windows) and expands it.  nx_snappy_decode_batch takes this path
+ * for batches of up to 32768 frames (a lone frame decodes in ~0.9 ms instead of the lane-serial
+ * parse's ~4 ms) and for frames of more than 16384 output-producing tags. */
 int32_t nx_snappy_decode_batch_fused(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                      uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                      uint32_t* out_len, uint32_t* consumed, int32_t* status,
                                      const uint32_t* expected_masked_crc, uint32_t* crc_out,
                                      uint32_t n, void* stream);
+
+/* Same contract, always the throughput pair (lane-serial parse to records, then the record
+ * expander) whatever the batch size: what nx_snappy_decode_batch runs above 32768 frames.  Exported so
+ * the parity tests and A/B tools exercise the pair on small batches too. */
+int32_t nx_snappy_decode_batch_pair(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                    uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                    uint32_t* out_len, uint32_t* consumed, int32_t* status,
+                                    const uint32_t* expected_masked_crc, uint32_t* crc_out,
+                                    uint32_t n, void* stream);
 
 
 /* Replaces the chunk walk of SnappyFrameDecoder.decode (SnappyFrameDecoder.java:85-231) as
@@ -182,6 +193,14 @@ size_t nx_lz4_max_compressed_length(size_t n);
 int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                             const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream);
 
+/* Same contract for lz4-java's highCompressor() (Lz4FrameEncoder(highCompressor = true),
+ * Lz4FrameEncoder.java:123-125,161-163): liblz4's LZ4_compress_HC at level 9 (hash-chain match finder,
+ * 256 candidates, pattern analysis, lazy three-match parse), bit-exact with the oracle's restatement,
+ * which is pinned byte-for-byte against pyarrow's liblz4 at level 9.  One lane per block with 256 KiB
+ * of tables in HBM (NX_WS_LZ4HC_ENC): a compatibility path, far slower than the fast compressor. */
+int32_t nx_lz4hc_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                              const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream);
+
 /* Replaces LZ4FastDecompressor.decompress as Lz4FrameDecoder.decode calls it for one
  * BLOCK_TYPE_COMPRESSED block (Lz4FrameDecoder.java:199-208; lz4-java 1.8.0 = liblz4's
  * LZ4_decompress_fast, restated from the published block format): block i = in[in_off[i] .. +in_len[i]) must decode to exactly out_len[i] bytes at
@@ -206,6 +225,11 @@ int32_t nx_xxhash32_batch(const uint8_t* in, const uint64_t* off, const uint32_t
 int32_t nx_lz4_frame_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                   uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
                                   int32_t compression_level, int32_t* status, uint32_t n, void* stream);
+/* The same with the block compressor chosen as the encoder's highCompressor flag (0: fast, else HC). */
+int32_t nx_lz4_frame_encode_batch_ex(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                     uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
+                                     int32_t compression_level, int32_t high_compressor, int32_t* status,
+                                     uint32_t n, void* stream);
 
 /* Replaces the block walk of Lz4FrameDecoder.decode (Lz4FrameDecoder.java:121-261) under
  * ByteToMessageDecoder.callDecode, for n device-resident cumulations (one per stream).
@@ -292,9 +316,16 @@ int32_t nx_fastlz_frame_decoder_decode(nx_fastlz_frame_decoder* d, const uint8_t
                                        size_t* consumed, const nx_msg** msgs, size_t* n_msgs,
                                        const char** err_msg);
 
-/* LzfEncoder(totalLength, compressThreshold)  LzfEncoder.java:127-216 */
+/* LzfEncoder(totalLength, compressThreshold)  LzfEncoder.java:127-216.  nx_lzf_encoder_new(t) =
+ * LzfEncoder(MAX_CHUNK_LEN, t); _new_ex(total_length, t) = LzfEncoder(totalLength, compressThreshold).
+ * NULL when totalLength is outside 16..65535 (:147-150) or compressThreshold < 16 (:152-156).
+ * totalLength does not change the output: it sizes compress-lzf's hash table, which the
+ * non-allocating ChunkEncoder LzfEncoder uses (:161-163) takes from max(totalLength, 65535)
+ * (16384 entries always).  The deprecated safeInstance flag selects an encoder with
+ * the same output (UnsafeChunkEncoderLE vs ChunkEncoder) and is not carried. */
 typedef struct nx_lzf_encoder nx_lzf_encoder;
 nx_lzf_encoder* nx_lzf_encoder_new(int32_t compress_threshold);
+nx_lzf_encoder* nx_lzf_encoder_new_ex(int32_t total_length, int32_t compress_threshold);
 void nx_lzf_encoder_free(nx_lzf_encoder* e);
 size_t nx_lzf_frame_max_encoded_length(size_t n);
 int64_t nx_lzf_encoder_encode(nx_lzf_encoder* e, const uint8_t* in, size_t n, uint8_t* out, size_t out_cap);
@@ -306,13 +337,21 @@ void nx_lzf_decoder_free(nx_lzf_decoder* d);
 int32_t nx_lzf_decoder_decode(nx_lzf_decoder* d, const uint8_t* in, size_t n, size_t* consumed,
                               const nx_msg** msgs, size_t* n_msgs, const char** err_msg);
 
-/* Lz4FrameEncoder(LZ4Factory.fastestInstance(), false, blockSize, new Lz4XXHash32(DEFAULT_SEED))
- * Lz4FrameEncoder.java:140-166; blockSize in [64, 2^25) (MAX_BLOCK_SIZE 2^25 itself is refused).
+/* Lz4FrameEncoder(LZ4Factory.fastestInstance(), highCompressor, blockSize, new Lz4XXHash32(DEFAULT_SEED),
+ * maxEncodeSize)  Lz4FrameEncoder.java:121-170; blockSize in [64, 2^25) (MAX_BLOCK_SIZE 2^25 itself
+ * is refused).  nx_lz4_frame_encoder_new(b) = _new_ex(b, 0, INT32_MAX) (:140-141, DEFAULT_MAX_ENCODE_SIZE).
+ * _new_ex returns NULL for max_encode_size <= 0 (checkPositive, :168) or a bad block size.
  * encode buffers a partial block (:231-248) and returns the bytes of every full block it flushed;
  * flush() writes the partial block (:291-300); close() flushes and appends the end block (:317-336),
- * after which encode passes bytes through (:233-239). */
+ * after which encode passes bytes through (:233-239).  encode and flush first size the output as
+ * allocateBuffer does (:190-214: sum over the pending bytes' blocks of LZ4_compressBound + 21) and
+ * fail with NX_ERR_LZ4_ENCODE_SIZE, changing nothing, when that exceeds maxEncodeSize; close does not
+ * (finishEncode allocates its footer directly, :306-315).  nx_lz4_frame_encoder_error: the last
+ * failure's message (the reference's EncoderException text), or NULL. */
 typedef struct nx_lz4_frame_encoder nx_lz4_frame_encoder;
 nx_lz4_frame_encoder* nx_lz4_frame_encoder_new(int32_t block_size);
+nx_lz4_frame_encoder* nx_lz4_frame_encoder_new_ex(int32_t block_size, int32_t high_compressor, int32_t max_encode_size);
+const char* nx_lz4_frame_encoder_error(nx_lz4_frame_encoder* e);
 void nx_lz4_frame_encoder_free(nx_lz4_frame_encoder* e);
 size_t nx_lz4_frame_max_encoded_length(size_t n, int32_t block_size);
 int64_t nx_lz4_frame_encoder_encode(nx_lz4_frame_encoder* e, const uint8_t* in, size_t n, uint8_t* out, size_t out_cap);

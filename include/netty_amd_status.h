@@ -68,6 +68,10 @@
 #define NX_ERR_LZ4_CHECKSUM_MISMATCH      (-56)
 /* :160-162  "stream corrupted: checksum error" (end block with a non-zero checksum) */
 #define NX_ERR_LZ4_END_CHECKSUM           (-57)
+/* Lz4FrameEncoder.allocateBuffer (Lz4FrameEncoder.java:190-214): EncoderException "requested encode
+ * buffer size (%d bytes) exceeds the maximum allowable size (%d bytes)" when the blocks of the pending
+ * bytes need more than maxEncodeSize (nx_lz4_frame_encoder_error has the message). */
+#define NX_ERR_LZ4_ENCODE_SIZE            (-58)
 
 /* Device frame scan (nx_snappy_frame_scan_batch), one code per SnappyFrameDecoder throw site: */
 /* :116-118  "Unexpected length of stream identifier: %d" */

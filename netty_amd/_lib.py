@@ -36,6 +36,7 @@ _SIGS = {
     "nx_snappy_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_snappy_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_snappy_decode_batch_fused": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
+    "nx_snappy_decode_batch_pair": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_crc32c_masked_batch": (i32, [vp, vp, vp, vp, u32, vp]),
     "nx_snappy_frame_scan_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, vp]),
     "nx_fastlz_compress_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
@@ -45,9 +46,11 @@ _SIGS = {
     "nx_lzf_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_lz4_decode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_lz4_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
+    "nx_lz4hc_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_lz4_max_compressed_length": (sz, [sz]),
     "nx_xxhash32_batch": (i32, [vp, vp, vp, u32, vp, u32, vp]),
     "nx_lz4_frame_encode_batch": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, u32, vp]),
+    "nx_lz4_frame_encode_batch_ex": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, vp, u32, vp]),
     "nx_lz4_frame_scan_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, vp]),
     "nx_textgen_device": (i32, [vp, u64, u32, u32, vp]),
     "nx_pack_batch": (i32, [vp, vp, vp, vp, vp, u32, vp]),
@@ -99,10 +102,13 @@ _SIGS = {
     "nx_fastlz_frame_decoder_decode": (i32, [vp, C.c_char_p, sz, C.POINTER(sz), C.POINTER(C.POINTER(NxMsg)),
                                              C.POINTER(sz), C.POINTER(C.c_char_p)]),
     "nx_lzf_encoder_new": (vp, [i32]),
+    "nx_lzf_encoder_new_ex": (vp, [i32, i32]),
     "nx_lzf_encoder_free": (None, [vp]),
     "nx_lzf_frame_max_encoded_length": (sz, [sz]),
     "nx_lzf_encoder_encode": (i64, [vp, C.c_char_p, sz, vp, sz]),
     "nx_lz4_frame_encoder_new": (vp, [i32]),
+    "nx_lz4_frame_encoder_new_ex": (vp, [i32, i32, i32]),
+    "nx_lz4_frame_encoder_error": (C.c_char_p, [vp]),
     "nx_lz4_frame_encoder_free": (None, [vp]),
     "nx_lz4_frame_max_encoded_length": (sz, [sz, i32]),
     "nx_lz4_frame_encoder_encode": (i64, [vp, C.c_char_p, sz, vp, sz]),

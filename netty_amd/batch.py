@@ -68,8 +68,8 @@ def snappy_decode(inp, in_off, in_len, out, out_off, out_cap=None, expected_crc=
                   out_len=None, status=None, variant="auto", fn=None):
     """Snappy.decode per chunk (+ fused masked-CRC32C verify).  Returns dict of tensors.
 
-    variant: "auto" (parse/expand kernel pair) or "fused" (single-kernel wave decoder), with the same
-    contract; fn: another entry point of that contract (the tests' lane-per-chunk cross-check kernel)."""
+    variant: "auto" (the fused decoder up to 32768 frames, the parse/expand pair above), "pair" (always
+    the parse/expand kernel pair) or "fused" (always the single-kernel wave decoder), same contract; fn: another entry point of that contract (the tests' lane-per-chunk cross-check kernel)."""
     n = in_len.numel()
     dev = inp.device
     out_len = torch.empty(n, dtype=torch.int32, device=dev) if out_len is None else out_len
@@ -78,7 +78,8 @@ def snappy_decode(inp, in_off, in_len, out, out_off, out_cap=None, expected_crc=
     crc = torch.empty(n, dtype=torch.int32, device=dev) if want_crc else None
     lib = _lib.load()
     if fn is None:
-        fn = {"auto": lib.nx_snappy_decode_batch, "fused": lib.nx_snappy_decode_batch_fused}[variant]
+        fn = {"auto": lib.nx_snappy_decode_batch, "fused": lib.nx_snappy_decode_batch_fused,
+              "pair": lib.nx_snappy_decode_batch_pair}[variant]
     _chk(fn(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(cons),
             _ptr(status), _ptr(expected_crc), _ptr(crc), n, _stream()), "nx_snappy_decode_batch")
     return {"out_len": out_len, "status": status, "consumed": cons, "crc": crc}
@@ -167,14 +168,16 @@ def lz4_max_compressed_length(n: int) -> int:
     return _lib.load().nx_lz4_max_compressed_length(n)
 
 
-def lz4_encode(inp, in_off, in_len, out, out_off):
-    """LZ4 block encode per chunk (nx_lz4_encode_batch).  Returns (out_len, status)."""
+def lz4_encode(inp, in_off, in_len, out, out_off, high: bool = False):
+    """LZ4 block encode per chunk (nx_lz4_encode_batch; high: lz4-java's highCompressor(), liblz4's
+    LZ4_compress_HC level 9, nx_lz4hc_encode_batch).  Returns (out_len, status)."""
     n = in_len.numel()
     dev = inp.device
     out_len = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
-    _chk(_lib.load().nx_lz4_encode_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_len),
-                                         _ptr(status), n, _stream()), "nx_lz4_encode_batch")
+    name = "nx_lz4hc_encode_batch" if high else "nx_lz4_encode_batch"
+    _chk(getattr(_lib.load(), name)(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off), _ptr(out_len),
+                                    _ptr(status), n, _stream()), name)
     return out_len, status
 
 
@@ -199,16 +202,18 @@ def xxhash32(inp, off, length, seed: int = LZ4_DEFAULT_SEED, out=None):
     return out
 
 
-def lz4_frame_encode(inp, in_off, in_len, out, out_off, compression_level: int = 6):
-    """Lz4FrameEncoder.flushBufferedData per block (nx_lz4_frame_encode_batch): header + block in each
-    out slot (capacity 21 + lz4_max_compressed_length).  Returns (out_len, status)."""
+def lz4_frame_encode(inp, in_off, in_len, out, out_off, compression_level: int = 6, high: bool = False):
+    """Lz4FrameEncoder.flushBufferedData per block (nx_lz4_frame_encode_batch_ex): header + block in each
+    out slot (capacity 21 + lz4_max_compressed_length); high = the highCompressor flag.
+    Returns (out_len, status)."""
     n = in_len.numel()
     dev = inp.device
     out_len = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
-    _chk(_lib.load().nx_lz4_frame_encode_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
-                                               _ptr(out_len), int(compression_level), _ptr(status), n, _stream()),
-         "nx_lz4_frame_encode_batch")
+    _chk(_lib.load().nx_lz4_frame_encode_batch_ex(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
+                                                  _ptr(out_len), int(compression_level), int(bool(high)), _ptr(status), n,
+                                                  _stream()),
+         "nx_lz4_frame_encode_batch_ex")
     return out_len, status
 
 

@@ -328,9 +328,15 @@ struct nx_lz4_frame_encoder {
     nx::h::Gpu g;
     uint32_t block_size = 65536;
     int32_t level = 6;
+    bool high = false;                  // highCompressor (Lz4FrameEncoder.java:161-163)
+    int32_t max_encode_size = 0x7FFFFFFF;  // maxEncodeSize (:168), DEFAULT_MAX_ENCODE_SIZE
+    std::string err;                    // the last failure's message
     bool finished = false;
     std::vector<uint8_t> buf;  // the block buffer (Lz4FrameEncoder.java:221-226)
 };
+
+// allocateBuffer's maxEncodeSize check (handlers.cpp; the batcher's submit runs it too)
+int32_t nx_lz4_frame_encoder_check_size(nx_lz4_frame_encoder* e, uint64_t remaining);
 
 struct nx_alt_decoder_base {
     nx::h::Gpu g;

@@ -1102,8 +1102,10 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         for (uint32_t a0 = 0; a0 < nze;) {  // one launch per compression level (usually one)
             uint32_t a1 = a0;
             while (a1 < nze && bt->lz4_e.aux[a1] == bt->lz4_e.aux[a0]) ++a1;
-            r = nx_lz4_frame_encode_batch(din, U64(2, 0) + a0, U32(2, 1) + a0, aslots, U64(2, 2) + a0, (uint32_t*)(D + o_zolen) + a0,
-                                          (int32_t)bt->lz4_e.aux[a0], (int32_t*)(D + o_zst) + a0, a1 - a0, s);
+            // aux = compressionLevel | highCompressor << 8: one launch per (level, compressor)
+            r = nx_lz4_frame_encode_batch_ex(din, U64(2, 0) + a0, U32(2, 1) + a0, aslots, U64(2, 2) + a0, (uint32_t*)(D + o_zolen) + a0,
+                                             (int32_t)(bt->lz4_e.aux[a0] & 0xFFu), (int32_t)(bt->lz4_e.aux[a0] >> 8),
+                                             (int32_t*)(D + o_zst) + a0, a1 - a0, s);
             if (r != NX_OK) return r;
             b->launches += 1;
             a0 = a1;
@@ -1941,8 +1943,15 @@ extern "C" int64_t nx_lzf_encoder_submit(nx_lzf_encoder* e, nx_batcher* b, const
 // encode passes bytes through, :233-239).  The handle's block buffer advances at submit.
 extern "C" int64_t nx_lz4_frame_encoder_submit(nx_lz4_frame_encoder* e, nx_batcher* b, const uint8_t* in, size_t n, int32_t op) {
     if (!e || !b || (!in && n) || op < 0 || op > 2) return NX_ERR_INVALID_ARG;
+    // allocateBuffer's maxEncodeSize check (Lz4FrameEncoder.java:190-214): write() sizes the message
+    // plus the buffered bytes; a bare flush (op 1, no bytes) sizes the buffer (:296-304); finishEncode
+    // checks nothing (:306-315).  Nothing is queued or buffered when it fails.
+    if (n > 0 || op == 0 || (op == 1 && !e->buf.empty())) {
+        const int32_t r = nx_lz4_frame_encoder_check_size(e, (uint64_t)n + e->buf.size());
+        if (r != NX_OK) return r;
+    }
     std::lock_guard<std::mutex> lk(b->mu);
-    if (!ensure_held(b, nx::WsKind::Lz4Enc)) return NX_ERR_HIP;
+    if (!ensure_held(b, e->high ? nx::WsKind::Lz4HcEnc : nx::WsKind::Lz4Enc)) return NX_ERR_HIP;
     Batch* bt = collecting(b);
     if (!bt) return NX_ERR_HIP;
     Job* j = new_alt_job(b, 2, 2);
@@ -1988,7 +1997,7 @@ extern "C" int64_t nx_lz4_frame_encoder_submit(nx_lz4_frame_encoder* e, nx_batch
                 P.slot = bt->aslots;
                 const uint64_t cap = nx::af::kLz4Header + nx_lz4_max_compressed_length(len);
                 bt->aslots += align16(cap) + 16;
-                P.res = push_list(bt->lz4_e, P.src, len, P.slot, (uint32_t)e->level);
+                P.res = push_list(bt->lz4_e, P.src, len, P.slot, (uint32_t)e->level | (e->high ? 0x100u : 0u));
                 bt->apc.push_back(P);
                 out_need += cap;
             }

@@ -45,7 +45,7 @@ static void build_tables(CrcTables* t) {
         for (int k = 0; k < 4; ++k)
             for (uint32_t b = 0; b < 256; ++b) t->SH[j][k][b] = gf_multmodp(K, b << (8 * k));
     }
-    for (int j = 0; j < 6; ++j) {
+    for (int j = 0; j < 7; ++j) {
         uint32_t K = gf_x8n(8ull << j);
         for (int k = 0; k < 8; ++k)
             for (uint32_t v = 0; v < 16; ++v) t->NS[j][k][v] = gf_multmodp(K, v << (4 * k));

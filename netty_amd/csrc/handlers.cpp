@@ -593,8 +593,19 @@ extern "C" int32_t nx_fastlz_frame_decoder_decode(nx_fastlz_frame_decoder* d, co
 }
 
 // ======================================================================= LZF encoder / decoder
+// LzfEncoder(totalLength, compressThreshold) (LzfEncoder.java:127-166).  totalLength is validated as
+// :147-150 does (MIN_BLOCK_TO_COMPRESS 16 .. MAX_CHUNK_LEN 65535) and does not change the bytes: it
+// only sizes the ChunkEncoder's hash table, and the non-allocating encoders LzfEncoder takes
+// (ChunkEncoderFactory.optimalNonAllocatingInstance / safeNonAllocatingInstance, :161-163) size it from
+// max(totalLength, MAX_CHUNK_LEN), i.e. the 16384-entry table for every totalLength (compress-lzf
+// 1.0.3 ChunkEncoder(int, BufferRecycler, boolean); DESIGN.md §2: restated, not pinned).
+extern "C" nx_lzf_encoder* nx_lzf_encoder_new_ex(int32_t total_length, int32_t compress_threshold) {
+    if (total_length < 16 || total_length > 65535) return nullptr;  // :147-150
+    return nx_lzf_encoder_new(compress_threshold);
+}
+
 extern "C" nx_lzf_encoder* nx_lzf_encoder_new(int32_t compress_threshold) {
-    if (compress_threshold < 16) return nullptr;  // LzfEncoder.java:155-160
+    if (compress_threshold < 16) return nullptr;  // LzfEncoder.java:152-156
     auto* e = new nx_lzf_encoder();
     if (!e->g.hold(nx::WsKind::LzfEnc)) {
         delete e;
@@ -767,21 +778,27 @@ using nx::af::kLz4Magic;
 using nx::af::kLz4Seed;
 
 
-extern "C" nx_lz4_frame_encoder* nx_lz4_frame_encoder_new(int32_t block_size) {
+extern "C" nx_lz4_frame_encoder* nx_lz4_frame_encoder_new_ex(int32_t block_size, int32_t high_compressor, int32_t max_encode_size) {
     // compressionLevel(blockSize) :158-166; the device block encoder takes blocks below 32 MiB
-    if (block_size < 64 || block_size > (1 << 25)) return nullptr;
+    if (block_size < 64 || block_size > (1 << 25) || max_encode_size <= 0) return nullptr;
     auto* e = new nx_lz4_frame_encoder();
-    if (!e->g.hold(nx::WsKind::Lz4Enc)) {
+    e->high = high_compressor != 0;
+    if (!e->g.hold(e->high ? nx::WsKind::Lz4HcEnc : nx::WsKind::Lz4Enc)) {
         delete e;
         return nullptr;
     }
+    e->max_encode_size = max_encode_size;
     e->block_size = (uint32_t)block_size;
     const int32_t ceil_log2 = 32 - __builtin_clz((uint32_t)block_size - 1u);
     e->level = ceil_log2 - 10 > 0 ? ceil_log2 - 10 : 0;
     e->buf.reserve(block_size);
     return e;
 }
+extern "C" nx_lz4_frame_encoder* nx_lz4_frame_encoder_new(int32_t block_size) {
+    return nx_lz4_frame_encoder_new_ex(block_size, 0, 0x7FFFFFFF);
+}
 extern "C" void nx_lz4_frame_encoder_free(nx_lz4_frame_encoder* e) { delete e; }
+extern "C" const char* nx_lz4_frame_encoder_error(nx_lz4_frame_encoder* e) { return e && !e->err.empty() ? e->err.c_str() : nullptr; }
 extern "C" size_t nx_lz4_frame_max_encoded_length(size_t n, int32_t block_size) {
     const size_t bs = block_size > 0 ? (size_t)block_size : 65536;
     return (n / bs + 2) * (kLz4Header + 16 + bs / 255) + n + kLz4Header;
@@ -809,8 +826,9 @@ int64_t lz4_flush_blocks(nx_lz4_frame_encoder* e, const uint8_t* src, size_t n, 
     bool ok = g.h2d(g.din.p, src, n) && g.h2d(g.a0.p, ioff.data(), 8ull * nb) && g.h2d(g.a1.p, ooff.data(), 8ull * nb) &&
               g.h2d(g.a2.p, ilen.data(), 4ull * nb);
     if (!ok) return NX_ERR_HIP;
-    int32_t r = nx_lz4_frame_encode_batch(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.dout.as<uint8_t>(),
-                                          g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), e->level, g.a4.as<int32_t>(), nb, g.s);
+    int32_t r = nx_lz4_frame_encode_batch_ex(g.din.as<uint8_t>(), g.a0.as<uint64_t>(), g.a2.as<uint32_t>(), g.dout.as<uint8_t>(),
+                                             g.a1.as<uint64_t>(), g.a3.as<uint32_t>(), e->level, e->high ? 1 : 0, g.a4.as<int32_t>(), nb,
+                                             g.s);
     if (r != NX_OK) return r;
     std::vector<uint32_t> olen(nb);
     std::vector<int32_t> st(nb);
@@ -832,10 +850,39 @@ int64_t lz4_flush_blocks(nx_lz4_frame_encoder* e, const uint8_t* src, size_t n, 
 }
 }  // namespace
 
+// allocateBuffer's size check (:190-214): the blocks of `remaining` pending bytes, each
+// maxCompressedLength(curSize) + HEADER_LENGTH, against maxEncodeSize (Java int arithmetic: a sum
+// that overflows is negative and fails too).  Returns NX_OK or NX_ERR_LZ4_ENCODE_SIZE with the message.
+int32_t nx_lz4_frame_encoder_check_size(nx_lz4_frame_encoder* e, uint64_t remaining) {
+    if (remaining > 0x7FFFFFFFull) {  // int remaining < 0 (:195-197)
+        e->err = "too much data to allocate a buffer for compression";
+        return NX_ERR_LZ4_ENCODE_SIZE;
+    }
+    int64_t target = 0;
+    while (remaining > 0) {
+        const uint64_t cur = remaining < e->block_size ? remaining : e->block_size;
+        remaining -= cur;
+        target += (int64_t)nx_lz4_max_compressed_length(cur) + (int64_t)kLz4Header;
+    }
+    const int32_t t32 = (int32_t)(uint32_t)(uint64_t)target;  // the Java int sum
+    if (t32 > e->max_encode_size || t32 < 0) {
+        char buf[160];
+        snprintf(buf, sizeof buf, "requested encode buffer size (%d bytes) exceeds the maximum allowable size (%d bytes)", t32,
+                 e->max_encode_size);
+        e->err = buf;
+        return NX_ERR_LZ4_ENCODE_SIZE;
+    }
+    return NX_OK;
+}
+
 extern "C" int64_t nx_lz4_frame_encoder_encode(nx_lz4_frame_encoder* e, const uint8_t* in, size_t n, uint8_t* out,
                                                size_t out_cap) {
     const nx::NoGrowScope no_grow;
     if (!e || (!in && n)) return NX_ERR_INVALID_ARG;
+    {   // MessageToByteEncoder.write: allocateBuffer before encode (:190-214), also after close()
+        const int32_t r = nx_lz4_frame_encoder_check_size(e, (uint64_t)n + e->buf.size());
+        if (r != NX_OK) return r;
+    }
     if (e->finished) {  // :233-239 — after close() the bytes pass through
         if (out_cap < n) return NX_ERR_INVALID_ARG;
         if (n) memcpy(out, in, n);
@@ -863,19 +910,27 @@ extern "C" int64_t nx_lz4_frame_encoder_encode(nx_lz4_frame_encoder* e, const ui
     return w;
 }
 
-extern "C" int64_t nx_lz4_frame_encoder_flush(nx_lz4_frame_encoder* e, uint8_t* out, size_t out_cap) {
-    const nx::NoGrowScope no_grow;
-    if (!e) return NX_ERR_INVALID_ARG;  // flush() :291-300
+static int64_t lz4_flush_buffer(nx_lz4_frame_encoder* e, uint8_t* out, size_t out_cap) {
     const int64_t w = lz4_flush_blocks(e, e->buf.data(), e->buf.size(), out, out_cap);
     if (w >= 0) e->buf.clear();
     return w;
 }
 
+extern "C" int64_t nx_lz4_frame_encoder_flush(nx_lz4_frame_encoder* e, uint8_t* out, size_t out_cap) {
+    const nx::NoGrowScope no_grow;
+    if (!e) return NX_ERR_INVALID_ARG;  // flush() :296-304: allocateBuffer(ctx, EMPTY_BUFFER, .., false) first
+    if (!e->buf.empty()) {
+        const int32_t r = nx_lz4_frame_encoder_check_size(e, e->buf.size());
+        if (r != NX_OK) return r;
+    }
+    return lz4_flush_buffer(e, out, out_cap);
+}
+
 extern "C" int64_t nx_lz4_frame_encoder_close(nx_lz4_frame_encoder* e, uint8_t* out, size_t out_cap) {
     const nx::NoGrowScope no_grow;
     if (!e) return NX_ERR_INVALID_ARG;
-    if (e->finished) return 0;  // finishEncode :318-321
-    const int64_t w = nx_lz4_frame_encoder_flush(e, out, out_cap);
+    if (e->finished) return 0;  // finishEncode :306-310
+    const int64_t w = lz4_flush_buffer(e, out, out_cap);  // the footer buffer: no maxEncodeSize check (:313-315)
     if (w < 0) return w;
     if ((size_t)w + kLz4Header > out_cap) return NX_ERR_INVALID_ARG;
     uint8_t* f = out + w;  // the end block :326-335

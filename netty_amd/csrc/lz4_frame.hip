@@ -282,9 +282,19 @@ extern "C" int32_t nx_xxhash32_batch(const uint8_t* in, const uint64_t* off, con
     return NX_OK;
 }
 
+extern "C" int32_t nx_lz4hc_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                         const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream);
+
 extern "C" int32_t nx_lz4_frame_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                              uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
                                              int32_t compression_level, int32_t* status, uint32_t n, void* stream) {
+    return nx_lz4_frame_encode_batch_ex(in, in_off, in_len, out, out_off, out_len, compression_level, 0, status, n, stream);
+}
+
+extern "C" int32_t nx_lz4_frame_encode_batch_ex(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                                uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
+                                                int32_t compression_level, int32_t high_compressor, int32_t* status, uint32_t n,
+                                                void* stream) {
     NX_CLEAR_STALE_ERROR();
     if (n == 0) return NX_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_len || !status || compression_level < 0 ||
@@ -292,7 +302,8 @@ extern "C" int32_t nx_lz4_frame_encode_batch(const uint8_t* in, const uint64_t* 
         return NX_ERR_INVALID_ARG;
     const hipStream_t st = (hipStream_t)stream;
     // block bodies go straight after each slot's header: the same out_off with the base moved by 21
-    int32_t rc = nx_lz4_encode_batch(in, in_off, in_len, out + nx::lz4f::kHeader, out_off, out_len, status, n, stream);
+    int32_t rc = (high_compressor ? nx_lz4hc_encode_batch : nx_lz4_encode_batch)(in, in_off, in_len, out + nx::lz4f::kHeader, out_off,
+                                                                               out_len, status, n, stream);
     if (rc != NX_OK) return rc;
     hipLaunchKernelGGL(nx::lz4f::k_xxhash32, dim3((n + 255) / 256), dim3(256), 0, st, in, in_off, in_len,
                        0x9747b28cu, (uint32_t*)nullptr, out, out_off, n);

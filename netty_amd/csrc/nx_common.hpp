@@ -34,12 +34,12 @@ constexpr uint32_t kCrcPoly = 0x82F63B78u;
 // Device-side CRC tables (filled once by crc_tables_init() on the host):
 //   T8[k][b]   : slicing-by-8 tables, T8[0] = byte table of Crc32c.java:27-92
 //   SH[j][k][b]: "shift by 16*2^j bytes" linear maps, j = 0..9 (16 B .. 8 KiB), byte k of the state
-//   NS[j][k][v]: nibble form of "shift by 8*2^j bytes", j = 0..5 (8 B .. 256 B), nibble k of the state
+//   NS[j][k][v]: nibble form of "shift by 8*2^j bytes", j = 0..6 (8 B .. 512 B), nibble k of the state
 //   XI[k]      : x^(-8k) mod P, k = 0..15 ("un-shift" by k zero bytes)
 struct CrcTables {
     uint32_t T8[8][256];
     uint32_t SH[10][4][256];
-    uint32_t NS[6][8][16];
+    uint32_t NS[7][8][16];  // shift by 8 * 2^j bytes (j = 6: 512 B, the unit expander's 16-byte lane slots)
     uint32_t XI[16];
 };
 // Device copy of the tables, allocated once per device by crc_tables_init() (kernels take the

@@ -59,6 +59,8 @@ constexpr int32_t kGuardTrip = -99;
 constexpr uint32_t kRecCap = 16384;      // records per frame slot (64 KiB)
 constexpr int32_t kNeedFused = -1000;    // internal status: the frame goes to k_decode_fused
 constexpr uint32_t kSubBatch = 262144;   // frames per parse/expand launch pair (16 GiB of record slots)
+constexpr uint32_t kFusedMaxFrames = 32768;  // batches up to this size decode on k_decode_fused alone
+constexpr int kDecodeAuto = 0, kDecodeFused = 1, kDecodePair = 2;  // decode_batch modes
 
 // CRC tables staged in LDS per workgroup: slicing-by-4 (4 KiB) and shift-by-512 B (4 KiB).  The
 // nibble tables of the once-per-frame fold are read from global memory.
@@ -1042,6 +1044,9 @@ __global__ void __launch_bounds__(kExpandWaves * 64, kExpandStaged ? 6 : 3)
 }
 
 
+#include "expand_units.hpp"
+
+
 // =====================================================================================
 // LZ4 blocks through the same record expander
 // =====================================================================================
@@ -1471,8 +1476,20 @@ static hipError_t wave_kernel_attrs(size_t lds) {
         attr_err = hipFuncSetAttribute((const void*)nx::dec::k_decode_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (attr_err == hipSuccess)
             attr_err = hipFuncSetAttribute((const void*)nx::dec::k_expand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kExpandLds);
+        if (attr_err == hipSuccess)
+            attr_err = hipFuncSetAttribute((const void*)nx::dec::k_expand_u, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nx::dec::kUxLds);
     });
     return attr_err;
+}
+
+// Which record expander launch_expand runs: the unit-lane k_expand_u (default) or the piece expander
+// k_expand (NX_EXPANDER=pieces, kept for same-box A/B runs).  Read once per process.
+static bool use_unit_expander() {
+    static const bool units = [] {
+        const char* e = getenv("NX_EXPANDER");
+        return !(e && strcmp(e, "pieces") == 0);
+    }();
+    return units;
 }
 
 // one launch of the record expander over m frames
@@ -1480,6 +1497,13 @@ static hipError_t launch_expand(const uint8_t* in, const uint64_t* in_off, const
                                 const uint32_t* rec, const uint32_t* nrec, uint32_t* out_len, int32_t* status, const uint32_t* expect,
                                 uint32_t* crc_out, uint32_t m, int cus, hipStream_t st) {
     using namespace nx::dec;
+    if (use_unit_expander()) {
+        const uint64_t per_cu = 160 * 1024 / kUxLds;
+        const uint64_t want = (uint64_t)cus * per_cu, need = (m + kUxWaves - 1) / kUxWaves;
+        hipLaunchKernelGGL(k_expand_u, dim3((unsigned)(need < want ? need : want)), dim3(kUxWaves * 64), kUxLds, st, in, in_off, in_len,
+                           out, out_off, rec, nrec, out_len, status, expect, crc_out, m, nx::crc_tables_dev());
+        return hipGetLastError();
+    }
 #ifdef NX_EXPAND_BLOCKS_PER_CU
     const uint64_t per_cu = NX_EXPAND_BLOCKS_PER_CU;
 #else
@@ -1493,7 +1517,7 @@ static hipError_t launch_expand(const uint8_t* in, const uint64_t* in_off, const
 
 static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
                             const uint32_t* out_cap, uint32_t* out_len, uint32_t* consumed, int32_t* status,
-                            const uint32_t* expected_masked_crc, uint32_t* crc_out, uint32_t n, void* stream, bool fused_only) {
+                            const uint32_t* expected_masked_crc, uint32_t* crc_out, uint32_t n, void* stream, int mode) {
     NX_CLEAR_STALE_ERROR();
     using namespace nx::dec;
     if (n == 0) return NX_OK;
@@ -1512,6 +1536,11 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
         const uint64_t need = (m + kWaves - 1) / kWaves;
         return (unsigned)(need < want ? need : want);
     };
+    // Batch-size policy (round 5, profiles/r05/s1/dec_latency.log): k_parse walks a frame's tags on
+    // one lane, ~4-7 ms for any batch that does not fill the chip, while k_decode_fused parses each
+    // frame wave-parallel (0.85 ms for one frame, 1.9 ms for 4 096, 5.6 ms for 16 384, against 4.3 /
+    // 7.4 / 9.1 for the pair).  The pair wins from ~34 K frames on (65 536: 16.4 vs 20.5 ms).
+    const bool fused_only = mode == kDecodeFused || (mode == kDecodeAuto && n <= kFusedMaxFrames);
     if (fused_only) {
         hipLaunchKernelGGL(k_decode_fused, dim3(wave_grid(n)), dim3(kWaves * 64), lds, st, in, in_off, in_len, out, out_off, out_cap,
                            out_len, consumed, status, expected_masked_crc, crc_out, n, nx::crc_tables_dev(), 0);
@@ -1548,7 +1577,7 @@ extern "C" int32_t nx_snappy_decode_batch(const uint8_t* in, const uint64_t* in_
                                           uint32_t* crc_out, uint32_t n, void* stream) {
     NX_CLEAR_STALE_ERROR();
     return decode_batch(in, in_off, in_len, out, out_off, out_cap, out_len, consumed, status, expected_masked_crc, crc_out, n, stream,
-                        false);
+                        nx::dec::kDecodeAuto);
 }
 
 extern "C" int32_t nx_snappy_decode_batch_fused(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
@@ -1556,7 +1585,15 @@ extern "C" int32_t nx_snappy_decode_batch_fused(const uint8_t* in, const uint64_
                                                 uint32_t* consumed, int32_t* status, const uint32_t* expected_masked_crc,
                                                 uint32_t* crc_out, uint32_t n, void* stream) {
     return decode_batch(in, in_off, in_len, out, out_off, out_cap, out_len, consumed, status, expected_masked_crc, crc_out, n, stream,
-                        true);
+                        nx::dec::kDecodeFused);
+}
+
+extern "C" int32_t nx_snappy_decode_batch_pair(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                               const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len,
+                                               uint32_t* consumed, int32_t* status, const uint32_t* expected_masked_crc,
+                                               uint32_t* crc_out, uint32_t n, void* stream) {
+    return decode_batch(in, in_off, in_len, out, out_off, out_cap, out_len, consumed, status, expected_masked_crc, crc_out, n, stream,
+                        nx::dec::kDecodePair);
 }
 
 // Replaces LZ4FastDecompressor.decompress as Lz4FrameDecoder.decode calls it for one

@@ -20,7 +20,7 @@
 
 namespace nx {
 
-enum class WsKind : int { SnappyEnc = 0, Lz4Enc, FastLzEnc, LzfEnc, DecRecords, Count };
+enum class WsKind : int { SnappyEnc = 0, Lz4Enc, FastLzEnc, LzfEnc, DecRecords, Lz4HcEnc, Count };
 
 // Table geometry per encoder kind (entry bytes, log2 entries per table, waves per CU of its launch);
 // each codec static_asserts its own constants against this.
@@ -29,7 +29,9 @@ struct WsSpec {
     uint32_t lg;
     unsigned waves_per_cu;
 };
-constexpr WsSpec kWsSpec[] = {{8, 14, 16}, {8, 13, 16}, {8, 13, 8}, {8, 14, 8}, {0, 0, 0}};
+// Lz4HcEnc: 2^15 x 8 bytes = liblz4's HC tables per lane (u32 hashTable[2^15] + u16 chainTable[2^16]),
+// 2 waves per CU (a dense launch holds 32 768 lanes, 8 GiB).
+constexpr WsSpec kWsSpec[] = {{8, 14, 16}, {8, 13, 16}, {8, 13, 8}, {8, 14, 8}, {0, 0, 0}, {8, 15, 2}};
 constexpr size_t kDecSlotBytes = 16384u * 4u + 8u;  // records of one frame + its count and length
 constexpr uint32_t kDecMaxFrames = 262144;           // frames per parse/expand launch pair
 

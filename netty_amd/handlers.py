@@ -199,14 +199,20 @@ class FastLzFrameDecoder(_Decoder):
 
 # ------------------------------------------------------------------------------------- LZF
 class LzfEncoder(_Encoder):
-    """LzfEncoder.java:36-253 (compressThreshold default 16, :42)."""
+    """LzfEncoder.java:36-253: LzfEncoder(totalLength = MAX_CHUNK_LEN, compressThreshold = 16)
+    (:111-166).  total_length is validated as the reference does and does not change the bytes
+    (include/netty_amd.h, nx_lzf_encoder_new_ex)."""
 
     _free = "nx_lzf_encoder_free"
+    MAX_CHUNK_LEN = 65535  # LZFChunk.MAX_CHUNK_LEN
+    MIN_BLOCK_TO_COMPRESS = 16  # LzfEncoder.java:42
 
-    def __init__(self, compress_threshold: int = 16):
-        if compress_threshold < 16:
+    def __init__(self, compress_threshold: int = 16, total_length: int = MAX_CHUNK_LEN):
+        if total_length < 16 or total_length > 65535:  # :147-150
+            raise ValueError(f"totalLength: {total_length} (expected: 16-65535)")
+        if compress_threshold < 16:  # :152-156
             raise ValueError(f"compressThreshold:{compress_threshold} expected >=16")
-        self._h = _new(_lib.load().nx_lzf_encoder_new(compress_threshold), "LzfEncoder")
+        self._h = _new(_lib.load().nx_lzf_encoder_new_ex(total_length, compress_threshold), "LzfEncoder")
 
     def encode(self, data: bytes) -> bytes:
         L = _lib.load()
@@ -230,23 +236,35 @@ class LzfDecoder(_Decoder):
 
 
 class Lz4FrameEncoder(_Encoder):
-    """Lz4FrameEncoder.java:61-403 (fast compressor, XXHash32 seed 0x9747b28c).  encode() returns the
-    full blocks it flushed (a partial block stays buffered, :231-248); flush() writes the partial
-    block (:291-300); finish_encode() = close(): flush + end block (:317-336)."""
+    """Lz4FrameEncoder.java:61-403 (XXHash32 seed 0x9747b28c).  high_compressor selects lz4-java's
+    highCompressor() (liblz4 LZ4_compress_HC level 9) over fastCompressor() (:121-125,161-163);
+    max_encode_size is the maxEncodeSize constructor argument (:150-170, default Integer.MAX_VALUE).
+    encode() returns the full blocks it flushed (a partial block stays buffered, :231-248); flush()
+    writes the partial block (:296-304); finish_encode() = close(): flush + end block (:306-330).
+    encode() and flush() raise EncoderException when the pending bytes' output would exceed
+    max_encode_size (allocateBuffer, :190-214), leaving the encoder unchanged."""
 
     _free = "nx_lz4_frame_encoder_free"
+    MAX_ENCODE_SIZE = (1 << 31) - 1  # DEFAULT_MAX_ENCODE_SIZE (:68)
 
-    def __init__(self, block_size: int = 1 << 16):
+    def __init__(self, block_size: int = 1 << 16, high_compressor: bool = False, max_encode_size: int = MAX_ENCODE_SIZE):
         if not 64 <= block_size <= 1 << 25:
             raise ValueError(f"blockSize: {block_size} (expected: 64-{1 << 25})")
+        if max_encode_size <= 0:  # ObjectUtil.checkPositive (:168)
+            raise ValueError(f"maxEncodeSize : {max_encode_size} (expected: > 0)")
         self.block_size = block_size
-        self._h = _new(_lib.load().nx_lz4_frame_encoder_new(block_size), "Lz4FrameEncoder")
+        self.high_compressor = bool(high_compressor)
+        self.max_encode_size = int(max_encode_size)
+        self._h = _new(_lib.load().nx_lz4_frame_encoder_new_ex(block_size, int(self.high_compressor), self.max_encode_size),
+                       "Lz4FrameEncoder")
 
     def _out(self, n: int):
         cap = _lib.load().nx_lz4_frame_max_encoded_length(n, self.block_size)
         return (C.c_uint8 * cap)(), cap
 
     def _ret(self, r, out) -> bytes:
+        if r == -58:  # NX_ERR_LZ4_ENCODE_SIZE: allocateBuffer's EncoderException
+            raise EncoderException(_lib.load().nx_lz4_frame_encoder_error(self._h).decode())
         if r < 0:
             raise CompressionException(_lib.status_string(r))
         return bytes(out[:r])

@@ -766,7 +766,10 @@ int32_t orc_lzf_decode_chunk(const uint8_t* in, int32_t in_len, uint8_t* out, in
 /* compress-lzf 1.0.3 ChunkEncoder.tryCompress (com.ning:compress-lzf, pom.xml:941-945; not vendored).
  * Netty's LzfEncoder takes ChunkEncoderFactory.optimalNonAllocatingInstance (LzfEncoder.java:161-163)
  * → UnsafeChunkEncoderLE on x86, whose output equals the safe ChunkEncoder's restated here:
- *   - int[16384] table (calcHashLen(max(65535, ...)) for the default totalLength = MAX_CHUNK_LEN),
+ *   - int[16384] table: the non-allocating constructor, ChunkEncoder(int totalLength, BufferRecycler,
+ *     boolean), sizes it as calcHashLen(max(totalLength, MAX_CHUNK_LEN)) = MAX_HASH_SIZE 16384 for
+ *     every totalLength LzfEncoder accepts (16..65535, LzfEncoder.java:147-150), so totalLength never
+ *     changes the bytes (restated from the published 1.0.3 source; unpinned: the library is absent),
  *     created with the encoder and kept for its lifetime: entries are absolute positions in the
  *     message array, zero-initialised (a Java zero is position 0); hash(h) = ((h * 57321) >> 9) &
  *     16383 on Java int (wrapping multiply, arithmetic shift) of `seen` = the big-endian int of the
@@ -1110,6 +1113,273 @@ last_literals:;
     return (int32_t)op;
 }
 
+/* LZ4_compress_HC at level 9 (LZ4HC_CLEVEL_DEFAULT), the block compressor lz4-java's JNI
+ * highCompressor() runs for Lz4FrameEncoder(highCompressor = true) (Lz4FrameEncoder.java:123-125,
+ * 161-163; lz4-java 1.8.0 bundles liblz4 1.9.x: a third-party dependency absent from the reference,
+ * pom.xml:946-950).  Restated from liblz4's published lz4hc.c: LZ4_compress_HC -> a zeroed
+ * LZ4_streamHC_t, LZ4HC_init_internal (indices start at 64 KiB, so an empty hash slot is below
+ * lowLimit) -> LZ4HC_compress_hashChain with nbSearches = 256 and patternAnalysis on (levels 9+):
+ *   - LZ4HC_Insert: every position up to the search point enters a 2^15-slot hash table (Knuth
+ *     hash of the 4 bytes) and a 64 Ki chain of u16 deltas to the previous position with that hash
+ *     (clamped to 65535);
+ *   - LZ4HC_InsertAndGetWiderMatch: walks the chain (at most 256 candidates, distance <= 65535),
+ *     screens a candidate by the 2 bytes at the current best length, extends forwards to
+ *     iend - LASTLITERALS and backwards to iLowLimit, and on runs of a 1-, 2- or 4-byte pattern
+ *     (chain delta 1) jumps along the repeated segment instead of stepping (pattern analysis);
+ *   - the lazy three-match parse (_Search2 / _Search3 with OPTIMAL_ML = 18 overlap corrections).
+ * Pinned byte-for-byte against pyarrow's bundled liblz4 (Codec('lz4_raw', compression_level=9)) by
+ * tests/test_oracle_kat.py; liblz4 kept this path's output unchanged from 1.9.x into pyarrow's
+ * 1.10 (its level changes were to levels 1-2), which that pin assumes. */
+enum { HC_LOG = 15, HC_DMAX = 65535, HC_OPT_ML = 18, HC_START = 65536, HC_ATTEMPTS = 256 };
+typedef struct {
+    uint32_t hash[1 << HC_LOG];
+    uint16_t chain[65536];
+    uint32_t next;     /* nextToUpdate */
+    const uint8_t* in; /* index i is in[i - HC_START] */
+} hc_ctx;
+#define HCP(c, i) ((c)->in + ((int64_t)(i) - HC_START))
+static uint32_t hc_hash(const uint8_t* p) { return (lz4_rd32(p) * 2654435761u) >> (32 - HC_LOG); }
+static uint16_t hc_rd16(const uint8_t* p) { uint16_t v; memcpy(&v, p, 2); return v; }
+
+static void hc_insert(hc_ctx* c, uint32_t target) {  /* LZ4HC_Insert: positions [next, target) */
+    for (uint32_t idx = c->next; idx < target; ++idx) {
+        const uint32_t h = hc_hash(HCP(c, idx));
+        uint32_t delta = idx - c->hash[h];
+        if (delta > HC_DMAX) delta = HC_DMAX;
+        c->chain[(uint16_t)idx] = (uint16_t)delta;
+        c->hash[h] = idx;
+    }
+    c->next = target;
+}
+static int64_t hc_count(const uint8_t* a, const uint8_t* b, const uint8_t* alim) {  /* LZ4_count */
+    const uint8_t* s = a;
+    while (a < alim && *a == *b) { ++a; ++b; }
+    return a - s;
+}
+/* LZ4HC_countPattern: bytes from p equal to the 4-byte pattern repeated (p[k] == pattern byte k mod 4) */
+static int64_t hc_count_pattern(const uint8_t* p, const uint8_t* end, uint32_t pat) {
+    int64_t k = 0;
+    while (p + k < end && p[k] == (uint8_t)(pat >> (8 * (k & 3)))) ++k;
+    return k;
+}
+/* LZ4HC_reverseCountPattern: bytes before p equal to the pattern read backwards from its byte 3 */
+static int64_t hc_rcount_pattern(const uint8_t* p, const uint8_t* low, uint32_t pat) {
+    int64_t k = 0;
+    while (p - k - 1 >= low && p[-k - 1] == (uint8_t)(pat >> (8 * (3 - (k & 3))))) ++k;
+    return k;
+}
+static int hc_protect(uint32_t dict_limit, uint32_t idx) { return (uint32_t)((dict_limit - 1) - idx) >= 3; }
+
+/* LZ4HC_InsertAndGetWiderMatch (prefix only: no dictionary; chainSwap off, as hashChain calls it) */
+static int hc_wider(hc_ctx* c, const uint8_t* ip, const uint8_t* ilow, const uint8_t* ihigh, int longest,
+                    const uint8_t** matchpos, const uint8_t** startpos) {
+    const uint32_t ip_idx = (uint32_t)(ip - c->in) + HC_START;
+    const uint32_t lowest = (HC_START + HC_DMAX + 1 > ip_idx) ? HC_START : ip_idx - HC_DMAX;
+    const int look_back = (int)(ip - ilow);
+    int attempts = HC_ATTEMPTS;
+    const uint32_t pattern = lz4_rd32(ip);
+    int repeat = 0; /* 0 untested, 1 confirmed, 2 not */
+    int64_t src_pattern_len = 0;
+    hc_insert(c, ip_idx);
+    uint32_t mi = c->hash[hc_hash(ip)];
+    while (mi >= lowest && attempts > 0) {
+        --attempts;
+        const uint8_t* mp = HCP(c, mi);
+        if (hc_rd16(ilow + longest - 1) == hc_rd16(mp - look_back + longest - 1) && lz4_rd32(mp) == pattern) {
+            int back = 0;
+            if (look_back) {
+                const int64_t mn = (ilow - ip) > (c->in - mp) ? (ilow - ip) : (c->in - mp);
+                while (back > mn && ip[back - 1] == mp[back - 1]) --back;
+            }
+            int ml = 4 + (int)hc_count(ip + 4, mp + 4, ihigh) - back;
+            if (ml > longest) {
+                longest = ml;
+                *matchpos = mp + back;
+                *startpos = ip + back;
+            }
+        }
+        const uint32_t dnext = c->chain[(uint16_t)mi];
+        if (dnext == 1) { /* pattern analysis (matchChainPos == 0 without chainSwap) */
+            const uint32_t cand = mi - 1;
+            if (repeat == 0) {
+                if (((pattern & 0xFFFF) == (pattern >> 16)) && ((pattern & 0xFF) == (pattern >> 24))) {
+                    repeat = 1;
+                    src_pattern_len = hc_count_pattern(ip + 4, ihigh, pattern) + 4;
+                } else {
+                    repeat = 2;
+                }
+            }
+            if (repeat == 1 && cand >= lowest && hc_protect(HC_START, cand)) {
+                const uint8_t* cp = HCP(c, cand);
+                if (lz4_rd32(cp) == pattern) {
+                    const int64_t fwd = hc_count_pattern(cp + 4, ihigh, pattern) + 4;
+                    int64_t bk = hc_rcount_pattern(cp, c->in, pattern);
+                    {   /* not below lowestMatchIndex */
+                        const uint32_t lo = cand - (uint32_t)bk > lowest ? cand - (uint32_t)bk : lowest;
+                        bk = cand - lo;
+                    }
+                    const int64_t seg = bk + fwd;
+                    if (seg >= src_pattern_len && fwd <= src_pattern_len) {
+                        const uint32_t nmi = cand + (uint32_t)fwd - (uint32_t)src_pattern_len;
+                        mi = hc_protect(HC_START, nmi) ? nmi : HC_START;
+                    } else {
+                        const uint32_t nmi = cand - (uint32_t)bk;
+                        if (!hc_protect(HC_START, nmi)) {
+                            mi = HC_START;
+                        } else {
+                            mi = nmi;
+                            if (look_back == 0) {
+                                const int64_t max_ml = seg < src_pattern_len ? seg : src_pattern_len;
+                                if ((int64_t)longest < max_ml) {
+                                    if ((uint64_t)(ip_idx - mi) > HC_DMAX) break;
+                                    longest = (int)max_ml;
+                                    *matchpos = HCP(c, mi);
+                                    *startpos = ip;
+                                }
+                                const uint32_t dp = c->chain[(uint16_t)mi];
+                                if (dp > mi) break;
+                                mi -= dp;
+                            }
+                        }
+                    }
+                    continue;
+                }
+            }
+        }
+        mi -= c->chain[(uint16_t)mi];
+    }
+    return longest;
+}
+
+/* LZ4HC_encodeSequence */
+static void hc_sequence(const uint8_t** ip, uint8_t** op, const uint8_t** anchor, int ml, const uint8_t* match) {
+    uint8_t* token = (*op)++;
+    size_t len = (size_t)(*ip - *anchor);
+    if (len >= 15) {
+        size_t l = len - 15;
+        *token = 15 << 4;
+        for (; l >= 255; l -= 255) *(*op)++ = 255;
+        *(*op)++ = (uint8_t)l;
+    } else {
+        *token = (uint8_t)(len << 4);
+    }
+    memcpy(*op, *anchor, len);
+    *op += len;
+    const size_t off = (size_t)(*ip - match);
+    *(*op)++ = (uint8_t)off;
+    *(*op)++ = (uint8_t)(off >> 8);
+    len = (size_t)ml - 4;
+    if (len >= 15) {
+        *token += 15;
+        len -= 15;
+        for (; len >= 510; len -= 510) { *(*op)++ = 255; *(*op)++ = 255; }
+        if (len >= 255) { len -= 255; *(*op)++ = 255; }
+        *(*op)++ = (uint8_t)len;
+    } else {
+        *token += (uint8_t)len;
+    }
+    *ip += ml;
+    *anchor = *ip;
+}
+
+int32_t orc_lz4hc_compress(const uint8_t* in, int32_t n, uint8_t* out) {
+    static hc_ctx C;
+    hc_ctx* c = &C;
+    memset(c, 0, sizeof *c);
+    c->in = in;
+    c->next = HC_START;
+    const uint8_t* ip = in;
+    const uint8_t* anchor = ip;
+    const uint8_t* const iend = in + n;
+    const uint8_t* const mflimit = iend - LZ4_MFLIMIT;
+    const uint8_t* const matchlimit = iend - LZ4_LASTLIT;
+    uint8_t* op = out;
+    int ml0, ml, ml2, ml3;
+    const uint8_t *start0, *ref0, *ref = NULL, *start2 = NULL, *ref2 = NULL, *start3 = NULL, *ref3 = NULL;
+    if (n < LZ4_MINLEN) goto last_literals;
+    while (ip <= mflimit) {
+        {   const uint8_t* useless = ip;
+            ml = hc_wider(c, ip, ip, matchlimit, 3, &ref, &useless);  /* LZ4HC_InsertAndFindBestMatch */
+        }
+        if (ml < 4) { ++ip; continue; }
+        start0 = ip; ref0 = ref; ml0 = ml;
+    search2:
+        if (ip + ml <= mflimit) ml2 = hc_wider(c, ip + ml - 2, ip, matchlimit, ml, &ref2, &start2);
+        else ml2 = ml;
+        if (ml2 == ml) {  /* no better match: encode ML1 */
+            hc_sequence(&ip, &op, &anchor, ml, ref);
+            continue;
+        }
+        if (start0 < ip && start2 < ip + ml0) { ip = start0; ref = ref0; ml = ml0; }  /* restore ML1 */
+        if (start2 - ip < 3) {  /* first match too small: removed */
+            ml = ml2; ip = start2; ref = ref2;
+            goto search2;
+        }
+    search3:
+        if (start2 - ip < HC_OPT_ML) {
+            int new_ml = ml;
+            if (new_ml > HC_OPT_ML) new_ml = HC_OPT_ML;
+            if (ip + new_ml > start2 + ml2 - 4) new_ml = (int)(start2 - ip) + ml2 - 4;
+            const int corr = new_ml - (int)(start2 - ip);
+            if (corr > 0) { start2 += corr; ref2 += corr; ml2 -= corr; }
+        }
+        if (start2 + ml2 <= mflimit) ml3 = hc_wider(c, start2 + ml2 - 3, start2, matchlimit, ml2, &ref3, &start3);
+        else ml3 = ml2;
+        if (ml3 == ml2) {  /* no better match: encode ML1 and ML2 */
+            if (start2 < ip + ml) ml = (int)(start2 - ip);
+            hc_sequence(&ip, &op, &anchor, ml, ref);
+            ip = start2;
+            hc_sequence(&ip, &op, &anchor, ml2, ref2);
+            continue;
+        }
+        if (start3 < ip + ml + 3) {  /* not enough space for match 2: remove it */
+            if (start3 >= ip + ml) {  /* Seq1 can be written now; Seq3 becomes Seq1 */
+                if (start2 < ip + ml) {
+                    const int corr = (int)(ip + ml - start2);
+                    start2 += corr; ref2 += corr; ml2 -= corr;
+                    if (ml2 < 4) { start2 = start3; ref2 = ref3; ml2 = ml3; }
+                }
+                hc_sequence(&ip, &op, &anchor, ml, ref);
+                ip = start3; ref = ref3; ml = ml3;
+                start0 = start2; ref0 = ref2; ml0 = ml2;
+                goto search2;
+            }
+            start2 = start3; ref2 = ref3; ml2 = ml3;
+            goto search3;
+        }
+        /* three ascending matches: write ML1 */
+        if (start2 < ip + ml) {
+            if (start2 - ip < HC_OPT_ML) {
+                if (ml > HC_OPT_ML) ml = HC_OPT_ML;
+                if (ip + ml > start2 + ml2 - 4) ml = (int)(start2 - ip) + ml2 - 4;
+                const int corr = ml - (int)(start2 - ip);
+                if (corr > 0) { start2 += corr; ref2 += corr; ml2 -= corr; }
+            } else {
+                ml = (int)(start2 - ip);
+            }
+        }
+        hc_sequence(&ip, &op, &anchor, ml, ref);
+        ip = start2; ref = ref2; ml = ml2;
+        start2 = start3; ref2 = ref3; ml2 = ml3;
+        goto search3;
+    }
+last_literals:;
+    {   const size_t last = (size_t)(iend - anchor);
+        if (last >= 15) {
+            size_t acc = last - 15;
+            *op++ = 15 << 4;
+            for (; acc >= 255; acc -= 255) *op++ = 255;
+            *op++ = (uint8_t)acc;
+        } else {
+            *op++ = (uint8_t)(last << 4);
+        }
+        memcpy(op, anchor, last);
+        op += last;
+    }
+    return (int32_t)(op - out);
+}
+#undef HCP
+
 /* ---- XXHash32 (published XXH32; lz4-java XXHash32 as Lz4XXHash32.java:37-88 calls it) ---- */
 static uint32_t xxh_rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 static uint32_t xxh_le32(const uint8_t* p) {
@@ -1140,8 +1410,12 @@ uint32_t orc_xxhash32(const uint8_t* p, size_t n, uint32_t seed) {
 }
 
 size_t orc_lz4_frame_block(const uint8_t* in, int32_t n, int32_t compression_level, uint8_t* out) {
+    return orc_lz4_frame_block_ex(in, n, compression_level, 0, out);
+}
+
+size_t orc_lz4_frame_block_ex(const uint8_t* in, int32_t n, int32_t compression_level, int32_t high, uint8_t* out) {
     const uint32_t check = orc_xxhash32(in, (size_t)n, 0x9747b28cu) & 0x0FFFFFFFu; /* :250-252 */
-    int32_t clen = orc_lz4_compress(in, n, out + 21);                               /* :259-269 */
+    int32_t clen = high ? orc_lz4hc_compress(in, n, out + 21) : orc_lz4_compress(in, n, out + 21);  /* :259-269 */
     int32_t type = 0x20;
     if (clen >= n) { /* :270-273 */
         type = 0x10;

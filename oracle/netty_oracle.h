@@ -94,6 +94,10 @@ size_t orc_lzf_frame_max_encoded(size_t n);
 int32_t orc_lz4_decompress(const uint8_t* in, int32_t in_len, uint8_t* out, int32_t out_len);
 int32_t orc_lz4_compress(const uint8_t* in, int32_t n, uint8_t* out);
 size_t orc_lz4_max_compressed(size_t n);
+/* LZ4_compress_HC level 9 (lz4-java highCompressor(), Lz4FrameEncoder.java:123-125,161-163): the
+ * hash-chain match finder (256 candidates, pattern analysis) and lazy three-match parse of liblz4's
+ * lz4hc.c.  Pinned against pyarrow's liblz4 Codec('lz4_raw', compression_level=9). */
+int32_t orc_lz4hc_compress(const uint8_t* in, int32_t n, uint8_t* out);
 
 /* XXHash32 (lz4-java 1.8.0 XXHash32.hash, third-party; restated from the published XXH32
  * algorithm: four lane accumulators over 16-byte stripes, then 4-byte and 1-byte tails and the
@@ -105,6 +109,8 @@ uint32_t orc_xxhash32(const uint8_t* p, size_t n, uint32_t seed);
  * LE checksum = XXH32(seed 0x9747b28c) & 0x0FFFFFFF) then the compressed block, or the raw bytes
  * when compression does not shrink them.  n >= 1.  Returns bytes written (<= 21 + max_compressed). */
 size_t orc_lz4_frame_block(const uint8_t* in, int32_t n, int32_t compression_level, uint8_t* out);
+/* The same with the block compressor of Lz4FrameEncoder(highCompressor = high) (:161-163). */
+size_t orc_lz4_frame_block_ex(const uint8_t* in, int32_t n, int32_t compression_level, int32_t high, uint8_t* out);
 
 /* ---- Test data: java.util.Random restatement and the text-like generator ---- */
 void orc_java_random_bytes(int64_t seed, uint8_t* out, size_t n);

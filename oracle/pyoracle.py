@@ -35,6 +35,9 @@ def lib():
         L.orc_lz4_max_compressed.restype = C.c_size_t
         L.orc_lz4_max_compressed.argtypes = [C.c_size_t]
         L.orc_lz4_compress.argtypes = [C.c_char_p, C.c_int32, C.c_void_p]
+        L.orc_lz4hc_compress.argtypes = [C.c_char_p, C.c_int32, C.c_void_p]
+        L.orc_lz4_frame_block_ex.restype = C.c_size_t
+        L.orc_lz4_frame_block_ex.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
         L.orc_lz4_decompress.argtypes = [C.c_char_p, C.c_int32, C.c_void_p, C.c_int32]
         L.orc_crc32c.argtypes = [C.c_char_p, C.c_size_t]
         L.orc_mask_checksum.restype = C.c_uint32
@@ -218,6 +221,14 @@ def lz4_compress(data: bytes) -> bytes:
     return bytes(out[:n])
 
 
+def lz4hc_compress(data: bytes) -> bytes:
+    """LZ4_compress_HC(data, level 9) — lz4-java's highCompressor() (pinned vs pyarrow lz4_raw level 9)."""
+    L = lib()
+    out = _buf(L.orc_lz4_max_compressed(len(data)))
+    n = L.orc_lz4hc_compress(bytes(data), len(data), out)
+    return bytes(out[:n])
+
+
 def lz4_decompress(block: bytes, out_len: int):
     """(status, bytes): NX_OK and out_len bytes, or NX_ERR_LZ4_MALFORMED (-50) and b''."""
     out = _buf(max(out_len, 1))
@@ -247,10 +258,11 @@ def lz4_compression_level(block_size: int) -> int:
     return max(0, (block_size - 1).bit_length() - 10)
 
 
-def lz4_frame_block(data: bytes, level: int = 6) -> bytes:
-    """One Lz4FrameEncoder.flushBufferedData block (header + compressed-or-raw payload)."""
+def lz4_frame_block(data: bytes, level: int = 6, high: bool = False) -> bytes:
+    """One Lz4FrameEncoder.flushBufferedData block (header + compressed-or-raw payload); high selects
+    the highCompressor (Lz4FrameEncoder.java:161-163)."""
     out = _buf(21 + lib().orc_lz4_max_compressed(len(data)))
-    n = lib().orc_lz4_frame_block(bytes(data), len(data), level, out)
+    n = lib().orc_lz4_frame_block_ex(bytes(data), len(data), level, int(bool(high)), out)
     return bytes(out[:n])
 
 
@@ -259,11 +271,11 @@ def lz4_frame_end(level: int = 6) -> bytes:
     return LZ4_MAGIC + bytes([0x10 | level]) + bytes(12)
 
 
-def lz4_frame_encode(data: bytes, block_size: int = 1 << 16, close: bool = True) -> bytes:
+def lz4_frame_encode(data: bytes, block_size: int = 1 << 16, close: bool = True, high: bool = False) -> bytes:
     """Lz4FrameEncoder.encode (:231-244: fill the block buffer, flush each full one) then close()
     (:317-336: flush the rest, append the end block)."""
     level = lz4_compression_level(block_size)
-    out = [lz4_frame_block(data[i:i + block_size], level) for i in range(0, len(data), block_size)]
+    out = [lz4_frame_block(data[i:i + block_size], level, high) for i in range(0, len(data), block_size)]
     return b"".join(out) + (lz4_frame_end(level) if close else b"")
 
 

@@ -80,15 +80,16 @@ def test_lzf_encoder_jobs_equal_sync_and_oracle(nx, oracle, threshold):
             assert o == s.encode(m) == oracle.lzf_frame_encode(m, compress_threshold=threshold)
 
 
-@pytest.mark.parametrize("block_size", [64, 4096, 1 << 16])
-def test_lz4_encoder_jobs_equal_sync(nx, oracle, block_size):
+@pytest.mark.parametrize("block_size,high", [(64, False), (4096, False), (1 << 16, False), (4096, True)])
+def test_lz4_encoder_jobs_equal_sync(nx, oracle, block_size, high):
     """encode / flush / close interleaved over many handles; the bytes equal the synchronous handle's
-    for the same call sequence (its block buffer carried across calls)."""
-    rng = random.Random(block_size)
+    for the same call sequence (its block buffer carried across calls).  high: highCompressor encoders
+    (LZ4_compress_HC blocks, launched apart from the fast ones)."""
+    rng = random.Random(block_size + high)
     b = nx.Batcher()
     chans, ops = [], []
     for c in range(16):
-        e = nx.Lz4FrameEncoder(block_size)
+        e = nx.Lz4FrameEncoder(block_size, high_compressor=high and c % 2 == 0)
         msgs = _msgs(oracle, rng, rng.randint(2, 6))
         op = [rng.choice((0, 0, 0, 1)) for _ in msgs]
         op[-1] = rng.choice((1, 2))
@@ -100,8 +101,8 @@ def test_lz4_encoder_jobs_equal_sync(nx, oracle, block_size):
         chans.append((lambda m, e=e, it=it: b.submit_encode(e, m, op=next(it)), msgs))
         ops.append(op)
     got = _run_jobs(b, chans)
-    for (_, msgs), op, outs in zip(chans, ops, got):
-        s = nx.Lz4FrameEncoder(block_size)
+    for c, ((_, msgs), op, outs) in enumerate(zip(chans, ops, got)):
+        s = nx.Lz4FrameEncoder(block_size, high_compressor=high and c % 2 == 0)
         for m, k, o in zip(msgs, op, outs):
             want = s.encode(m)
             if k == 1:

@@ -69,7 +69,7 @@ def _damage(rng, blk: bytes) -> bytes:
 def test_snappy_decode_fuzz(dev, B, oracle):
     rng = random.Random(101)
     cases = [_damage(rng, oracle.snappy_encode(p)) for p in _payloads(oracle, rng, N_PER_CODEC)]
-    for variant in ("auto", "fused"):
+    for variant in ("auto", "pair", "fused"):
         inp, off, ln = B.pack(cases, dev)
         out, ooff = B.out_slots([65536] * len(cases), dev)
         r = B.snappy_decode(inp, off, ln, out, ooff, consumed=True, variant=variant)

@@ -348,3 +348,17 @@ def test_lz4_block_size_and_flush(nx, oracle):
     assert comp == want
     assert b"".join(nx.Lz4FrameDecoder(True).channel_read(comp)) == data
     assert enc.encode(b"raw after close") == b"raw after close"
+
+
+def test_lzf_encoder_total_length_argument(nx, oracle):
+    """LzfEncoder(totalLength, compressThreshold) (LzfEncoder.java:127-166): totalLength outside
+    16..65535 is refused with the reference's message (:147-150); inside it the output is the default
+    encoder's (the non-allocating ChunkEncoder sizes its table from max(totalLength, MAX_CHUNK_LEN))."""
+    for bad in (15, 65536, -1):
+        with pytest.raises(ValueError, match=f"totalLength: {bad} \\(expected: 16-65535\\)"):
+            nx.LzfEncoder(total_length=bad)
+    msgs = [oracle.textgen_chunk(i, n) for i, n in enumerate((20, 100, 5000, 70000))]
+    for tl in (16, 100, 4096, 65535):
+        e, ref = nx.LzfEncoder(total_length=tl), nx.LzfEncoder()
+        for m in msgs:
+            assert e.encode(m) == ref.encode(m) == oracle.lzf_frame_encode(m)

@@ -100,3 +100,48 @@ def test_lz4_encode_parity_and_roundtrip(dev, B, oracle, align):
         assert blocks[i] == oracle.lz4_compress(d), i
     st2, outs = _run(B, dev, blocks, [len(d) for d in data], align)
     assert st2 == [0] * len(data) and outs == list(data)
+
+
+def _hc_corpus(oracle):
+    rng = random.Random(13)
+    data = [b"", b"a", b"hello", b"abcdabcdabcda", bytes(100), bytes(range(256)) * 3, b"x" * 5000, b"ab" * 3000,
+            b"abc" * 2000, b"abcd" * 2000, (b"q" * 300 + b"rs" * 100 + oracle.textgen_chunk(3, 500)) * 6]
+    for n in (13, 17, 64, 1000, 4096, 30000, 65536):
+        data.append(oracle.textgen_chunk(900 + n, n))
+        data.append(bytes(rng.getrandbits(8) for _ in range(min(n, 2000))))
+    data += [bytes((i % p) * 29 & 0xFF for i in range(12000)) for p in (1, 2, 3, 5, 64)]
+    data.append(oracle.textgen_chunk(77, 150000))  # > 64 KiB: the chain table wraps, 65535-distance limit
+    return data
+
+
+@pytest.mark.parametrize("align", [16, 1])
+def test_lz4hc_encode_parity_and_roundtrip(dev, B, oracle, align):
+    """Lz4FrameEncoder(highCompressor = true)'s block compressor (LZ4_compress_HC level 9): GPU bytes ==
+    the oracle's restatement (itself byte-equal to liblz4 at level 9), and the blocks decode back."""
+    data = _hc_corpus(oracle)
+    inp, off, ln = B.pack(data, dev, align=align)
+    cap = [B.lz4_max_compressed_length(len(d)) for d in data]
+    out, ooff = B.out_slots(cap, dev, align=align)
+    olen, st = B.lz4_encode(inp, off, ln, out, ooff, high=True)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [0] * len(data)
+    outh, oo, ol = out.cpu().numpy().tobytes(), ooff.cpu().tolist(), olen.cpu().tolist()
+    blocks = [outh[o:o + n] for o, n in zip(oo, ol)]
+    for i, d in enumerate(data):
+        assert blocks[i] == oracle.lz4hc_compress(d), i
+    st2, outs = _run(B, dev, blocks, [len(d) for d in data], align)
+    assert st2 == [0] * len(data) and outs == list(data)
+
+
+def test_lz4hc_repeated_launches_reuse_tables(dev, B, oracle):
+    """A lane's tables carry the earlier blocks' entries (no clearing between blocks: each block gets
+    a higher index base); 20 launches over the same lanes give the fresh-context bytes every time."""
+    data = [oracle.textgen_chunk(40 + i, 20000 + 531 * i) for i in range(6)]
+    want = [oracle.lz4hc_compress(d) for d in data]
+    inp, off, ln = B.pack(data, dev)
+    out, ooff = B.out_slots([B.lz4_max_compressed_length(len(d)) for d in data], dev)
+    for r in range(20):
+        olen, st = B.lz4_encode(inp, off, ln, out, ooff, high=True)
+        torch.cuda.synchronize()
+        outh, oo, ol = out.cpu().numpy().tobytes(), ooff.cpu().tolist(), olen.cpu().tolist()
+        assert [outh[o:o + n] for o, n in zip(oo, ol)] == want, r

@@ -224,3 +224,59 @@ def test_lz4_frame_encoder_large_block_size(dev, oracle, block_size):
     comp = enc.encode(data) + enc.finish_encode()
     assert comp == oracle.lz4_frame_encode(data, block_size=block_size)
     assert b"".join(nx.Lz4FrameDecoder(True).channel_read(comp)) == data
+
+
+def test_lz4_frame_encode_parity_high_compressor(dev, B, oracle):
+    """nx_lz4_frame_encode_batch_ex with highCompressor: header + LZ4_compress_HC block (or raw when not
+    smaller), as Lz4FrameEncoder(highCompressor = true).flushBufferedData writes them."""
+    data = [b"Netty", oracle.textgen_chunk(3, 65536), oracle.java_random_bytes(4, 5000), bytes(3000), oracle.textgen_chunk(8, 777)]
+    inp, off, ln = B.pack(data, dev)
+    out, ooff = B.out_slots([21 + B.lz4_max_compressed_length(len(d)) for d in data], dev)
+    olen, st = B.lz4_frame_encode(inp, off, ln, out, ooff, 6, high=True)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [0] * len(data)
+    outh, oo, ol = out.cpu().numpy().tobytes(), ooff.cpu().tolist(), olen.cpu().tolist()
+    for i, d in enumerate(data):
+        assert outh[oo[i]:oo[i] + ol[i]] == oracle.lz4_frame_block(d, 6, high=True), i
+
+
+@pytest.mark.parametrize("block_size", [4096, 1 << 16])
+def test_lz4_frame_encoder_high_compressor(dev, oracle, block_size):
+    """Lz4FrameEncoder(highCompressor = true) through the handle: the oracle's frame bytes (HC blocks),
+    smaller than the fast compressor's on text, and the stream decodes."""
+    import netty_amd as nx
+    data = oracle.textgen_chunk(72, 3 * block_size + 999) + oracle.java_random_bytes(2, 3000)
+    enc = nx.Lz4FrameEncoder(block_size, high_compressor=True)
+    comp = enc.encode(data[:5000]) + enc.encode(data[5000:]) + enc.finish_encode()
+    assert comp == oracle.lz4_frame_encode(data, block_size=block_size, high=True)
+    assert len(comp) < len(oracle.lz4_frame_encode(data, block_size=block_size))
+    assert b"".join(nx.Lz4FrameDecoder(True).channel_read(comp)) == data
+
+
+def test_lz4_frame_encoder_max_encode_size(dev, oracle):
+    """maxEncodeSize (Lz4FrameEncoder.java:150-170, allocateBuffer :190-214): encode and flush refuse
+    pending bytes whose worst-case output exceeds it with the reference's EncoderException message,
+    changing nothing; finishEncode does not check (:306-315); maxEncodeSize <= 0 is refused (:168)."""
+    import netty_amd as nx
+    from netty_amd.handlers import EncoderException
+    with pytest.raises(ValueError, match="maxEncodeSize : 0"):
+        nx.Lz4FrameEncoder(4096, max_encode_size=0)
+    bound = lambda n: n + n // 255 + 16 + 21  # compressor.maxCompressedLength + HEADER_LENGTH
+    limit = 2 * bound(4096) + 100
+    enc = nx.Lz4FrameEncoder(4096, max_encode_size=limit)
+    ref = nx.Lz4FrameEncoder(4096)
+    data = oracle.textgen_chunk(5, 20000)
+    assert enc.encode(data[:3000]) == ref.encode(data[:3000]) == b""  # 3000 pending: one block's bound
+    want = bound(4096) * 2 + bound(3000 + 8000 - 8192)
+    with pytest.raises(EncoderException) as ei:
+        enc.encode(data[3000:11000])  # 11000 pending: three blocks
+    assert str(ei.value) == (f"requested encode buffer size ({want} bytes) exceeds the maximum "
+                             f"allowable size ({limit} bytes)")
+    # the refused call changed nothing: the same calls then give the unlimited encoder's bytes
+    assert enc.encode(data[3000:8000]) == ref.encode(data[3000:8000]) != b""
+    assert enc.flush() == ref.flush()
+    assert enc.finish_encode() == ref.finish_encode()
+    tight = nx.Lz4FrameEncoder(4096, max_encode_size=bound(100) - 1)
+    with pytest.raises(EncoderException):
+        tight.encode(b"x" * 100)  # even a message that only fills the buffer is sized first
+    assert tight.encode(b"x" * 50) == b""

@@ -67,7 +67,7 @@ def test_snappy_encode_parity(dev, B, oracle, kat, in_align, out_align):
         assert got == want, (i, len(c))
 
 
-@pytest.mark.parametrize("variant,align", [("auto", 16), ("auto", 1), ("fused", 16), ("fused", 1), ("naive", 16)])
+@pytest.mark.parametrize("variant,align", [("auto", 16), ("pair", 16), ("pair", 1), ("fused", 16), ("fused", 1), ("naive", 16)])
 def test_snappy_decode_parity(dev, B, oracle, kat, naive_decode, variant, align):
     chunks = _corpus(oracle, kat)
     enc = [oracle.snappy_encode(c) for c in chunks]
@@ -112,7 +112,7 @@ def _crafted_streams(oracle, kat):
     return cases
 
 
-@pytest.mark.parametrize("variant", ["auto", "fused", "naive"])
+@pytest.mark.parametrize("variant", ["auto", "pair", "fused", "naive"])
 def test_snappy_decode_edge_cases(dev, B, oracle, kat, naive_decode, variant):
     cases = _crafted_streams(oracle, kat)
     inp, off, ln = B.pack(cases, dev)

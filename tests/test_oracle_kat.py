@@ -406,6 +406,25 @@ def test_lz4_compress_equals_liblz4(oracle):
         assert oracle.lz4_decompress(oracle.lz4_compress(data), len(data)) == (0, data), name
 
 
+def test_lz4hc_compress_equals_liblz4_level9(oracle):
+    """Lz4FrameEncoder(highCompressor = true) compresses with lz4-java's highCompressor(), liblz4's
+    LZ4_compress_HC at its default level 9 (Lz4FrameEncoder.java:123-125,161-163): the oracle's
+    restatement of the hash-chain match finder (256 candidates, pattern analysis) and the lazy
+    three-match parse is byte-for-byte equal to pyarrow's bundled liblz4 at compression_level=9 on the
+    LZ4 corpus (text, random, runs, short periods, every end-of-block limit) plus repeated 1-, 2-, 3-
+    and 4-byte patterns that drive the pattern analysis, and round-trips through the decoder."""
+    pa = pytest.importorskip("pyarrow")
+    z = pa.Codec("lz4_raw", compression_level=9)
+    corpus = _lz4_corpus(oracle)
+    corpus.update({"run_a": b"a" * 5000, "period2": b"ab" * 5000, "period3": b"abc" * 4000, "period4": b"abcd" * 4000,
+                   "runs_mixed": (b"x" * 300 + b"yz" * 200 + oracle.textgen_chunk(9, 777)) * 20,
+                   "period5_200k": bytes((i % 5) for i in range(200000))})
+    for name, data in corpus.items():
+        hc = oracle.lz4hc_compress(data)
+        assert hc == z.compress(data).to_pybytes(), name
+        assert oracle.lz4_decompress(hc, len(data)) == (0, data), name
+
+
 def test_snappy_blocks_decode_with_libsnappy(oracle, kat):
     """Independent decode cross-check: pyarrow's bundled libsnappy decodes every
     Netty-format block the oracle encodes (Netty's encoder output differs from libsnappy's, so this
