@@ -37,7 +37,7 @@ CHUNK = 65536
 CONFIG5_CHUNKS = 1638400  # 100 GiB of 64 KiB chunks
 # kernels whose PMC traffic backs roofline.traffic; the summary must have been taken on these sources
 PMC_SOURCES = ("netty_amd/csrc/snappy_encode.hip", "netty_amd/csrc/snappy_decode.hip", "netty_amd/csrc/crc32c.hip",
-               "netty_amd/csrc/nx_common.hpp")
+               "netty_amd/csrc/nx_common.hpp", "netty_amd/csrc/expand_units.hpp")
 
 
 def parse(argv=None):
@@ -61,6 +61,8 @@ def parse(argv=None):
     ap.add_argument("--no-alt", action="store_true", help="skip the FastLZ/LZF/LZ4 (configs[3]) measurement")
     ap.add_argument("--no-probe-ceiling", action="store_true", help="skip the live random-access ceiling of the encoder")
     ap.add_argument("--alt-chunks", type=int, default=262144)
+    ap.add_argument("--hc-chunks", type=int, default=1024, help="chunks of the LZ4 HC (highCompressor) leg (0 = skip)")
+    ap.add_argument("--no-latency", action="store_true", help="skip the per-batch-size latency leg")
     ap.add_argument("--no-frame-scan", action="store_true", help="skip the framed-stream (§8f row 1) measurement")
     ap.add_argument("--scan-chunks", type=int, default=131072, help="chunks laid out as framed streams")
     ap.add_argument("--scan-per-stream", type=int, default=64, help="chunks per stream (one cumulation each)")
@@ -419,7 +421,7 @@ def encoder_placement():
             "probe_ms": [round(ms[k], 3) for k in range(n.value)], "pick": pick.value}
 
 
-DEC_KERNELS = ["nx::dec::k_parse", "nx::dec::k_expand"]
+DEC_KERNELS = ["nx::dec::k_parse", "nx::dec::k_expand_u"]  # k_expand (NX_EXPANDER=pieces) for A/B runs only
 
 
 def timed_legs(torch, leg, steps, warmup, sync, S, dev, cdev=None):
@@ -564,7 +566,10 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
         if want_ceiling:  # with the job's buffers freed, the ceiling can draw as many placements as the encoder
             fill_random_access()
         if not args.no_alt:
-            line["alt_codecs"] = bench_alt_codecs(torch, B, dev, args.alt_chunks)
+            line["alt_codecs"] = bench_alt_codecs(torch, B, dev, args.alt_chunks, hc_n=args.hc_chunks)
+            torch.cuda.empty_cache()
+        if not args.no_latency:
+            line["latency"] = bench_latency(torch, B, dev)
             torch.cuda.empty_cache()
         if not args.no_e2e:
             # host memory in, host memory out, through the C-ABI a JNI caller binds (never `value`)
@@ -675,7 +680,41 @@ def bench_frame_scan(torch, B, dev, leg, m: int, per_stream: int, reps: int = 3)
     ok = (cnt == [m, 0, m] and int((r["status"] != 0).sum()) == 0 and bool(torch.equal(r["consumed"], slen))
           and int((d["status"] != 0).sum()) == 0 and bool(torch.equal(dec[:m * CHUNK], src[:m * CHUNK])))
     ts, ta = min(t_scan), min(t_all)
-    return {"streams": ns, "chunks_per_stream": per_stream, "chunks": m, "framed_bytes": total,
+    # §8f row 1 follow-up: the first streams up to 1 GiB as ONE cumulation (their stream identifiers
+    # in between are legal chunks): the lane walk (one lane, ~35 K dependent header loads) against the
+    # segmented walk (nx_snappy_frame_scan_long); both lists must be equal
+    kk = max(1, int((ends <= (1 << 30)).sum().item()))
+    L1, m1 = int(ends[kk - 1].item()), kk * per_stream
+    st1 = torch.zeros(1, dtype=torch.int32, device=dev)
+    zero = torch.zeros(1, dtype=torch.int64, device=dev)
+    lens = torch.tensor([L1], dtype=torch.int64, device=dev)
+
+    def best(fn):
+        fn()
+        torch.cuda.synchronize()
+        tt = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st1.zero_()
+            a.record()
+            box["r"] = fn()
+            b.record()
+            torch.cuda.synchronize()
+            tt.append(a.elapsed_time(b))
+        return min(tt)
+
+    box = {}
+    t_lane = best(lambda: B.snappy_frame_scan(buf, zero, lens, st1, m1))
+    rl = box["r"]
+    t_long = best(lambda: B.snappy_frame_scan_long(buf, L1, st1, m1))
+    rg = box["r"]
+    same = all(bool(torch.equal(rl[k][:m1], rg[k][:m1])) for k in ("data_off", "data_len", "masked_crc", "seq"))
+    long_ok = (same and rg["counts"].tolist() == [m1, 0, m1] and int(rg["consumed"].item()) == L1 and int(rg["status"].item()) == 0)
+    ok = ok and long_ok
+    long_res = {"bytes": L1, "chunks": m1, "lane_walk_ms": round(t_lane, 3), "segmented_walk_ms": round(t_long, 3),
+                "speedup": round(t_lane / t_long, 1), "verified": long_ok,
+                "note": "one cumulation; the segmented walk's list equals the lane walk's"}
+    return {"streams": ns, "chunks_per_stream": per_stream, "chunks": m, "framed_bytes": total, "long_stream": long_res,
             "scan_ms": round(ts, 3), "scan_chunks_per_s": round(m / (ts / 1e3)),
             "scan_decode_ms": round(ta, 3), "framed_decode_gib_s": round(m * CHUNK / (ta / 1e3) / 2**30, 2),
             "note": "scan = one lane per stream walking its chunk headers (it reads the 8-byte headers only, "
@@ -684,7 +723,7 @@ def bench_frame_scan(torch, B, dev, leg, m: int, per_stream: int, reps: int = 3)
             "verified": ok}
 
 
-def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2):
+def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2, hc_n: int = 1024):
     """configs[3]: FastLZ (level 1 and 2) and LZF encode/decode of a mixed batch — sizes uniform in
     [4096, 65535], half text-like, half random — device-resident.  GiB/s of uncompressed bytes."""
     g = torch.Generator(device=dev).manual_seed(1234)
@@ -807,6 +846,29 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2):
     res["lz4"] = {"encode_gib_s": round(U / te * 1e3 / 2**30, 3), "decode_gib_s": round(U / td * 1e3 / 2**30, 3),
                   "ratio": round(Cz / U, 4), "verified": ok,
                   "roofline_encode": roof(U + Cz, te), "roofline_decode": roof(U + Cz, td)}
+    # LZ4 HC (Lz4FrameEncoder(highCompressor = true): LZ4_compress_HC level 9, one lane per block with
+    # 256 KiB of hash/chain tables in HBM) on the first hc_n chunks of the same mix; decoded back
+    hn = min(n, hc_n)
+    if hn:
+        Uh = int(ln[:hn].to(torch.int64).sum())
+
+        def henc():
+            box["h"] = B.lz4_encode(src, off[:hn], ln[:hn], zout, zoff[:hn], high=True)
+
+        th = timed(henc)
+        hlen, hst = box["h"]
+
+        def hdec():
+            box["hd"] = B.lz4_decode(zout, zoff[:hn], hlen, dec, off[:hn], ln[:hn])
+
+        dec.zero_()
+        thd = timed(hdec)
+        ok = (int((hst != 0).sum()) == 0 and int((box["hd"] != 0).sum()) == 0 and same(torch.arange(hn, device=dev), ln[:hn]))
+        Ch = int(hlen.to(torch.int64).sum())
+        res["lz4_hc"] = {"chunks": hn, "encode_gib_s": round(Uh / th * 1e3 / 2**30, 4), "encode_ms": round(th, 2),
+                         "decode_gib_s": round(Uh / thd * 1e3 / 2**30, 3), "ratio": round(Ch / Uh, 4), "verified": ok,
+                         "roofline_encode": roof(Uh + Ch, th), "roofline_decode": roof(Uh + Ch, thd),
+                         "note": "LZ4_compress_HC level 9 (256-candidate hash chains) per lane: a compatibility path"}
     del zout
     # LZ4 frame (Lz4FrameEncoder / Lz4FrameDecoder with validateChecksums): XXH32, frame blocks into
     # slots, gathered into 4096 contiguous streams (64 blocks each), then device scan -> block decode -> XXH32 verify.
@@ -848,6 +910,55 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2):
                         "non_compressed_blocks": nu, "verified": ok,
                         "note": "decode leg = scan + LZ4 block decode + XXH32 of every block vs its header (one host sync for the list counts)"}
     return res
+
+
+def bench_latency(torch, B, dev, sizes=(1, 64, 1024, 16384), reps: int = 3):
+    """Per-batch latency of the Snappy encode (+ CRC32C) and decode (+ verify) batch calls, as a
+    handler call or a batcher flush of that many 64 KiB text chunks sees it: best of `reps` HIP-event
+    timings on the current stream, outputs checked against the sources."""
+    nmax = max(sizes)
+    src = torch.empty(nmax * CHUNK, dtype=torch.uint8, device=dev)
+    B.textgen(src, 0, nmax, CHUNK)
+    cap = (B.snappy_max_compressed_length(CHUNK) + 15) // 16 * 16
+    enc = torch.empty(nmax * cap, dtype=torch.uint8, device=dev)
+    dec = torch.empty(nmax * CHUNK, dtype=torch.uint8, device=dev)
+    rows = []
+
+    def best(fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        return min(ts)
+
+    for m in sizes:
+        off = torch.arange(m, dtype=torch.int64, device=dev) * CHUNK
+        ln = torch.full((m,), CHUNK, dtype=torch.int32, device=dev)
+        eoff = torch.arange(m, dtype=torch.int64, device=dev) * cap
+        box = {}
+
+        def e():
+            box["crc"] = B.crc32c_masked(src, off, ln)
+            box["e"] = B.snappy_encode(src, off, ln, enc, eoff)
+
+        te = best(e)
+        elen, est = box["e"]
+
+        def d():
+            box["d"] = B.snappy_decode(enc, eoff, elen, dec, off, expected_crc=box["crc"])
+
+        td = best(d)
+        ok = (int((est != 0).sum()) == 0 and int((box["d"]["status"] != 0).sum()) == 0
+              and torch.equal(dec[:m * CHUNK], src[:m * CHUNK]))
+        rows.append({"chunks": m, "encode_ms": round(te, 3), "decode_verify_ms": round(td, 3), "verified": ok})
+    return {"sizes": rows, "note": "one nx_crc32c_masked_batch + nx_snappy_encode_batch call, and one nx_snappy_decode_batch "
+                                   "call with CRC verify (fused decoder up to 32768 frames), per batch of 64 KiB text chunks"}
 
 
 # ---------------------------------------------------------------------------------------- launcher

@@ -139,6 +139,18 @@ int32_t nx_snappy_frame_scan_batch(const uint8_t* in, const uint64_t* in_off, co
                                    uint32_t* chunk_stream, uint32_t* chunk_seq, uint32_t* counts,
                                    uint32_t cap, uint32_t n, void* stream);
 
+/* The same walk for ONE long cumulation in[0, len) whose length the caller holds on the host (a
+ * ByteBuf's readableBytes): outputs as nx_snappy_frame_scan_batch with n = 1 (chunk_stream 0).  The
+ * cumulation is cut into 1 MiB segments (more when it exceeds 1 GiB); a wave per segment guesses
+ * where the chain enters it (four consecutive plausible data-chunk headers), a lane per segment walks
+ * it with the decoder's exact semantics, one workgroup stitches the true chain (re-walking any
+ * segment whose guess was wrong) and a lane per segment writes its entries: the result equals the
+ * serial walk's whatever the guesses.  A 1 GiB stream takes well under a millisecond where one lane
+ * needs ~35 K dependent header loads.  Asynchronous on `stream`. */
+int32_t nx_snappy_frame_scan_long(const uint8_t* in, uint64_t len, uint32_t* state, uint64_t* consumed, int32_t* status,
+                                  uint64_t* data_off, uint32_t* data_len, uint32_t* masked_crc, uint32_t* chunk_stream,
+                                  uint32_t* chunk_seq, uint32_t* counts, uint32_t cap, void* stream);
+
 /* Replaces Snappy.calculateChecksum(ByteBuf, off, len)  Snappy.java:668-676
  * (Crc32c.java:105-124 + maskChecksum :720-722).  masked_out[i] = mask(crc32c(chunk i)). */
 int32_t nx_crc32c_masked_batch(const uint8_t* in, const uint64_t* off, const uint32_t* len,

@@ -39,6 +39,7 @@ _SIGS = {
     "nx_snappy_decode_batch_pair": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_crc32c_masked_batch": (i32, [vp, vp, vp, vp, u32, vp]),
     "nx_snappy_frame_scan_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, vp]),
+    "nx_snappy_frame_scan_long": (i32, [vp, C.c_uint64, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_fastlz_compress_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_fastlz_decompress_batch": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
     "nx_adler32_batch": (i32, [vp, vp, vp, vp, u32, vp]),

@@ -110,6 +110,27 @@ def snappy_frame_scan(inp, in_off, in_len, state, cap: int):
     return r
 
 
+def snappy_frame_scan_long(inp, length: int, state, cap: int, offset: int = 0):
+    """The segmented walk of ONE long cumulation inp[offset, offset + length) (nx_snappy_frame_scan_long);
+    state: a one-element int32 tensor, updated in place.  Same result dict as snappy_frame_scan with
+    n = 1 (data_off relative to inp[offset])."""
+    dev = inp.device
+    c = max(int(cap), 1)
+    r = {"consumed": torch.empty(1, dtype=torch.int64, device=dev),
+         "status": torch.empty(1, dtype=torch.int32, device=dev),
+         "data_off": torch.empty(c, dtype=torch.int64, device=dev),
+         "data_len": torch.empty(c, dtype=torch.int32, device=dev),
+         "masked_crc": torch.empty(c, dtype=torch.int32, device=dev),
+         "stream": torch.empty(c, dtype=torch.int32, device=dev),
+         "seq": torch.empty(c, dtype=torch.int32, device=dev),
+         "counts": torch.empty(3, dtype=torch.int32, device=dev)}
+    _chk(_lib.load().nx_snappy_frame_scan_long(_ptr(inp) + int(offset), int(length), _ptr(state), _ptr(r["consumed"]),
+                                               _ptr(r["status"]), _ptr(r["data_off"]), _ptr(r["data_len"]),
+                                               _ptr(r["masked_crc"]), _ptr(r["stream"]), _ptr(r["seq"]), _ptr(r["counts"]),
+                                               int(cap), _stream()), "nx_snappy_frame_scan_long")
+    return r
+
+
 def crc32c_masked(inp, off, length, out=None):
     """Snappy.calculateChecksum per chunk (Snappy.java:668-676)."""
     n = length.numel()

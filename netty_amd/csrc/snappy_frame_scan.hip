@@ -19,6 +19,8 @@
 // [cap - counts[1], cap).  Entries are claimed with atomics, so their order across streams is not
 // fixed; chunk_stream / chunk_seq give each entry's stream and its position among that stream's
 // data chunks.
+#include <stdlib.h>
+#include <vector>
 #include "nx_common.hpp"
 #include "../../include/netty_amd.h"
 
@@ -29,6 +31,119 @@ __device__ __forceinline__ uint32_t le32(const uint8_t* p) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// The chunk walk of SnappyFrameDecoder.decode (:85-231) from position w.p up to the first header at
+// or after `stop` (or the end of the readable bytes, an error, or a list entry refused by `emit`).
+// emit(type, header_pos, chunkLength, stored_crc) lists a data chunk and returns false when the list
+// cannot take it (the walk then stops before the chunk).  k_frame_scan walks a whole cumulation with
+// it; the segmented long-stream path below walks 1 MiB segments with it.
+enum WalkEnd : uint32_t { kOpen = 0, kEnd = 1, kError = 2, kFull = 3 };
+struct Walk {
+    uint64_t p;
+    uint64_t skip;  // numBytesToSkip (< 2^24: a chunk length)
+    bool started;
+    int32_t res;
+};
+template <class Emit>
+__device__ WalkEnd walk(const uint8_t* __restrict__ b, uint64_t len, Walk& w, uint64_t stop, Emit&& emit) {
+    uint64_t p = w.p, skip = w.skip;
+    bool started = w.started;
+    int32_t res = NX_OK;
+    WalkEnd how = kEnd;
+    while (p < len) {
+        if (skip) {  // :91-99
+            const uint64_t k = skip < len - p ? skip : len - p;
+            p += k;
+            skip -= k;
+            continue;
+        }
+        if (p >= stop) {
+            how = kOpen;
+            break;
+        }
+        const uint64_t avail = len - p;
+        if (avail < 4) break;  // :104-108
+        const uint32_t type = b[p];
+        const uint32_t clen = (uint32_t)b[p + 1] | ((uint32_t)b[p + 2] << 8) | ((uint32_t)b[p + 3] << 16);
+        if (type == 0xFFu) {  // STREAM_IDENTIFIER :115-136
+            if (clen != 6u) {
+                res = NX_ERR_SNAPPY_STREAM_ID_LENGTH;
+                break;
+            }
+            if (avail < 10) break;
+            const uint8_t* q = b + p + 4;
+            p += 10;  // skipBytes(4 + 6) precede the content check (:124-133)
+            if (q[0] != 's' || q[1] != 'N' || q[2] != 'a' || q[3] != 'P' || q[4] != 'p' || q[5] != 'Y') {
+                res = NX_ERR_SNAPPY_STREAM_ID_CONTENT;
+                break;
+            }
+            started = true;
+            continue;
+        }
+        if (type & 0x80u) {  // RESERVED_SKIPPABLE :137-151
+            if (!started) {
+                res = NX_ERR_SNAPPY_SKIPPABLE_BEFORE_ID;
+                break;
+            }
+            p += 4;
+            const uint64_t k = clen < len - p ? (uint64_t)clen : len - p;
+            p += k;
+            skip = clen - k;
+            continue;
+        }
+        if (type > 1u) {  // RESERVED_UNSKIPPABLE :152-157
+            res = NX_ERR_SNAPPY_UNSKIPPABLE;
+            break;
+        }
+        if (!started) {  // :159-161, :181-183
+            res = type ? NX_ERR_SNAPPY_UNCOMPRESSED_BEFORE_ID : NX_ERR_SNAPPY_COMPRESSED_BEFORE_ID;
+            break;
+        }
+        if (type == 1u && clen > 65536u + 4u) {  // :162-165
+            res = NX_ERR_SNAPPY_UNCOMPRESSED_TOO_LARGE;
+            break;
+        }
+        if (avail < 4ull + clen) break;  // :167-169, :190-192
+        if (clen < 4u) {  // the 4-byte checksum does not fit the chunk
+            res = NX_ERR_SNAPPY_CHUNK_TOO_SHORT;
+            break;
+        }
+        if (type == 0u) {
+            // snappy.getPreamble(in) reads the varint from the cumulation, not the chunk
+            // (Snappy.java:404-441), then :197-201 bounds it.
+            uint32_t ulen = 0;
+            bool complete = false;
+            for (uint32_t i = 0; i < 4u && p + 8 + i < len; ++i) {
+                const uint32_t c = b[p + 8 + i];
+                ulen |= (c & 0x7Fu) << (7u * i);
+                if (!(c & 0x80u)) {
+                    complete = true;
+                    break;
+                }
+                if (i == 3u) res = NX_ERR_SNAPPY_PREAMBLE_TOO_LONG;
+            }
+            if (res) break;
+            if (!complete) ulen = 0;
+            if (ulen > 65536u) {
+                res = NX_ERR_SNAPPY_DECOMPRESSED_TOO_LARGE;
+                break;
+            }
+        }
+        if (!emit(type, p, clen, le32(b + p + 4))) {  // a full list stops the stream before this chunk
+            res = NX_SCAN_LIST_FULL;
+            how = kFull;
+            break;
+        }
+        p += 4ull + clen;
+    }
+    if (res < 0) how = kError;
+    w.p = p;
+    w.skip = skip;
+    w.started = started;
+    w.res = res;
+    return how;
+}
+
+// One lane per cumulation.
 __global__ void __launch_bounds__(256) k_frame_scan(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                     const uint64_t* __restrict__ in_len, uint32_t* __restrict__ state,
                                                     uint64_t* __restrict__ consumed, int32_t* __restrict__ status,
@@ -42,108 +157,275 @@ __global__ void __launch_bounds__(256) k_frame_scan(const uint8_t* __restrict__ 
     const uint8_t* b = in + base;
     const uint64_t len = in_len[s];
     const uint32_t st = state[s];
-    bool started = st & 1u;
     bool corrupted = (st >> 1) & 1u;
-    uint64_t skip = st >> 8;  // numBytesToSkip (< 2^24: a chunk length)
-    uint64_t p = 0;
-    int32_t res = NX_OK;
+    Walk w{0, st >> 8, (st & 1u) != 0, NX_OK};
     uint32_t seq = 0;
     if (corrupted) {  // :86-89 — everything readable is discarded
-        p = len;
+        w.p = len;
     } else {
-        while (p < len) {
-            if (skip) {  // :91-99
-                const uint64_t k = skip < len - p ? skip : len - p;
-                p += k;
-                skip -= k;
-                continue;
-            }
-            const uint64_t avail = len - p;
-            if (avail < 4) break;  // :104-108
-            const uint32_t type = b[p];
-            const uint32_t clen = (uint32_t)b[p + 1] | ((uint32_t)b[p + 2] << 8) | ((uint32_t)b[p + 3] << 16);
-            if (type == 0xFFu) {  // STREAM_IDENTIFIER :115-136
-                if (clen != 6u) {
-                    res = NX_ERR_SNAPPY_STREAM_ID_LENGTH;
-                    break;
-                }
-                if (avail < 10) break;
-                const uint8_t* q = b + p + 4;
-                p += 10;  // skipBytes(4 + 6) precede the content check (:124-133)
-                if (q[0] != 's' || q[1] != 'N' || q[2] != 'a' || q[3] != 'P' || q[4] != 'p' || q[5] != 'Y') {
-                    res = NX_ERR_SNAPPY_STREAM_ID_CONTENT;
-                    break;
-                }
-                started = true;
-                continue;
-            }
-            if (type & 0x80u) {  // RESERVED_SKIPPABLE :137-151
-                if (!started) {
-                    res = NX_ERR_SNAPPY_SKIPPABLE_BEFORE_ID;
-                    break;
-                }
-                p += 4;
-                const uint64_t k = clen < len - p ? (uint64_t)clen : len - p;
-                p += k;
-                skip = clen - k;
-                continue;
-            }
-            if (type > 1u) {  // RESERVED_UNSKIPPABLE :152-157
-                res = NX_ERR_SNAPPY_UNSKIPPABLE;
-                break;
-            }
-            if (!started) {  // :159-161, :181-183
-                res = type ? NX_ERR_SNAPPY_UNCOMPRESSED_BEFORE_ID : NX_ERR_SNAPPY_COMPRESSED_BEFORE_ID;
-                break;
-            }
-            if (type == 1u && clen > 65536u + 4u) {  // :162-165
-                res = NX_ERR_SNAPPY_UNCOMPRESSED_TOO_LARGE;
-                break;
-            }
-            if (avail < 4ull + clen) break;  // :167-169, :190-192
-            if (clen < 4u) {  // the 4-byte checksum does not fit the chunk
-                res = NX_ERR_SNAPPY_CHUNK_TOO_SHORT;
-                break;
-            }
-            if (type == 0u) {
-                // snappy.getPreamble(in) reads the varint from the cumulation, not the chunk
-                // (Snappy.java:404-441), then :197-201 bounds it.
-                uint32_t ulen = 0;
-                bool complete = false;
-                for (uint32_t i = 0; i < 4u && p + 8 + i < len; ++i) {
-                    const uint32_t c = b[p + 8 + i];
-                    ulen |= (c & 0x7Fu) << (7u * i);
-                    if (!(c & 0x80u)) {
-                        complete = true;
-                        break;
-                    }
-                    if (i == 3u) res = NX_ERR_SNAPPY_PREAMBLE_TOO_LONG;
-                }
-                if (res) break;
-                if (!complete) ulen = 0;
-                if (ulen > 65536u) {
-                    res = NX_ERR_SNAPPY_DECOMPRESSED_TOO_LARGE;
-                    break;
-                }
-            }
-            // claim a list entry; a full list stops the stream before this chunk
-            if (atomicAdd(&counts[2], 1u) >= cap) {
-                res = NX_SCAN_LIST_FULL;
-                break;
-            }
+        walk(b, len, w, ~0ull, [&](uint32_t type, uint64_t p, uint32_t clen, uint32_t crc) {
+            if (atomicAdd(&counts[2], 1u) >= cap) return false;
             const uint32_t k = type == 0u ? atomicAdd(&counts[0], 1u) : cap - 1u - atomicAdd(&counts[1], 1u);
             data_off[k] = base + p + 8;
             data_len[k] = clen - 4u;
-            masked_crc[k] = le32(b + p + 4);
+            masked_crc[k] = crc;
             chunk_stream[k] = s;
             chunk_seq[k] = seq++;
-            p += 4ull + clen;
+            return true;
+        });
+    }
+    if (w.res < 0) corrupted = true;  // :227-230
+    consumed[s] = w.p;
+    status[s] = w.res;
+    state[s] = (w.started ? 1u : 0u) | (corrupted ? 2u : 0u) | ((uint32_t)w.skip << 8);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Segmented walk of ONE long cumulation (round 5).  The chain is serial — each
+// header gives the next header's position — so a lone lane needs one dependent memory round trip
+// per chunk (~35 K for 1 GiB of 30 KB chunks).  Here the cumulation is cut into segments of SEG bytes:
+//   k_seg_guess  — one wave per segment j >= 1 finds the first position q >= j*SEG from which four
+//                  consecutive hops are plausible data-chunk headers (type 0 or 1, lengths and
+//                  preamble within the decoder's limits).  A guess is only a speculation;
+//   k_seg_count  — one lane per segment walks (walk() above, the exact decoder semantics) from its
+//                  guess (segment 0: from 0 with the caller's state) to the first header at or past
+//                  the segment's end, counting data chunks;
+//   k_seg_stitch — one workgroup follows the true chain through the segments: the walk of segment
+//                  j is accepted only if it started exactly where the previous accepted walk left
+//                  off; otherwise (a wrong or missing guess) the workgroup re-walks the segment from
+//                  the true position.  It prefix-sums the accepted segments' counts, claims list
+//                  entries (stopping at the list capacity as the lane walk does) and writes the
+//                  cumulation's consumed / status / state;
+//   k_seg_emit   — one lane per accepted segment walks it again and writes its list entries.
+// The result equals the lane walk's whatever the guesses: they decide only how much is walked twice.
+constexpr uint64_t kSegBytes = 1ull << 20;
+constexpr uint32_t kSegMax = 1024;          // segments per cumulation (the segment size doubles beyond 1 GiB)
+constexpr uint32_t kGuessWindow = 1u << 17; // guesses are searched in the first 128 KiB of a segment
+constexpr uint64_t kNone = ~0ull;
+
+struct SegInfo {
+    uint64_t entry;  // where the segment's walk started (kNone: no guess)
+    uint64_t exit;   // its Walk.p at the end
+    uint64_t skip;
+    uint32_t ncomp, nunc;
+    uint32_t how;    // WalkEnd
+    int32_t res;
+    uint32_t started;
+    uint32_t pad;
+};
+struct SegStep {     // one accepted segment, in chain order
+    uint32_t seg, o0, o1, pad;  // its first compressed / uncompressed entry among the stream's
+};
+struct SegPath {
+    uint32_t nseg;         // accepted segments
+    uint32_t base0, base1; // list slots of the stream's first compressed / uncompressed entry
+    uint32_t limit;        // data chunks that get entries (fewer than the chain's when the list fills)
+    uint32_t state_in;     // the cumulation's decoder state before the walk
+    uint32_t pad[3];
+};
+
+// Is q the start of four consecutive plausible data chunks (type 0 / 1 within the decoder's length
+// limits, a compressed chunk's preamble <= 65536)?  Reaching the end exactly counts as plausible.
+__device__ __forceinline__ bool plausible_run(const uint8_t* __restrict__ b, uint64_t len, uint64_t q) {
+    for (int h = 0; h < 4; ++h) {
+        if (q == len) return true;
+        if (q + 9 > len) return h > 0;
+        const uint32_t type = b[q];
+        const uint32_t clen = (uint32_t)b[q + 1] | ((uint32_t)b[q + 2] << 8) | ((uint32_t)b[q + 3] << 16);
+        if (type > 1u || clen < 5u || (type == 1u && clen > 65540u)) return false;
+        if (type == 0u) {
+            uint32_t ulen = 0, i = 0;
+            for (; i < 3u; ++i) {
+                const uint32_t c = b[q + 8 + i];
+                ulen |= (c & 0x7Fu) << (7u * i);
+                if (!(c & 0x80u)) break;
+            }
+            if (i == 3u || ulen > 65536u) return false;
+        }
+        q += 4ull + clen;
+        if (q > len) return h > 0;
+    }
+    return true;
+}
+
+// One wave per segment j >= 1: the first plausible position in [j*seg, j*seg + kGuessWindow).  The
+// wave stages 4 KiB of the segment in LDS at a time; lane l tests positions q0 + l + 64 t in rounds
+// t = 0..63 (a header byte and its length from LDS), the few that pass that first check follow their
+// hops in HBM, and the lowest passing position of the first round with one wins.
+__global__ void __launch_bounds__(64) k_seg_guess(const uint8_t* __restrict__ b, uint64_t len, uint64_t seg, uint32_t nseg,
+                                                  SegInfo* __restrict__ info) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[4096 + 64];
+    const uint32_t j = blockIdx.x + 1u;
+    if (j >= nseg) return;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t lo = (uint64_t)j * seg;
+    const uint64_t hi = min(len, lo + (uint64_t)kGuessWindow);
+    uint64_t found = kNone;
+    for (uint64_t q0 = lo; q0 < hi && found == kNone; q0 += 4096) {
+        __syncthreads();
+        for (uint32_t i = lane; i < 4096u + 64u; i += 64u) win[i] = q0 + i < len ? b[q0 + i] : 0u;
+        __syncthreads();
+        for (uint32_t t = 0; t < 64u; ++t) {
+            const uint32_t o = 64u * t + lane;
+            const uint64_t q = q0 + o;
+            bool ok = false;
+            if (q < hi) {
+                const uint32_t type = win[o];
+                const uint32_t clen = (uint32_t)win[o + 1] | ((uint32_t)win[o + 2] << 8) | ((uint32_t)win[o + 3] << 16);
+                if (type <= 1u && clen >= 5u) ok = plausible_run(b, len, q);
+            }
+            const uint64_t m = __ballot(ok);
+            if (m) {
+                found = q0 + 64u * t + (uint64_t)__ffsll((long long)m) - 1u;
+                break;
+            }
         }
     }
-    if (res < 0) corrupted = true;  // :227-230
-    consumed[s] = p;
-    status[s] = res;
-    state[s] = (started ? 1u : 0u) | (corrupted ? 2u : 0u) | ((uint32_t)skip << 8);
+    if (lane == 0) info[j].entry = found;
+}
+
+__global__ void __launch_bounds__(256) k_seg_count(const uint8_t* __restrict__ b, uint64_t len, uint64_t seg, uint32_t nseg,
+                                                   const uint32_t* __restrict__ state_p, SegInfo* __restrict__ info) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nseg) return;
+    SegInfo I = info[j];
+    Walk w{0, 0, true, NX_OK};
+    if (j == 0) {
+        const uint32_t st = *state_p;
+        I.entry = 0;
+        w.skip = st >> 8;
+        w.started = (st & 1u) != 0;
+    } else if (I.entry == kNone) {
+        I.how = kEnd;
+        info[j] = I;
+        return;
+    } else {
+        w.p = I.entry;
+    }
+    uint32_t nc = 0, nu = 0;
+    const uint64_t stop = j + 1u < nseg ? (uint64_t)(j + 1u) * seg : ~0ull;
+    I.how = walk(b, len, w, stop, [&](uint32_t type, uint64_t, uint32_t, uint32_t) {
+        (type == 0u ? nc : nu) += 1u;
+        return true;
+    });
+    I.exit = w.p;
+    I.skip = w.skip;
+    I.res = w.res;
+    I.started = w.started;
+    I.ncomp = nc;
+    I.nunc = nu;
+    info[j] = I;
+}
+
+// One workgroup: follows the true chain through the segments (in LDS), re-walking any segment whose
+// speculative walk did not start where the chain entered it, prefix-sums the accepted segments'
+// counts and claims list entries as the lane walk would (one per data chunk until the list is full).
+__global__ void __launch_bounds__(256) k_seg_stitch(const uint8_t* __restrict__ b, uint64_t len, uint64_t seg, uint32_t nseg,
+                                                    SegInfo* __restrict__ info, SegStep* __restrict__ path, SegPath* __restrict__ P,
+                                                    uint32_t* __restrict__ counts, uint32_t cap, uint32_t* __restrict__ state_p,
+                                                    uint64_t* __restrict__ consumed_p, int32_t* __restrict__ status_p) {
+    __shared__ SegInfo si[kSegMax];
+    for (uint32_t i = threadIdx.x; i < nseg; i += blockDim.x) si[i] = info[i];
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const uint32_t st_in = *state_p;
+    P->state_in = st_in;
+    if ((st_in >> 1) & 1u) {  // corrupted (:86-89): everything readable is discarded
+        P->nseg = 0;
+        *consumed_p = len;
+        *status_p = NX_OK;
+        return;
+    }
+    uint32_t j = 0, np = 0, c0 = 0, c1 = 0;
+    for (;;) {
+        const SegInfo& cur = si[j];
+        path[np++] = SegStep{j, c0, c1, 0u};
+        c0 += cur.ncomp;
+        c1 += cur.nunc;
+        if (cur.how != kOpen) break;
+        const uint32_t nj = (uint32_t)min((uint64_t)(nseg - 1u), cur.exit / seg);
+        if (si[nj].entry != cur.exit) {  // a wrong or missing guess: walk it from the true position
+            Walk w{cur.exit, 0, cur.started != 0, NX_OK};
+            uint32_t nc = 0, nu = 0;
+            const uint64_t stop = nj + 1u < nseg ? (uint64_t)(nj + 1u) * seg : ~0ull;
+            SegInfo R;
+            R.how = walk(b, len, w, stop, [&](uint32_t type, uint64_t, uint32_t, uint32_t) {
+                (type == 0u ? nc : nu) += 1u;
+                return true;
+            });
+            R.entry = cur.exit;
+            R.exit = w.p;
+            R.skip = w.skip;
+            R.res = w.res;
+            R.started = w.started;
+            R.ncomp = nc;
+            R.nunc = nu;
+            R.pad = 0;
+            si[nj] = R;
+            info[nj] = R;
+        }
+        j = nj;
+    }
+    const uint32_t tot = c0 + c1;
+    const uint32_t used = counts[2];
+    const uint32_t room = used < cap ? cap - used : 0u;
+    const uint32_t limit = tot < room ? tot : room;
+    P->nseg = np;
+    P->limit = limit;
+    P->base0 = counts[0];
+    P->base1 = counts[1];
+    counts[2] = used + limit + (limit < tot ? 1u : 0u);  // the lane walk's refused claim counts too
+    if (limit == tot) {
+        counts[0] = P->base0 + c0;
+        counts[1] = P->base1 + c1;
+        const SegInfo& L = si[j];
+        *consumed_p = L.exit;
+        *status_p = L.res;
+        *state_p = (L.started ? 1u : 0u) | (L.res < 0 ? 2u : 0u) | ((uint32_t)L.skip << 8);
+    }
+    // else k_seg_emit's segment holding chunk `limit` stops before it and writes the rest
+}
+
+// One lane per accepted segment: walks it again and writes its list entries.
+__global__ void __launch_bounds__(256) k_seg_emit(const uint8_t* __restrict__ b, uint64_t base, uint64_t len, uint64_t seg,
+                                                  uint32_t nseg, uint32_t s, const SegInfo* __restrict__ info,
+                                                  const SegStep* __restrict__ path, const SegPath* __restrict__ P,
+                                                  uint64_t* __restrict__ data_off, uint32_t* __restrict__ data_len,
+                                                  uint32_t* __restrict__ masked_crc, uint32_t* __restrict__ chunk_stream,
+                                                  uint32_t* __restrict__ chunk_seq, uint32_t* __restrict__ counts, uint32_t cap,
+                                                  uint32_t* __restrict__ state_p, uint64_t* __restrict__ consumed_p,
+                                                  int32_t* __restrict__ status_p) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= P->nseg) return;
+    const SegStep S = path[k];
+    const SegInfo I = info[S.seg];
+    const uint32_t first = S.o0 + S.o1, n = I.ncomp + I.nunc, limit = P->limit;
+    // segments wholly past the cut list nothing; the one holding chunk `limit` stops before it
+    if (first > limit || (first == limit && !(limit < first + n))) return;
+    Walk w{I.entry, 0, true, NX_OK};
+    if (k == 0) {
+        w.skip = P->state_in >> 8;
+        w.started = (P->state_in & 1u) != 0;
+    }
+    const uint64_t stop = S.seg + 1u < nseg ? (uint64_t)(S.seg + 1u) * seg : ~0ull;
+    uint32_t n0 = S.o0, n1 = S.o1;
+    const WalkEnd how = walk(b, len, w, stop, [&](uint32_t type, uint64_t p, uint32_t clen, uint32_t crc) {
+        if (n0 + n1 >= limit) return false;
+        const uint32_t e = type == 0u ? P->base0 + n0++ : cap - 1u - (P->base1 + n1++);
+        data_off[e] = base + p + 8;
+        data_len[e] = clen - 4u;
+        masked_crc[e] = crc;
+        chunk_stream[e] = s;
+        chunk_seq[e] = n0 + n1 - 1u;
+        return true;
+    });
+    if (how == kFull) {  // the list filled up here: the lane walk stops before this chunk
+        counts[0] = P->base0 + n0;
+        counts[1] = P->base1 + n1;
+        *consumed_p = w.p;
+        *status_p = NX_SCAN_LIST_FULL;
+        *state_p = (w.started ? 1u : 0u) | ((uint32_t)w.skip << 8);
+    }
 }
 
 }  // namespace fscan
@@ -164,5 +446,38 @@ extern "C" int32_t nx_snappy_frame_scan_batch(const uint8_t* in, const uint64_t*
     hipLaunchKernelGGL(nx::fscan::k_frame_scan, dim3((n + 255) / 256), dim3(256), 0, st, in, in_off, in_len, state,
                        consumed, status, data_off, data_len, masked_crc, chunk_stream, chunk_seq, counts, cap, n);
     NX_HIP_CHECK(hipGetLastError());
+    return NX_OK;
+}
+
+// One long cumulation in[0, len) (its length a host value, as a ByteBuf's readableBytes is): the
+// segmented walk.  Same outputs as nx_snappy_frame_scan_batch with n = 1 (stream index 0), counts
+// zeroed first; asynchronous on `stream` (its 2 KiB-per-segment scratch is stream-ordered).
+extern "C" int32_t nx_snappy_frame_scan_long(const uint8_t* in, uint64_t len, uint32_t* state, uint64_t* consumed, int32_t* status,
+                                             uint64_t* data_off, uint32_t* data_len, uint32_t* masked_crc, uint32_t* chunk_stream,
+                                             uint32_t* chunk_seq, uint32_t* counts, uint32_t cap, void* stream) {
+    NX_CLEAR_STALE_ERROR();
+    using namespace nx::fscan;
+    if (!counts || !state || !consumed || !status || (len && !in) ||
+        (cap && (!data_off || !data_len || !masked_crc || !chunk_stream || !chunk_seq)))
+        return NX_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    NX_HIP_CHECK(hipMemsetAsync(counts, 0, 3 * sizeof(uint32_t), st));
+    uint64_t seg = kSegBytes;
+    while ((len + seg - 1) / seg > kSegMax) seg *= 2;
+    const uint32_t nseg = len ? (uint32_t)((len + seg - 1) / seg) : 1u;
+    void* scratch = nullptr;
+    const size_t sb = sizeof(SegInfo) * nseg + sizeof(SegStep) * nseg + sizeof(SegPath);
+    NX_HIP_CHECK(hipMallocAsync(&scratch, sb, st));
+    SegInfo* info = static_cast<SegInfo*>(scratch);
+    SegStep* path = reinterpret_cast<SegStep*>(info + nseg);
+    SegPath* P = reinterpret_cast<SegPath*>(path + nseg);
+    if (nseg > 1) hipLaunchKernelGGL(k_seg_guess, dim3(nseg - 1), dim3(64), 0, st, in, len, seg, nseg, info);
+    hipLaunchKernelGGL(k_seg_count, dim3((nseg + 255) / 256), dim3(256), 0, st, in, len, seg, nseg, state, info);
+    hipLaunchKernelGGL(k_seg_stitch, dim3(1), dim3(256), 0, st, in, len, seg, nseg, info, path, P, counts, cap, state, consumed,
+                       status);
+    hipLaunchKernelGGL(k_seg_emit, dim3((nseg + 255) / 256), dim3(256), 0, st, in, (uint64_t)0, len, seg, nseg, 0u, info, path, P,
+                       data_off, data_len, masked_crc, chunk_stream, chunk_seq, counts, cap, state, consumed, status);
+    NX_HIP_CHECK(hipGetLastError());
+    NX_HIP_CHECK(hipFreeAsync(scratch, st));
     return NX_OK;
 }

@@ -177,3 +177,101 @@ def test_frame_scan_feeds_decode(dev, B, oracle):
         pieces.setdefault(sd[k], []).append((sq[k], datah[do[k]:do[k] + dl[k]]))
     for i, want in enumerate(msgs):
         assert b"".join(p for _, p in sorted(pieces[i])) == want, i
+
+
+# ---- one long cumulation: the segmented walk (nx_snappy_frame_scan_long) -----------------------------
+def _scan_long(B, dev, buf, st0, cap):
+    data = torch.frombuffer(bytearray(buf + bytes(16)), dtype=torch.uint8).to(dev)
+    state = torch.tensor([st0], dtype=torch.int64, device=dev).to(torch.int32)
+    r = B.snappy_frame_scan_long(data, len(buf), state, cap)
+    torch.cuda.synchronize()
+    cnt = r["counts"].cpu().tolist()
+    do, dl, mc, sd, sq = (r[k].cpu().tolist() for k in ("data_off", "data_len", "masked_crc", "stream", "seq"))
+    got = sorted((sq[k], 0 if k < cnt[0] else 1, do[k], dl[k], mc[k] & 0xFFFFFFFF)
+                 for k in list(range(cnt[0])) + list(range(cap - cnt[1], cap)))
+    assert all(sd[k] == 0 for k in list(range(cnt[0])) + list(range(cap - cnt[1], cap)))
+    return got, r["consumed"].item(), r["status"].item(), state.item() & 0xFFFFFFFF, cnt
+
+
+def _check_long(B, dev, oracle, buf, st0=0, cap=1 << 16):
+    got, cons, stat, st, cnt = _scan_long(B, dev, buf, st0, cap)
+    ents, c, s, res = oracle.snappy_frame_scan(buf, st0, cap)
+    assert [e[0] for e in got] == list(range(len(got)))
+    assert [e[1:] for e in got] == ents
+    assert (cons, stat, st) == (c, res, s)
+    return got, cnt
+
+
+def _long_stream(oracle, mib, seed, extras=()):
+    """A SnappyFrameEncoder stream of ~mib MiB (text, random and short chunks), with `extras`
+    (position fraction, bytes) spliced in at chunk boundaries."""
+    rng = random.Random(seed)
+    parts, size = [ID], 10
+    cuts = sorted(extras)
+    while size < mib << 20:
+        if cuts and size >= cuts[0][0] * (mib << 20):
+            parts.append(cuts.pop(0)[1])
+            size += len(parts[-1])
+            continue
+        r = rng.random()
+        d = (oracle.textgen_chunk(rng.randrange(1 << 20), rng.randint(100000, 400000)) if r < 0.8
+             else oracle.java_random_bytes(rng.randrange(1 << 20), rng.randint(1, 200000)))
+        parts.append(oracle.snappy_frame_encode(d, started=True)[0])
+        size += len(parts[-1])
+    return b"".join(parts)
+
+
+def _skippable(t, k):
+    return bytes([t]) + k.to_bytes(3, "little") + bytes(k)
+
+
+def test_frame_scan_long_parity(dev, B, oracle, kat):
+    """The segmented walk of one long cumulation lists exactly the oracle walk's chunks, consumed
+    position, status and state: plain streams, skippable / padding chunks (one of 3 MiB spanning
+    segments, so guesses land inside it and are corrected), a second stream identifier, an error
+    in the middle, a cut at the end, and the incoming states (no identifier yet, corrupted, bytes
+    left to skip)."""
+    base = _long_stream(oracle, 24, 1)
+    _check_long(B, dev, oracle, base)
+    _check_long(B, dev, oracle, base[:len(base) - 12345])                  # partial last chunk
+    _check_long(B, dev, oracle, base[:(5 << 20) + 7])
+    withskip = _long_stream(oracle, 24, 2, extras=[(0.2, _skippable(0x80, 3 << 20)), (0.5, _skippable(0xFE, 100)),
+                                                   (0.6, ID), (0.7, _skippable(0xC3, 70000))])
+    _check_long(B, dev, oracle, withskip)
+    bad = _long_stream(oracle, 16, 3, extras=[(0.55, b"\x02\x10\x00\x00" + bytes(16))])
+    got, _ = _check_long(B, dev, oracle, bad)
+    assert len(got) > 50
+    bad2 = _long_stream(oracle, 16, 4, extras=[(0.4, b"\x00\x08\x00\x00" + bytes(4) + b"\x81\x80\x04\x00")])
+    _check_long(B, dev, oracle, bad2)
+    noid = base[10:]
+    _check_long(B, dev, oracle, noid, 0)                                     # data before the identifier
+    _check_long(B, dev, oracle, noid, 1)                                     # a continuation
+    _check_long(B, dev, oracle, noid, 2)                                     # corrupted: discarded
+    sk = _skippable(0x90, 5000)
+    _check_long(B, dev, oracle, sk[1000:] + base[10:], 1 | (4004 << 8))      # skip carried in
+    _check_long(B, dev, oracle, base[:3 << 20], 1)
+    # every short stream of the lane-walk tests through the segmented path too (one segment)
+    for s, st in _streams(oracle, kat, n=24, seed=11):
+        _check_long(B, dev, oracle, s, st)
+
+
+def test_frame_scan_long_list_full(dev, B, oracle):
+    """A list that fills up stops the walk before the first chunk it cannot list, as the lane walk:
+    at the first chunk, inside a segment, and exactly at a segment's first chunk."""
+    buf = _long_stream(oracle, 12, 5)
+    all_ents = oracle.snappy_frame_scan(buf, 0, None)[0]
+    n = len(all_ents)
+    # the index of the first chunk that starts in the second segment
+    first_seg1 = next(i for i, e in enumerate(all_ents) if e[1] - 8 >= 1 << 20)
+    for cap in (1, 2, 37, first_seg1, first_seg1 + 1, n - 1, n, n + 5):
+        got, cnt = _check_long(B, dev, oracle, buf, 0, cap)
+        assert len(got) == min(cap, n)
+        assert cnt[2] == min(cap, n) + (1 if cap < n else 0)
+
+
+def test_frame_scan_long_equals_lane_walk(dev, B, oracle):
+    """The segmented walk and the lane walk (nx_snappy_frame_scan_batch, n = 1) give the same list."""
+    buf = _long_stream(oracle, 20, 6, extras=[(0.3, _skippable(0x81, 2 << 20))])
+    got, _, _, _, _ = _scan_long(B, dev, buf, 0, 1 << 16)
+    _, r, cnt, per, states = _scan(B, dev, [(buf, 0)], 1 << 16)
+    assert [(e[1], e[2], e[3], e[4]) for e in got] == [(e[1], e[2], e[3], e[4]) for e in per[0]]
