@@ -32,10 +32,10 @@
 // flushed output (far copies); no read precedes a chunk's or a frame's first byte.
 
 #ifndef NX_UX_RING
-#define NX_UX_RING 8192
+#define NX_UX_RING 4096
 #endif
 #ifndef NX_UX_WAVES
-#define NX_UX_WAVES 4
+#define NX_UX_WAVES 6
 #endif
 #ifndef NX_UX_AHEAD
 #define NX_UX_AHEAD 128
@@ -46,7 +46,9 @@
 constexpr uint32_t kUxRing = NX_UX_RING;     // output history per wave (bytes, power of two)
 constexpr uint32_t kUxSlots = kUxRing / 16;  // unit slots in the ring
 constexpr uint32_t kUxRR = 256;              // record ring entries (output start, record)
-constexpr uint32_t kUxUF = 512;              // unit -> first record ring entries
+constexpr uint32_t kUxUF = 256;              // unit -> first record ring entries
+constexpr uint32_t kUxIn = 32;               // records per intake (<= 2 KiB of output: 16 * kUxUF >= 2 * kUxIn * 64)
+static_assert(16u * kUxUF >= 2u * kUxIn * 64u, "an intake fits the unit-first ring beside the unit being assigned");
 constexpr uint32_t kUxAhead = NX_UX_AHEAD;   // units assigned past the lowest pending one
 constexpr int kUxWaves = NX_UX_WAVES;        // waves (frames in flight) per workgroup
 constexpr int kUxK = NX_UX_K;                // segment attempts per lane per round
@@ -146,21 +148,23 @@ __global__ void __launch_bounds__(kUxWaves * 64)
         uint32_t nxt = 0, lowpend = 0, flushed = 0, rin = 0, Oin = 0, rlow = 0, rounds = 0;
         // lane state: unit, its first record, pending segments (bit k = record rf + k), applied bytes,
         // the unit's bytes, and the HBM load in flight (its bytes, its byte range b0 | b1 << 8)
-        uint32_t u = kUxNone, rf = 0, pend = 0, am = 0, ldb = 0;
+        uint32_t u = kUxNone, rf = 0, pend = 0, am = 0, ldb = 0, hbm = 0;
         bool infl = false;
         uint4 dat = make_uint4(0, 0, 0, 0), ldv = make_uint4(0, 0, 0, 0);
         uint32_t acc = 0;
-        uint32_t rpre = lane < N ? R[lane] : 0u;
+        uint32_t rpre = lane < kUxIn && lane < N ? R[lane] : 0u;
         bool guard = false;
         for (;;) {
-            // ---- intake: 64 records at a time into the record ring, output starts by a prefix sum, and
-            // each unit whose first byte lies in a record marks that record
+            // ---- intake: 32 records at a time (at most 2 KiB of output, so the unit-first ring of 256
+            // units always has room for them beside the unit being assigned) into the record ring, output
+            // starts by a prefix sum, and each unit whose first byte lies in a record marks that record
             for (int t = 0; t < 2; ++t) {
-                if (!(rin < N && rin + 64u <= rlow + kUxRR && Oin + 4096u + 16u <= 16u * (nxt + kUxUF))) break;
-                const bool valid = rin + lane < N;
+                if (!(rin < N && rin + kUxIn <= rlow + kUxRR)) break;
+                const bool valid = lane < kUxIn && rin + lane < N;
                 const uint32_t r = rpre;
                 const uint32_t len = valid ? ((r >> 25) & 63u) + 1u : 0u;
                 const uint32_t incl = incl_scan(len);
+                if (Oin + uni((uint32_t)__builtin_amdgcn_readlane((int)incl, 63)) > 16u * (nxt + kUxUF)) break;
                 const uint32_t os = Oin + incl - len;
                 if (valid) {
                     L.rr[(rin + lane) & (kUxRR - 1)] = make_uint2(os, r);
@@ -170,8 +174,8 @@ __global__ void __launch_bounds__(kUxWaves * 64)
                         if (16u * (c0 + k) < os + len) L.uf[(c0 + k) & (kUxUF - 1)] = (uint16_t)(rin + lane);
                 }
                 Oin += uni((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
-                rin = rin + 64u < N ? rin + 64u : N;
-                rpre = rin + lane < N ? R[rin + lane] : 0u;
+                rin = rin + kUxIn < N ? rin + kUxIn : N;
+                rpre = lane < kUxIn && rin + lane < N ? R[rin + lane] : 0u;
             }
             wave_sync();
             // ---- refill: free lanes take the next units, in unit order by lane rank
@@ -194,6 +198,8 @@ __global__ void __launch_bounds__(kUxWaves * 64)
                         u = v;
                         rf = f;
                         pend = (2u << (rl - f)) - 1u;
+                        hbm = 0;  // literal segments read the compressed chunk in HBM: the load step's
+                        for (uint32_t k = 0; k <= rl - f; ++k) hbm |= (L.rr[(f + k) & (kUxRR - 1)].y >> 31) ? 0u : 1u << k;
                         am = 0;
                         dat = make_uint4(0, 0, 0, 0);
                         L.umask[v & (kUxSlots - 1)] = 0;
@@ -202,8 +208,71 @@ __global__ void __launch_bounds__(kUxWaves * 64)
                 }
             }
             wave_sync();
-            // ---- merge the HBM bytes loaded last round.  The wait also retires last round's flush stores,
-            // so a far copy issued below never reads a line before its bytes reach the L2.
+            // ---- attempts: the kUxK lowest pending segments that read LDS (ring copies); a segment found
+            // to read HBM (literal, or a copy older than the ring) is marked and left to the load step
+            const uint32_t farU = nxt > kUxSlots ? nxt - kUxSlots : 0u;  // units below this are not in the ring
+            uint32_t tried = hbm;
+            for (int a = 0; a < kUxK; ++a) {
+                const uint32_t cand = pend & ~tried;
+                if (!__ballot(cand != 0u)) break;
+                if (cand) {
+                    const uint32_t k = (uint32_t)__builtin_ctz(cand);
+                    tried |= 1u << k;
+                    const uint2 e = L.rr[(rf + k) & (kUxRR - 1)];
+                    const uint32_t os = e.x, r = e.y;
+                    const uint32_t len = ((r >> 25) & 63u) + 1u, x = r & 0x1FFFFFFu;
+                    const uint32_t U0 = u << 4;
+                    const uint32_t q0 = max(os, U0), q1 = min(os + len, U0 + 16u);
+                    const uint32_t b0 = q0 - U0, b1 = q1 - U0;
+                    // source bytes this copy reads: [s0, s1); a copy with offset < 16 reads its period
+                    const bool per = x < 16u;
+                    const uint32_t s0 = per ? os - x : q0 - x, s1 = per ? os : q1 - x;
+                    const uint32_t v0 = s0 >> 4, v1 = (s1 - 1u) >> 4;
+                    if (!per && v1 < farU) {  // older than the ring: the load step reads it from HBM
+                        hbm |= 1u << k;
+                    } else {
+                        // bytes applied? (own unit: the lane's mask; below lowpend: final).  v0 < farU <= v1
+                        // (a copy straddling the ring's end): v0 is flushed, so below lowpend and final;
+                        // its bytes are read one by one, from HBM and the ring.
+                        const uint32_t n0 = bits16(s0 & 15u, v1 == v0 ? ((s1 - 1u) & 15u) + 1u : 16u);
+                        const uint32_t n1 = v1 == v0 ? 0u : bits16(0u, ((s1 - 1u) & 15u) + 1u);
+                        const uint32_t m0 = v0 == u ? am : (v0 < lowpend ? 0xFFFFu : (uint32_t)L.umask[v0 & (kUxSlots - 1)]);
+                        const uint32_t m1 = v1 == u ? am : (v1 < lowpend ? 0xFFFFu : (uint32_t)L.umask[v1 & (kUxSlots - 1)]);
+                        if ((m0 & n0) == n0 && (m1 & n1) == n1) {
+                            uint4 v;
+                            if (per || v0 < farU) {  // byte by byte: period copies, copies straddling the ring's end
+                                if (per) *reinterpret_cast<uint4*>(&L.ring[(U0 & (kUxRing - 1)) >> 2]) = dat;  // own bytes readable
+                                uint32_t w[4] = {0u, 0u, 0u, 0u};
+                                uint32_t t = per ? (U0 + b0 - os) % x : 0u;
+                                for (uint32_t j = b0; j < b1; ++j) {
+                                    const uint32_t p = per ? os - x + t : U0 + j - x;
+                                    const uint32_t byte = (p >> 4) < farU ? dst[p] : ring8[p & (kUxRing - 1)];
+                                    t = t + 1u == x ? 0u : t + 1u;
+                                    w[j >> 2] |= byte << (8u * (j & 3u));
+                                }
+                                v = make_uint4(w[0], w[1], w[2], w[3]);
+                            } else {  // ring: 5 dwords from the unit-aligned source start
+                                const uint32_t sa = (U0 - x) & (kUxRing - 1);
+                                const uint32_t* q = &L.ring[sa >> 2];
+                                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+                                const uint32_t sh = sa & 3u;
+                                v = make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                                               __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+                            }
+                            const uint4 m0 = lowm[b0], m1 = lowm[b1];
+                            dat.x = bfi32(m0.x ^ m1.x, v.x, dat.x);
+                            dat.y = bfi32(m0.y ^ m1.y, v.y, dat.y);
+                            dat.z = bfi32(m0.z ^ m1.z, v.z, dat.z);
+                            dat.w = bfi32(m0.w ^ m1.w, v.w, dat.w);
+                            am |= bits16(b0, b1);
+                            pend &= ~(1u << k);
+                        }
+                    }
+                }
+            }
+            // ---- merge the HBM bytes loaded last round (a round of LDS work after their issue).  The wait
+            // also retires last round's flush stores, so a far copy issued below never reads a line
+            // before its bytes reach the L2.
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (infl) {
                 const uint4 m0 = lowm[ldb & 31u], m1 = lowm[ldb >> 8];
@@ -214,15 +283,12 @@ __global__ void __launch_bounds__(kUxWaves * 64)
                 am |= bits16(ldb & 31u, ldb >> 8);
                 infl = false;
             }
-            // ---- attempts: the kUxK lowest pending segments
-            const uint32_t farU = nxt > kUxSlots ? nxt - kUxSlots : 0u;  // units below this are not in the ring
-            uint32_t tried = 0;
-            for (int a = 0; a < kUxK; ++a) {
-                const uint32_t cand = pend & ~tried;
-                if (!__ballot(cand != 0u)) break;
-                if (cand) {
-                    const uint32_t k = (uint32_t)__builtin_ctz(cand);
-                    tried |= 1u << k;
+            // ---- load step: each lane's lowest pending HBM segment, one 16-byte load aligned to the unit,
+            // merged next round (at a chunk's edges: its bytes one by one now)
+            if (__ballot((pend & hbm) != 0u)) {
+                const uint32_t hm = pend & hbm;
+                if (hm) {
+                    const uint32_t k = (uint32_t)__builtin_ctz(hm);
                     const uint2 e = L.rr[(rf + k) & (kUxRR - 1)];
                     const uint32_t os = e.x, r = e.y;
                     const uint32_t len = ((r >> 25) & 63u) + 1u, x = r & 0x1FFFFFFu;
@@ -230,69 +296,25 @@ __global__ void __launch_bounds__(kUxWaves * 64)
                     const uint32_t U0 = u << 4;
                     const uint32_t q0 = max(os, U0), q1 = min(os + len, U0 + 16u);
                     const uint32_t b0 = q0 - U0, b1 = q1 - U0;
-                    // source bytes this segment reads: [s0, s1); a copy with offset < 16 reads its period
-                    const bool per = isc && x < 16u;
-                    const uint32_t s0 = per ? os - x : q0 - x, s1 = per ? os : q1 - x;
-                    const uint32_t v0 = s0 >> 4, v1 = (s1 - 1u) >> 4;
-                    const bool far = isc && !per && v1 < farU;
-                    bool ready = !isc || far;
-                    bool slow = false;
-                    if (isc && !far) {  // bytes applied? (own unit: the lane's mask; below lowpend: final)
-                        const uint32_t n0 = bits16(s0 & 15u, v1 == v0 ? ((s1 - 1u) & 15u) + 1u : 16u);
-                        const uint32_t n1 = v1 == v0 ? 0u : bits16(0u, ((s1 - 1u) & 15u) + 1u);
-                        const uint32_t m0 = v0 == u ? am : (v0 < lowpend ? 0xFFFFu : (uint32_t)L.umask[v0 & (kUxSlots - 1)]);
-                        const uint32_t m1 = v1 == u ? am : (v1 < lowpend ? 0xFFFFu : (uint32_t)L.umask[v1 & (kUxSlots - 1)]);
-                        // (v0 < farU <= v1, a copy straddling the ring's end: v0 is flushed, so below
-                        // lowpend and final; its bytes are read one by one, from HBM and the ring)
-                        ready = (m0 & n0) == n0 && (m1 & n1) == n1;
-                        slow = per || v0 < farU;
-                    }
-                    // HBM source, unit-aligned: literal input position / output position of unit byte 0
-                    const bool hbm = !isc || far;
+                    // literal: input position of unit byte 0; far copy: output position of unit byte 0
                     const uint32_t ga = isc ? U0 - x : x + U0 - os;
                     const bool gfast = isc ? (U0 >= x) : (x + U0 >= os && ga + 16u <= ilen);
-                    if (hbm && gfast) {
-                        if (!infl) {
-                            const uint8_t* p = isc ? dst + ga : src + ga;
-                            ldv = g_ld16u(p);
-                            ldb = b0 | (b1 << 8);
-                            infl = true;
-                            pend &= ~(1u << k);
-                        }
-                    } else if (ready) {
-                        uint4 v;
-                        if (hbm || slow) {  // byte by byte: chunk ends, period copies, copies near the frame start
-                            if (per) *reinterpret_cast<uint4*>(&L.ring[(U0 & (kUxRing - 1)) >> 2]) = dat;  // own bytes readable
-                            uint32_t w[4] = {0u, 0u, 0u, 0u};
-                            uint32_t t = per ? (U0 + b0 - os) % x : 0u;
-                            for (uint32_t j = b0; j < b1; ++j) {
-                                uint32_t byte;
-                                if (!isc) {
-                                    byte = src[x + U0 + j - os];
-                                } else {
-                                    const uint32_t p = per ? os - x + t : U0 + j - x;
-                                    byte = (p >> 4) < farU ? dst[p] : ring8[p & (kUxRing - 1)];
-                                    t = t + 1u == x ? 0u : t + 1u;
-                                }
-                                w[j >> 2] |= byte << (8u * (j & 3u));
-                            }
-                            v = make_uint4(w[0], w[1], w[2], w[3]);
-                        } else {  // ring: 5 dwords from the unit-aligned source start
-                            const uint32_t sa = (U0 - x) & (kUxRing - 1);
-                            const uint32_t* q = &L.ring[sa >> 2];
-                            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
-                            const uint32_t sh = sa & 3u;
-                            v = make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
-                                           __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
-                        }
+                    if (gfast) {
+                        ldv = g_ld16u(isc ? dst + ga : src + ga);
+                        ldb = b0 | (b1 << 8);
+                        infl = true;
+                    } else {
+                        uint32_t w[4] = {0u, 0u, 0u, 0u};
+                        for (uint32_t j = b0; j < b1; ++j)
+                            w[j >> 2] |= (uint32_t)(isc ? dst[U0 + j - x] : src[x + U0 + j - os]) << (8u * (j & 3u));
                         const uint4 m0 = lowm[b0], m1 = lowm[b1];
-                        dat.x = bfi32(m0.x ^ m1.x, v.x, dat.x);
-                        dat.y = bfi32(m0.y ^ m1.y, v.y, dat.y);
-                        dat.z = bfi32(m0.z ^ m1.z, v.z, dat.z);
-                        dat.w = bfi32(m0.w ^ m1.w, v.w, dat.w);
+                        dat.x = bfi32(m0.x ^ m1.x, w[0], dat.x);
+                        dat.y = bfi32(m0.y ^ m1.y, w[1], dat.y);
+                        dat.z = bfi32(m0.z ^ m1.z, w[2], dat.z);
+                        dat.w = bfi32(m0.w ^ m1.w, w[3], dat.w);
                         am |= bits16(b0, b1);
-                        pend &= ~(1u << k);
                     }
+                    pend &= ~(1u << k);
                 }
             }
             // ---- publish the units' bytes and applied masks; completed units free their lanes
