@@ -421,7 +421,7 @@ def encoder_placement():
             "probe_ms": [round(ms[k], 3) for k in range(n.value)], "pick": pick.value}
 
 
-DEC_KERNELS = ["nx::dec::k_parse", "nx::dec::k_expand_u"]  # k_expand (NX_EXPANDER=pieces) for A/B runs only
+DEC_KERNELS = ["nx::dec::k_parse", "nx::dec::k_expand"]
 
 
 def timed_legs(torch, leg, steps, warmup, sync, S, dev, cdev=None):

@@ -62,6 +62,8 @@ struct UxLds {
     uint2 rr[kUxRR];                 // record ring: (output start, record)
     uint16_t umask[kUxSlots];        // applied-byte mask of the unit in each ring slot
     uint16_t uf[kUxUF];              // first record (the one holding byte 16v) of unit v
+    uint32_t litb[kUxRR / 32];       // bit r % 32 of word (r / 32) % 8: record r is a literal
+    uint32_t pad2[(16 - (kUxRR / 32) % 16) % 4];
 };
 static_assert(sizeof(UxLds) % 16 == 0, "keep per-wave LDS 16-byte aligned");
 // per workgroup: slicing-by-4 (4 KiB), shift by 1 KiB (4 KiB), byte-range masks lowm[b] (17 x 16 B)
@@ -166,6 +168,10 @@ __global__ void __launch_bounds__(kUxWaves * 64)
                 const uint32_t incl = incl_scan(len);
                 if (Oin + uni((uint32_t)__builtin_amdgcn_readlane((int)incl, 63)) > 16u * (nxt + kUxUF)) break;
                 const uint32_t os = Oin + incl - len;
+                {
+                    const uint64_t lm = __ballot(valid && (r >> 31) == 0u);  // rin is a multiple of kUxIn
+                    if (lane == 0) L.litb[(rin >> 5) & (kUxRR / 32 - 1)] = (uint32_t)lm;
+                }
                 if (valid) {
                     L.rr[(rin + lane) & (kUxRR - 1)] = make_uint2(os, r);
                     const uint32_t c0 = (os + 15u) >> 4;
@@ -198,8 +204,11 @@ __global__ void __launch_bounds__(kUxWaves * 64)
                         u = v;
                         rf = f;
                         pend = (2u << (rl - f)) - 1u;
-                        hbm = 0;  // literal segments read the compressed chunk in HBM: the load step's
-                        for (uint32_t k = 0; k <= rl - f; ++k) hbm |= (L.rr[(f + k) & (kUxRR - 1)].y >> 31) ? 0u : 1u << k;
+                        {   // literal segments read the compressed chunk in HBM: the load step's
+                            const uint64_t lw = (uint64_t)L.litb[(f >> 5) & (kUxRR / 32 - 1)] |
+                                                ((uint64_t)L.litb[((f >> 5) + 1u) & (kUxRR / 32 - 1)] << 32);
+                            hbm = (uint32_t)(lw >> (f & 31u)) & ((2u << (rl - f)) - 1u);
+                        }
                         am = 0;
                         dat = make_uint4(0, 0, 0, 0);
                         L.umask[v & (kUxSlots - 1)] = 0;
@@ -224,9 +233,17 @@ __global__ void __launch_bounds__(kUxWaves * 64)
                     const uint32_t U0 = u << 4;
                     const uint32_t q0 = max(os, U0), q1 = min(os + len, U0 + 16u);
                     const uint32_t b0 = q0 - U0, b1 = q1 - U0;
-                    // source bytes this copy reads: [s0, s1); a copy with offset < 16 reads its period
-                    const bool per = x < 16u;
-                    const uint32_t s0 = per ? os - x : q0 - x, s1 = per ? os : q1 - x;
+                    // A copy with offset x < 16 repeats its first x bytes: once a segment byte lies dm - x or
+                    // more into the copy (dm = the least multiple of x >= 16), every byte of the segment is
+                    // the byte dm back, an ordinary unit-aligned ring read; only the first bytes of such a
+                    // copy (per) read its period [os - x, os) byte by byte.
+                    uint32_t xs = x;
+                    if (x < 16u) {
+                        const uint32_t m = (uint32_t)((float)(15u + x) * __builtin_amdgcn_rcpf((float)x) + 1e-3f);
+                        if (q0 + x >= os + m * x) xs = m * x;
+                    }
+                    const bool per = xs < 16u;
+                    const uint32_t s0 = per ? os - x : q0 - xs, s1 = per ? os : q1 - xs;
                     const uint32_t v0 = s0 >> 4, v1 = (s1 - 1u) >> 4;
                     if (!per && v1 < farU) {  // older than the ring: the load step reads it from HBM
                         hbm |= 1u << k;
@@ -240,19 +257,25 @@ __global__ void __launch_bounds__(kUxWaves * 64)
                         const uint32_t m1 = v1 == u ? am : (v1 < lowpend ? 0xFFFFu : (uint32_t)L.umask[v1 & (kUxSlots - 1)]);
                         if ((m0 & n0) == n0 && (m1 & n1) == n1) {
                             uint4 v;
-                            if (per || v0 < farU) {  // byte by byte: period copies, copies straddling the ring's end
-                                if (per) *reinterpret_cast<uint4*>(&L.ring[(U0 & (kUxRing - 1)) >> 2]) = dat;  // own bytes readable
+                            if (per) {  // the period, byte by byte from the ring (own bytes stored first)
+                                *reinterpret_cast<uint4*>(&L.ring[(U0 & (kUxRing - 1)) >> 2]) = dat;
                                 uint32_t w[4] = {0u, 0u, 0u, 0u};
-                                uint32_t t = per ? (U0 + b0 - os) % x : 0u;
+                                const uint32_t n = U0 + b0 - os;  // < 80
+                                uint32_t t = n - x * (uint32_t)((float)n * __builtin_amdgcn_rcpf((float)x) + 1e-3f);
                                 for (uint32_t j = b0; j < b1; ++j) {
-                                    const uint32_t p = per ? os - x + t : U0 + j - x;
-                                    const uint32_t byte = (p >> 4) < farU ? dst[p] : ring8[p & (kUxRing - 1)];
+                                    w[j >> 2] |= (uint32_t)ring8[(os - x + t) & (kUxRing - 1)] << (8u * (j & 3u));
                                     t = t + 1u == x ? 0u : t + 1u;
-                                    w[j >> 2] |= byte << (8u * (j & 3u));
+                                }
+                                v = make_uint4(w[0], w[1], w[2], w[3]);
+                            } else if (v0 < farU) {  // straddling the ring's end (rare): HBM and ring bytes
+                                uint32_t w[4] = {0u, 0u, 0u, 0u};
+                                for (uint32_t j = b0; j < b1; ++j) {
+                                    const uint32_t p = U0 + j - xs;
+                                    w[j >> 2] |= (uint32_t)((p >> 4) < farU ? dst[p] : ring8[p & (kUxRing - 1)]) << (8u * (j & 3u));
                                 }
                                 v = make_uint4(w[0], w[1], w[2], w[3]);
                             } else {  // ring: 5 dwords from the unit-aligned source start
-                                const uint32_t sa = (U0 - x) & (kUxRing - 1);
+                                const uint32_t sa = (U0 - xs) & (kUxRing - 1);
                                 const uint32_t* q = &L.ring[sa >> 2];
                                 const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
                                 const uint32_t sh = sa & 3u;

@@ -1482,12 +1482,13 @@ static hipError_t wave_kernel_attrs(size_t lds) {
     return attr_err;
 }
 
-// Which record expander launch_expand runs: the unit-lane k_expand_u (default) or the piece expander
-// k_expand (NX_EXPANDER=pieces, kept for same-box A/B runs).  Read once per process.
+// Which record expander launch_expand runs: the piece expander k_expand, or the round-5 unit-lane
+// k_expand_u when NX_EXPANDER=units (an experiment kept for same-box A/B runs: bit-exact on every
+// decode test, 2.3x slower, DESIGN.md §4 "Round 5").  Read once per process.
 static bool use_unit_expander() {
     static const bool units = [] {
         const char* e = getenv("NX_EXPANDER");
-        return !(e && strcmp(e, "pieces") == 0);
+        return e && strcmp(e, "units") == 0;
     }();
     return units;
 }
