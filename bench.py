@@ -912,7 +912,7 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2, hc_n: int = 1024):
     return res
 
 
-def bench_latency(torch, B, dev, sizes=(1, 64, 1024, 16384), reps: int = 3):
+def bench_latency(torch, B, dev, sizes=(1, 64, 1024, 4096, 16384), reps: int = 3):
     """Per-batch latency of the Snappy encode (+ CRC32C) and decode (+ verify) batch calls, as a
     handler call or a batcher flush of that many 64 KiB text chunks sees it: best of `reps` HIP-event
     timings on the current stream, outputs checked against the sources."""

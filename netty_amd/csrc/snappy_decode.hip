@@ -1045,6 +1045,7 @@ __global__ void __launch_bounds__(kExpandWaves * 64, kExpandStaged ? 6 : 3)
 
 
 #include "expand_units.hpp"
+#include "expand_frame.hpp"
 
 
 // =====================================================================================
@@ -1478,19 +1479,23 @@ static hipError_t wave_kernel_attrs(size_t lds) {
             attr_err = hipFuncSetAttribute((const void*)nx::dec::k_expand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kExpandLds);
         if (attr_err == hipSuccess)
             attr_err = hipFuncSetAttribute((const void*)nx::dec::k_expand_u, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nx::dec::kUxLds);
+        if (attr_err == hipSuccess)
+            attr_err = hipFuncSetAttribute((const void*)nx::dec::k_expand_f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nx::dec::kFxLds);
     });
     return attr_err;
 }
 
-// Which record expander launch_expand runs: the piece expander k_expand, or the round-5 unit-lane
-// k_expand_u when NX_EXPANDER=units (an experiment kept for same-box A/B runs: bit-exact on every
-// decode test, 2.3x slower, DESIGN.md §4 "Round 5").  Read once per process.
-static bool use_unit_expander() {
-    static const bool units = [] {
+// Which record expander launch_expand runs: the piece expander k_expand (0), or one of the round-5
+// experiments kept for same-box A/B runs (DESIGN.md §4 "Round 5"): the unit-lane k_expand_u
+// (NX_EXPANDER=units, 1) or the frame-window k_expand_f (NX_EXPANDER=frame, 2).  Read once per process.
+static int expander_choice() {
+    static const int which = [] {
         const char* e = getenv("NX_EXPANDER");
-        return e && strcmp(e, "units") == 0;
+        if (e && strcmp(e, "units") == 0) return 1;
+        if (e && strcmp(e, "frame") == 0) return 2;
+        return 0;
     }();
-    return units;
+    return which;
 }
 
 // one launch of the record expander over m frames
@@ -1498,7 +1503,13 @@ static hipError_t launch_expand(const uint8_t* in, const uint64_t* in_off, const
                                 const uint32_t* rec, const uint32_t* nrec, uint32_t* out_len, int32_t* status, const uint32_t* expect,
                                 uint32_t* crc_out, uint32_t m, int cus, hipStream_t st) {
     using namespace nx::dec;
-    if (use_unit_expander()) {
+    if (expander_choice() == 2) {  // one workgroup (two frame windows) per CU
+        const uint64_t need = (m + 1u) / 2u, want = (uint64_t)cus;
+        hipLaunchKernelGGL(k_expand_f, dim3((unsigned)(need < want ? need : want)), dim3(256), kFxLds, st, in, in_off, in_len, out,
+                           out_off, rec, nrec, out_len, status, expect, crc_out, m, nx::crc_tables_dev());
+        return hipGetLastError();
+    }
+    if (expander_choice() == 1) {
         const uint64_t per_cu = 160 * 1024 / kUxLds;
         const uint64_t want = (uint64_t)cus * per_cu, need = (m + kUxWaves - 1) / kUxWaves;
         hipLaunchKernelGGL(k_expand_u, dim3((unsigned)(need < want ? need : want)), dim3(kUxWaves * 64), kUxLds, st, in, in_off, in_len,

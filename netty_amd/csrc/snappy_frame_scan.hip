@@ -20,6 +20,7 @@
 // fixed; chunk_stream / chunk_seq give each entry's stream and its position among that stream's
 // data chunks.
 #include <stdlib.h>
+#include <mutex>
 #include <vector>
 #include "nx_common.hpp"
 #include "../../include/netty_amd.h"
@@ -27,8 +28,24 @@
 namespace nx {
 namespace fscan {
 
-__device__ __forceinline__ uint32_t le32(const uint8_t* p) {
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
+typedef v4u_ __attribute__((aligned(1))) v4uu_;
+typedef __attribute__((address_space(1))) const v4uu_ gv4uu_;
+
+// The 16 bytes at b[p, p + 16) as four LE dwords (one unaligned dwordx4 load), zero past len: a chunk
+// header (type, length, masked CRC) and the preamble varint behind it in one memory round trip.
+__device__ __forceinline__ uint4 hdr16(const uint8_t* __restrict__ b, uint64_t len, uint64_t p) {
+    if (p + 16u <= len) {
+        const v4u_ v = *(gv4uu_*)(b + p);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t i = 0; i < 16u && p + i < len; ++i) w[i >> 2] |= (uint32_t)b[p + i] << (8u * (i & 3u));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ uint32_t byte_of(const uint4& h, uint32_t i) {
+    const uint32_t d = i < 4u ? h.x : (i < 8u ? h.y : (i < 12u ? h.z : h.w));
+    return (d >> (8u * (i & 3u))) & 0xFFu;
 }
 
 // The chunk walk of SnappyFrameDecoder.decode (:85-231) from position w.p up to the first header at
@@ -62,17 +79,18 @@ __device__ WalkEnd walk(const uint8_t* __restrict__ b, uint64_t len, Walk& w, ui
         }
         const uint64_t avail = len - p;
         if (avail < 4) break;  // :104-108
-        const uint32_t type = b[p];
-        const uint32_t clen = (uint32_t)b[p + 1] | ((uint32_t)b[p + 2] << 8) | ((uint32_t)b[p + 3] << 16);
+        const uint4 h = hdr16(b, len, p);
+        const uint32_t type = h.x & 0xFFu;
+        const uint32_t clen = h.x >> 8;
         if (type == 0xFFu) {  // STREAM_IDENTIFIER :115-136
             if (clen != 6u) {
                 res = NX_ERR_SNAPPY_STREAM_ID_LENGTH;
                 break;
             }
             if (avail < 10) break;
-            const uint8_t* q = b + p + 4;
             p += 10;  // skipBytes(4 + 6) precede the content check (:124-133)
-            if (q[0] != 's' || q[1] != 'N' || q[2] != 'a' || q[3] != 'P' || q[4] != 'p' || q[5] != 'Y') {
+            if (h.y != 0x50614E73u || (h.z & 0xFFFFu) != 0x5970u) {  // "sNaPpY"
+
                 res = NX_ERR_SNAPPY_STREAM_ID_CONTENT;
                 break;
             }
@@ -113,7 +131,7 @@ __device__ WalkEnd walk(const uint8_t* __restrict__ b, uint64_t len, Walk& w, ui
             uint32_t ulen = 0;
             bool complete = false;
             for (uint32_t i = 0; i < 4u && p + 8 + i < len; ++i) {
-                const uint32_t c = b[p + 8 + i];
+                const uint32_t c = byte_of(h, 8u + i);
                 ulen |= (c & 0x7Fu) << (7u * i);
                 if (!(c & 0x80u)) {
                     complete = true;
@@ -128,7 +146,7 @@ __device__ WalkEnd walk(const uint8_t* __restrict__ b, uint64_t len, Walk& w, ui
                 break;
             }
         }
-        if (!emit(type, p, clen, le32(b + p + 4))) {  // a full list stops the stream before this chunk
+        if (!emit(type, p, clen, h.y)) {  // a full list stops the stream before this chunk
             res = NX_SCAN_LIST_FULL;
             how = kFull;
             break;
@@ -184,8 +202,8 @@ __global__ void __launch_bounds__(256) k_frame_scan(const uint8_t* __restrict__ 
 // Segmented walk of ONE long cumulation (round 5).  The chain is serial — each
 // header gives the next header's position — so a lone lane needs one dependent memory round trip
 // per chunk (~35 K for 1 GiB of 30 KB chunks).  Here the cumulation is cut into segments of SEG bytes:
-//   k_seg_guess  — one wave per segment j >= 1 finds the first position q >= j*SEG from which four
-//                  consecutive hops are plausible data-chunk headers (type 0 or 1, lengths and
+//   k_seg_guess  — one workgroup per segment j >= 1 finds the first position q >= j*SEG from which
+//                  four consecutive hops are plausible data-chunk headers (type 0 or 1, lengths and
 //                  preamble within the decoder's limits).  A guess is only a speculation;
 //   k_seg_count  — one lane per segment walks (walk() above, the exact decoder semantics) from its
 //                  guess (segment 0: from 0 with the caller's state) to the first header at or past
@@ -224,64 +242,86 @@ struct SegPath {
     uint32_t pad[3];
 };
 
-// Is q the start of four consecutive plausible data chunks (type 0 / 1 within the decoder's length
-// limits, a compressed chunk's preamble <= 65536)?  Reaching the end exactly counts as plausible.
-__device__ __forceinline__ bool plausible_run(const uint8_t* __restrict__ b, uint64_t len, uint64_t q) {
-    for (int h = 0; h < 4; ++h) {
-        if (q == len) return true;
-        if (q + 9 > len) return h > 0;
-        const uint32_t type = b[q];
-        const uint32_t clen = (uint32_t)b[q + 1] | ((uint32_t)b[q + 2] << 8) | ((uint32_t)b[q + 3] << 16);
-        if (type > 1u || clen < 5u || (type == 1u && clen > 65540u)) return false;
-        if (type == 0u) {
-            uint32_t ulen = 0, i = 0;
-            for (; i < 3u; ++i) {
-                const uint32_t c = b[q + 8 + i];
-                ulen |= (c & 0x7Fu) << (7u * i);
-                if (!(c & 0x80u)) break;
+// A plausible data-chunk header: type 0 / 1, a length the decoder accepts for that type (a
+// compressed chunk no longer than Snappy's bound for 64 KiB plus its checksum), a compressed chunk's
+// preamble a varint of at most 3 bytes and <= 65536.  Only a speculation filter: the stitch accepts
+// nothing it has not walked exactly.
+constexpr uint32_t kMaxCompChunk = 4u + 32u + 65536u + 65536u / 6u;
+__device__ __forceinline__ bool hop_ok(uint32_t type, uint32_t clen, uint32_t v0, uint32_t v1, uint32_t v2) {
+    if (type > 1u || clen < 5u || clen > (type ? 65540u : kMaxCompChunk)) return false;
+    if (type == 0u) {
+        uint32_t ulen = v0 & 0x7Fu;
+        if (v0 & 0x80u) {
+            ulen |= (v1 & 0x7Fu) << 7;
+            if (v1 & 0x80u) {
+                if (v2 & 0x80u) return false;
+                ulen |= v2 << 14;
             }
-            if (i == 3u || ulen > 65536u) return false;
         }
-        q += 4ull + clen;
-        if (q > len) return h > 0;
+        if (ulen > 65536u) return false;
     }
     return true;
 }
 
-// One wave per segment j >= 1: the first plausible position in [j*seg, j*seg + kGuessWindow).  The
-// wave stages 4 KiB of the segment in LDS at a time; lane l tests positions q0 + l + 64 t in rounds
-// t = 0..63 (a header byte and its length from LDS), the few that pass that first check follow their
-// hops in HBM, and the lowest passing position of the first round with one wins.
-__global__ void __launch_bounds__(64) k_seg_guess(const uint8_t* __restrict__ b, uint64_t len, uint64_t seg, uint32_t nseg,
-                                                  SegInfo* __restrict__ info) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[4096 + 64];
+// Do the chunks after the one at q (of total size 4 + clen) continue plausibly for three more hops?
+// Reaching the end exactly counts as plausible.
+__device__ __forceinline__ bool plausible_tail(const uint8_t* __restrict__ b, uint64_t len, uint64_t q) {
+    for (int h = 1; h < 4; ++h) {
+        if (q == len) return true;
+        if (q > len) return h > 1;  // the candidate's own chunk must fit; a later one may be cut off
+        if (q + 9 > len) return true;
+        const uint4 x = hdr16(b, len, q);
+        const uint32_t type = x.x & 0xFFu, clen = x.x >> 8;
+        if (!hop_ok(type, clen, x.z & 0xFFu, (x.z >> 8) & 0xFFu, (x.z >> 16) & 0xFFu)) return false;
+        q += 4ull + clen;
+    }
+    return true;
+}
+
+// One workgroup (4 waves) per segment j >= 1: the first plausible position in [j*seg, j*seg +
+// kGuessWindow).  Each wave stages a 16 KiB window of the segment in LDS (16-byte loads), so the
+// workgroup covers 64 KiB per pass; lane l tests positions 64 t + l of its wave's window against the
+// whole first-hop rule from LDS, follows the rare survivors' next three hops in HBM, and keeps its
+// lowest; the workgroup's lowest wins.
+constexpr uint32_t kGuessWin = 16384;
+__global__ void __launch_bounds__(256) k_seg_guess(const uint8_t* __restrict__ b, uint64_t len, uint64_t seg, uint32_t nseg,
+                                                   SegInfo* __restrict__ info) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[4][kGuessWin + 16];
+    __shared__ unsigned long long best;
     const uint32_t j = blockIdx.x + 1u;
     if (j >= nseg) return;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t lo = (uint64_t)j * seg;
     const uint64_t hi = min(len, lo + (uint64_t)kGuessWindow);
-    uint64_t found = kNone;
-    for (uint64_t q0 = lo; q0 < hi && found == kNone; q0 += 4096) {
-        __syncthreads();
-        for (uint32_t i = lane; i < 4096u + 64u; i += 64u) win[i] = q0 + i < len ? b[q0 + i] : 0u;
-        __syncthreads();
-        for (uint32_t t = 0; t < 64u; ++t) {
-            const uint32_t o = 64u * t + lane;
-            const uint64_t q = q0 + o;
-            bool ok = false;
-            if (q < hi) {
-                const uint32_t type = win[o];
-                const uint32_t clen = (uint32_t)win[o + 1] | ((uint32_t)win[o + 2] << 8) | ((uint32_t)win[o + 3] << 16);
-                if (type <= 1u && clen >= 5u) ok = plausible_run(b, len, q);
-            }
-            const uint64_t m = __ballot(ok);
-            if (m) {
-                found = q0 + 64u * t + (uint64_t)__ffsll((long long)m) - 1u;
-                break;
+    if (threadIdx.x == 0) best = kNone;
+    uint8_t* w8 = win[wv];
+    for (uint64_t pass = lo; pass < hi; pass += 4ull * kGuessWin) {
+        const uint64_t q0 = pass + (uint64_t)wv * kGuessWin;
+        if (q0 < hi) {
+            for (uint32_t u = lane; u <= kGuessWin / 16u; u += 64u) {
+                const uint4 d = hdr16(b, len, q0 + 16ull * u);
+                *reinterpret_cast<uint4*>(w8 + 16u * u) = d;
             }
         }
+        __syncthreads();
+        uint64_t mine = kNone;
+        if (q0 < hi) {
+            const uint32_t nq = (uint32_t)min((uint64_t)kGuessWin, hi - q0);
+            for (uint32_t o = lane; o < nq; o += 64u) {
+                const uint32_t type = w8[o];
+                const uint32_t clen = (uint32_t)w8[o + 1] | ((uint32_t)w8[o + 2] << 8) | ((uint32_t)w8[o + 3] << 16);
+                if (hop_ok(type, clen, w8[o + 8], w8[o + 9], w8[o + 10]) && q0 + o + 9 <= len &&
+                    plausible_tail(b, len, q0 + o + 4ull + clen)) {
+                    mine = q0 + o;
+                    break;
+                }
+            }
+        }
+        if (mine != kNone) atomicMin(&best, (unsigned long long)mine);
+        __syncthreads();
+        if (best != kNone) break;
     }
-    if (lane == 0) info[j].entry = found;
+    if (threadIdx.x == 0) info[j].entry = best;
 }
 
 __global__ void __launch_bounds__(256) k_seg_count(const uint8_t* __restrict__ b, uint64_t len, uint64_t seg, uint32_t nseg,
@@ -317,31 +357,75 @@ __global__ void __launch_bounds__(256) k_seg_count(const uint8_t* __restrict__ b
     info[j] = I;
 }
 
-// One workgroup: follows the true chain through the segments (in LDS), re-walking any segment whose
-// speculative walk did not start where the chain entered it, prefix-sums the accepted segments'
-// counts and claims list entries as the lane walk would (one per data chunk until the list is full).
+// One workgroup: follows the true chain through the segments (in LDS).  The straight prefix — segments
+// 0..J whose walks each ended in the next segment exactly where its guess started — is found and
+// prefix-summed in parallel; from J on, one lane follows the chain, re-walking any segment whose
+// speculative walk did not start where the chain entered it.  Then list entries are claimed as the
+// lane walk would (one per data chunk until the list is full).
 __global__ void __launch_bounds__(256) k_seg_stitch(const uint8_t* __restrict__ b, uint64_t len, uint64_t seg, uint32_t nseg,
                                                     SegInfo* __restrict__ info, SegStep* __restrict__ path, SegPath* __restrict__ P,
                                                     uint32_t* __restrict__ counts, uint32_t cap, uint32_t* __restrict__ state_p,
                                                     uint64_t* __restrict__ consumed_p, int32_t* __restrict__ status_p) {
     __shared__ SegInfo si[kSegMax];
-    for (uint32_t i = threadIdx.x; i < nseg; i += blockDim.x) si[i] = info[i];
-    __syncthreads();
-    if (threadIdx.x != 0) return;
+    __shared__ uint32_t first_bad;
+    __shared__ uint32_t s0[256], s1[256];
+    const uint32_t t = threadIdx.x;
     const uint32_t st_in = *state_p;
-    P->state_in = st_in;
     if ((st_in >> 1) & 1u) {  // corrupted (:86-89): everything readable is discarded
-        P->nseg = 0;
-        *consumed_p = len;
-        *status_p = NX_OK;
+        if (t == 0) {
+            P->state_in = st_in;
+            P->nseg = 0;
+            *consumed_p = len;
+            *status_p = NX_OK;
+        }
         return;
     }
-    uint32_t j = 0, np = 0, c0 = 0, c1 = 0;
+    for (uint32_t i = t; i < nseg; i += blockDim.x) si[i] = info[i];
+    if (t == 0) first_bad = nseg - 1u;
+    __syncthreads();
+    for (uint32_t i = t; i + 1u < nseg; i += blockDim.x) {
+        const SegInfo& c = si[i];
+        const bool straight = c.how == kOpen && c.exit / seg == (uint64_t)(i + 1u) && si[i + 1u].entry == c.exit;
+        if (!straight) atomicMin(&first_bad, i);
+    }
+    __syncthreads();
+    const uint32_t J = first_bad;
+    // inclusive prefix sums over segments 0..J: four per thread, then a scan of the 256 partials
+    uint32_t a0 = 0, a1 = 0;
+    for (uint32_t k = 0; k < 4u; ++k) {
+        const uint32_t i = 4u * t + k;
+        if (i <= J && i < nseg) {
+            a0 += si[i].ncomp;
+            a1 += si[i].nunc;
+        }
+    }
+    s0[t] = a0;
+    s1[t] = a1;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256u; d <<= 1) {
+        const uint32_t x0 = t >= d ? s0[t - d] : 0u, x1 = t >= d ? s1[t - d] : 0u;
+        __syncthreads();
+        s0[t] += x0;
+        s1[t] += x1;
+        __syncthreads();
+    }
+    {
+        uint32_t c0 = s0[t] - a0, c1 = s1[t] - a1;  // exclusive: before segment 4t
+        for (uint32_t k = 0; k < 4u; ++k) {
+            const uint32_t i = 4u * t + k;
+            if (i <= J && i < nseg) {
+                path[i] = SegStep{i, c0, c1, 0u};
+                c0 += si[i].ncomp;
+                c1 += si[i].nunc;
+            }
+        }
+    }
+    __syncthreads();
+    if (t != 0) return;
+    P->state_in = st_in;
+    uint32_t j = J, np = J + 1u, c0 = s0[255], c1 = s1[255];
     for (;;) {
         const SegInfo& cur = si[j];
-        path[np++] = SegStep{j, c0, c1, 0u};
-        c0 += cur.ncomp;
-        c1 += cur.nunc;
         if (cur.how != kOpen) break;
         const uint32_t nj = (uint32_t)min((uint64_t)(nseg - 1u), cur.exit / seg);
         if (si[nj].entry != cur.exit) {  // a wrong or missing guess: walk it from the true position
@@ -365,6 +449,9 @@ __global__ void __launch_bounds__(256) k_seg_stitch(const uint8_t* __restrict__ 
             info[nj] = R;
         }
         j = nj;
+        path[np++] = SegStep{j, c0, c1, 0u};
+        c0 += si[j].ncomp;
+        c1 += si[j].nunc;
     }
     const uint32_t tot = c0 + c1;
     const uint32_t used = counts[2];
@@ -465,13 +552,22 @@ extern "C" int32_t nx_snappy_frame_scan_long(const uint8_t* in, uint64_t len, ui
     uint64_t seg = kSegBytes;
     while ((len + seg - 1) / seg > kSegMax) seg *= 2;
     const uint32_t nseg = len ? (uint32_t)((len + seg - 1) / seg) : 1u;
+    static std::once_flag keep;  // keep freed stream-ordered scratch in the pool rather than returning it at each sync
+    std::call_once(keep, [] {
+        int dev = 0;
+        hipMemPool_t pool = nullptr;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+            uint64_t thr = 64ull << 20;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        }
+    });
     void* scratch = nullptr;
     const size_t sb = sizeof(SegInfo) * nseg + sizeof(SegStep) * nseg + sizeof(SegPath);
     NX_HIP_CHECK(hipMallocAsync(&scratch, sb, st));
     SegInfo* info = static_cast<SegInfo*>(scratch);
     SegStep* path = reinterpret_cast<SegStep*>(info + nseg);
     SegPath* P = reinterpret_cast<SegPath*>(path + nseg);
-    if (nseg > 1) hipLaunchKernelGGL(k_seg_guess, dim3(nseg - 1), dim3(64), 0, st, in, len, seg, nseg, info);
+    if (nseg > 1) hipLaunchKernelGGL(k_seg_guess, dim3(nseg - 1), dim3(256), 0, st, in, len, seg, nseg, info);
     hipLaunchKernelGGL(k_seg_count, dim3((nseg + 255) / 256), dim3(256), 0, st, in, len, seg, nseg, state, info);
     hipLaunchKernelGGL(k_seg_stitch, dim3(1), dim3(256), 0, st, in, len, seg, nseg, info, path, P, counts, cap, state, consumed,
                        status);

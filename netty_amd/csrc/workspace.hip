@@ -203,7 +203,10 @@ extern "C" int32_t nx_workspaces_trim(void) {
         nx::SharedWs& W = nx::shared_ws((nx::WsKind)k, dev);
         std::lock_guard<std::mutex> lk(W.mu);
         W.kept = false;
-        if (W.owners == 0 && nx::ws_drop(W) != hipSuccess) r = NX_ERR_HIP;
+        if (W.owners == 0) {
+            const hipError_t e = nx::ws_drop(W);
+            if (e != hipSuccess) r = nx_hip_fail(e, __FILE__, __LINE__ + k * 1000);  // line + 1000 * kind under NX_HIP_DEBUG
+        }
     }
     return r;
 }

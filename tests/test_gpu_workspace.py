@@ -149,7 +149,8 @@ def test_batcher_large_flushes_on_all_streams_one_workspace(nx, B, oracle):
 
 
 def test_record_part_leases_overlap_streams(nx, B, oracle):
-    """The decoder's record workspace is leased by part (a ring of frame slots): batches on different
+    """(The parse/expand pair: below 32 768 frames "auto" takes the fused decoder, which uses no
+    record workspace.)  The decoder's record workspace is leased by part (a ring of frame slots): batches on different
     streams take disjoint slots and run together, a batch that wraps onto slots still in use waits
     for their batch.  Twelve decodes over four streams, launched back to back with no host sync,
     against a 3000-slot workspace (three 1000-frame batches fit, the fourth reuses the first's
@@ -169,7 +170,7 @@ def test_record_part_leases_overlap_streams(nx, B, oracle):
     eoff = torch.arange(3000, dtype=torch.int64, device=dev) * cap
     elen, est = B.snappy_encode(src, off, ln, enc, eoff)
     dec = torch.zeros_like(src)
-    r = B.snappy_decode(enc, eoff, elen, dec, off)  # grows the workspace to 3000 slots
+    r = B.snappy_decode(enc, eoff, elen, dec, off, variant="pair")  # grows the workspace to 3000 slots
     torch.cuda.synchronize()
     assert int((est != 0).sum()) == 0 and int((r["status"] != 0).sum()) == 0 and torch.equal(dec, src)
     assert B.workspace_info(B.WS_DEC_RECORDS)[0] >= 3000 * 16384 * 4
@@ -181,7 +182,7 @@ def test_record_part_leases_overlap_streams(nx, B, oracle):
         part = slice(1000 * (k % 3), 1000 * (k % 3 + 1))
         o = bufs[k]
         with torch.cuda.stream(streams[k % 4]):
-            res = B.snappy_decode(enc, eoff[part], elen[part], o, off[part])
+            res = B.snappy_decode(enc, eoff[part], elen[part], o, off[part], variant="pair")
         outs.append((part, o, res, streams[k % 4]))
     torch.cuda.synchronize()
     for part, o, res, s in outs:
