@@ -1552,6 +1552,13 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
     // one lane, ~4-7 ms for any batch that does not fill the chip, while k_decode_fused parses each
     // frame wave-parallel (0.85 ms for one frame, 1.9 ms for 4 096, 5.6 ms for 16 384, against 4.3 /
     // 7.4 / 9.1 for the pair).  The pair wins from ~34 K frames on (65 536: 16.4 vs 20.5 ms).
+    static const int forced = [] {  // NX_DECODE_MODE=pair|fused overrides "auto" (A/B runs of callers such as the batcher)
+        const char* e = getenv("NX_DECODE_MODE");
+        if (e && strcmp(e, "pair") == 0) return (int)kDecodePair;
+        if (e && strcmp(e, "fused") == 0) return (int)kDecodeFused;
+        return (int)kDecodeAuto;
+    }();
+    if (mode == kDecodeAuto) mode = forced;
     const bool fused_only = mode == kDecodeFused || (mode == kDecodeAuto && n <= kFusedMaxFrames);
     if (fused_only) {
         hipLaunchKernelGGL(k_decode_fused, dim3(wave_grid(n)), dim3(kWaves * 64), lds, st, in, in_off, in_len, out, out_off, out_cap,

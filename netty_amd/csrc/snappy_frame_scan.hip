@@ -19,6 +19,7 @@
 // [cap - counts[1], cap).  Entries are claimed with atomics, so their order across streams is not
 // fixed; chunk_stream / chunk_seq give each entry's stream and its position among that stream's
 // data chunks.
+#include <stdio.h>
 #include <stdlib.h>
 #include <mutex>
 #include <vector>
@@ -239,7 +240,7 @@ struct SegPath {
     uint32_t base0, base1; // list slots of the stream's first compressed / uncompressed entry
     uint32_t limit;        // data chunks that get entries (fewer than the chain's when the list fills)
     uint32_t state_in;     // the cumulation's decoder state before the walk
-    uint32_t pad[3];
+    uint32_t stats[3];     // diagnostics (NX_SCAN_STATS): straight prefix J, parallel re-walks, serial re-walks
 };
 
 // A plausible data-chunk header: type 0 / 1, a length the decoder accepts for that type (a
@@ -380,7 +381,51 @@ __global__ void __launch_bounds__(256) k_seg_stitch(const uint8_t* __restrict__ 
         }
         return;
     }
+    __shared__ uint32_t nfix;
     for (uint32_t i = t; i < nseg; i += blockDim.x) si[i] = info[i];
+    if (t == 0) nfix = 0;
+    __syncthreads();
+    // a wrong or missing guess for segment i + 1 whose predecessor's walk ended inside it: re-walk it
+    // from there, all such segments at once (twice, for a fix whose own exit then disagrees); the
+    // serial pass below accepts a segment only where the chain really enters it
+    for (int it = 0; it < 2; ++it) {
+        bool fix = false;
+        uint32_t fi = 0;
+        for (uint32_t i = t; i + 1u < nseg; i += blockDim.x) {
+            const SegInfo& c = si[i];
+            if (c.how == kOpen && c.exit / seg == (uint64_t)(i + 1u) && si[i + 1u].entry != c.exit && !fix) {
+                fix = true;
+                fi = i;
+            }
+        }
+        __syncthreads();
+        SegInfo R;
+        if (fix) {
+            const SegInfo& c = si[fi];
+            Walk w{c.exit, 0, c.started != 0, NX_OK};
+            uint32_t nc = 0, nu = 0;
+            const uint64_t stop = fi + 2u < nseg ? (uint64_t)(fi + 2u) * seg : ~0ull;
+            R.how = walk(b, len, w, stop, [&](uint32_t type, uint64_t, uint32_t, uint32_t) {
+                (type == 0u ? nc : nu) += 1u;
+                return true;
+            });
+            R.entry = c.exit;
+            R.exit = w.p;
+            R.skip = w.skip;
+            R.res = w.res;
+            R.started = w.started;
+            R.ncomp = nc;
+            R.nunc = nu;
+            R.pad = 0;
+        }
+        __syncthreads();  // every fixing thread has read its predecessor before any segment changes
+        if (fix) {
+            si[fi + 1u] = R;
+            info[fi + 1u] = R;
+            atomicAdd(&nfix, 1u);
+        }
+        __syncthreads();
+    }
     if (t == 0) first_bad = nseg - 1u;
     __syncthreads();
     for (uint32_t i = t; i + 1u < nseg; i += blockDim.x) {
@@ -423,6 +468,9 @@ __global__ void __launch_bounds__(256) k_seg_stitch(const uint8_t* __restrict__ 
     __syncthreads();
     if (t != 0) return;
     P->state_in = st_in;
+    P->stats[0] = J;
+    P->stats[1] = nfix;
+    uint32_t nser = 0;
     uint32_t j = J, np = J + 1u, c0 = s0[255], c1 = s1[255];
     for (;;) {
         const SegInfo& cur = si[j];
@@ -447,12 +495,14 @@ __global__ void __launch_bounds__(256) k_seg_stitch(const uint8_t* __restrict__ 
             R.pad = 0;
             si[nj] = R;
             info[nj] = R;
+            ++nser;
         }
         j = nj;
         path[np++] = SegStep{j, c0, c1, 0u};
         c0 += si[j].ncomp;
         c1 += si[j].nunc;
     }
+    P->stats[2] = nser;
     const uint32_t tot = c0 + c1;
     const uint32_t used = counts[2];
     const uint32_t room = used < cap ? cap - used : 0u;
@@ -574,6 +624,14 @@ extern "C" int32_t nx_snappy_frame_scan_long(const uint8_t* in, uint64_t len, ui
     hipLaunchKernelGGL(k_seg_emit, dim3((nseg + 255) / 256), dim3(256), 0, st, in, (uint64_t)0, len, seg, nseg, 0u, info, path, P,
                        data_off, data_len, masked_crc, chunk_stream, chunk_seq, counts, cap, state, consumed, status);
     NX_HIP_CHECK(hipGetLastError());
+    static const bool stats = getenv("NX_SCAN_STATS") != nullptr;
+    if (stats) {  // diagnostics only: synchronous
+        SegPath h{};
+        NX_HIP_CHECK(hipMemcpyAsync(&h, P, sizeof(h), hipMemcpyDeviceToHost, st));
+        NX_HIP_CHECK(hipStreamSynchronize(st));
+        fprintf(stderr, "nx_snappy_frame_scan_long: %u segments, straight prefix to %u, %u parallel and %u serial re-walks, %u on the path\n",
+                nseg, h.stats[0], h.stats[1], h.stats[2], h.nseg);
+    }
     NX_HIP_CHECK(hipFreeAsync(scratch, st));
     return NX_OK;
 }

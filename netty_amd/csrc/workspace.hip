@@ -1,4 +1,6 @@
 // workspace.hip — storage, growth and ownership of the shared device workspaces (workspace.hpp).
+#include <stdio.h>
+#include <stdlib.h>
 #include <algorithm>
 #include "workspace.hpp"
 
@@ -11,8 +13,10 @@ thread_local bool t_no_grow = false;
 // Free W (waits for its last use first: nothing may still read or write it).
 hipError_t ws_drop(SharedWs& W) {
     hipError_t e = hipSuccess;
+    static const bool dbg = getenv("NX_HIP_DEBUG") != nullptr;
     for (const WsUse& u : W.uses) {
         const hipError_t f = hipEventSynchronize(u.ev);
+        if (f != hipSuccess && dbg) fprintf(stderr, "netty_amd: ws_drop: part-use event sync: %s\n", hipGetErrorString(f));
         if (e == hipSuccess) e = f;
         W.spare.push_back(u.ev);
     }
@@ -20,8 +24,10 @@ hipError_t ws_drop(SharedWs& W) {
     W.cursor = 0;
     if (W.p) {
         const hipError_t f = W.used ? hipEventSynchronize(W.ev) : hipSuccess;
+        if (f != hipSuccess && dbg) fprintf(stderr, "netty_amd: ws_drop: last-use event sync: %s\n", hipGetErrorString(f));
         if (e == hipSuccess) e = f;
         const hipError_t g = hipFree(W.p);
+        if (g != hipSuccess && dbg) fprintf(stderr, "netty_amd: ws_drop: hipFree(%p): %s\n", W.p, hipGetErrorString(g));
         if (e == hipSuccess) e = g;
     }
     W.p = nullptr;

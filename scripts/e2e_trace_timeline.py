@@ -9,7 +9,8 @@ import csv
 import os
 import sys
 
-KEEP = ("k_gather_host", "HOST_TO_DEVICE", "k_parse", "k_expand", "k_dec_finish", "DEVICE_TO_HOST")
+KEEP = ("k_gather_host", "HOST_TO_DEVICE", "k_parse", "k_expand", "k_decode_fused", "k_dec_finish", "DEVICE_TO_HOST")
+DECODE = ("k_parse", "k_decode_fused")
 
 
 def main():
@@ -23,7 +24,8 @@ def main():
     for m in csv.DictReader(open(os.path.join(d, "tr_memory_copy_trace.csv"))):
         ev.append((int(m["Start_Timestamp"]), int(m["End_Timestamp"]), m["Stream_Id"], m["Direction"].replace("MEMORY_COPY_", ""), ""))
     ev.sort()
-    parses = [e for e in ev if e[3] == "k_parse"]
+    parses = [e for e in ev if e[3] in DECODE and e[4] != "" and int(e[4]) > 64 * 1024] or [e for e in ev if e[3] in DECODE]
+    a, b = min(a, len(parses) - 1), min(b, len(parses) - 1)
     t0 = parses[a][0] - 12_000_000
     t1 = parses[b][1] + 30_000_000
     sel = [e for e in ev if t0 <= e[0] <= t1 and e[3] in KEEP]
