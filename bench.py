@@ -37,7 +37,11 @@ CHUNK = 65536
 CONFIG5_CHUNKS = 1638400  # 100 GiB of 64 KiB chunks
 # kernels whose PMC traffic backs roofline.traffic; the summary must have been taken on these sources
 PMC_SOURCES = ("netty_amd/csrc/snappy_encode.hip", "netty_amd/csrc/snappy_decode.hip", "netty_amd/csrc/crc32c.hip",
-               "netty_amd/csrc/nx_common.hpp", "netty_amd/csrc/expand_units.hpp")
+               "netty_amd/csrc/nx_common.hpp", "netty_amd/csrc/expand_units.hpp", "netty_amd/csrc/expand_frame.hpp")
+# the alt-codec legs' kernels (their parses share the Snappy decoder's translation unit and expander)
+ALT_PMC_SOURCES = ("netty_amd/csrc/fastlz.hip", "netty_amd/csrc/lzf.hip", "netty_amd/csrc/lz4.hip",
+                   "netty_amd/csrc/snappy_decode.hip", "netty_amd/csrc/nx_common.hpp", "netty_amd/csrc/expand_units.hpp",
+                   "netty_amd/csrc/expand_frame.hpp")
 
 
 def parse(argv=None):
@@ -205,12 +209,33 @@ def config4_cpu(O, seconds: float):
 
 
 # ---------------------------------------------------------------------------------------- PMC traffic
-def source_digest() -> str:
+def source_digest(paths=PMC_SOURCES) -> str:
     h = hashlib.sha256()
-    for p in PMC_SOURCES:
+    for p in paths:
         with open(os.path.join(ROOT, p), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
+
+
+def alt_source_digest() -> str:
+    return source_digest(ALT_PMC_SOURCES)
+
+
+def load_alt_traffic():
+    """HBM bytes per call of each alt-codec leg's encode / decode from the newest committed
+    alt_traffic.json (scripts/pmc_alt_traffic.sh) taken on these kernel sources, else (None, reason)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", "alt_traffic.json"), recursive=True),
+                   key=os.path.getmtime)
+    want = alt_source_digest()
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("source_digest") == want:
+            return d["legs"], os.path.relpath(f, ROOT)
+    return None, f"no alt-codec PMC summary for kernel sources {want} (run scripts/pmc_alt_traffic.sh)"
 
 
 def load_traffic():
@@ -739,9 +764,23 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2, hc_n: int = 1024):
            "roofline_note": "per leg: algorithmic bytes U + C (uncompressed + compressed, SURVEY.md section 8d) / the "
                             "leg's HIP-event time, against 8 TB/s HBM"}
 
-    def roof(nbytes, ms):
+    alt_tr, alt_src = load_alt_traffic()
+    res["traffic_source"] = alt_src
+
+    def roof(nbytes, ms, leg=None, phase=None):
+        """algorithmic bytes / time against HBM peak; with a digest-matched PMC summary (taken over this
+        same leg at the default --alt-chunks), also the measured HBM bytes per call and the fraction of
+        HBM bandwidth they occupied over the call's time"""
         a = nbytes / (ms / 1e3) / 1e9
-        return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBS, 4)}
+        r = {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBS, 4)}
+        t = (alt_tr or {}).get(leg, {}).get(phase)
+        if t and n == 262144:
+            hb = t["hbm_bytes_per_call"]
+            r.update({"traffic": round(hb), "traffic_per_chunk": round(hb / n), "traffic_over_algorithmic": round(hb / nbytes, 2),
+                      "traffic_frac": round(hb / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)})
+        else:
+            r["traffic"] = None
+        return r
 
     def same(rows, lens):
         """every decoded chunk equals its source (rows: chunk indices), 16384 chunks at a time"""
@@ -790,7 +829,8 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2, hc_n: int = 1024):
         C = int(flen.to(torch.int64).sum())
         res[f"fastlz_l{level}"] = {"encode_gib_s": round(U / te * 1e3 / 2**30, 3), "decode_gib_s": round(U / td * 1e3 / 2**30, 3),
                                    "ratio": round(C / U, 4), "verified": ok,
-                                   "roofline_encode": roof(U + C, te), "roofline_decode": roof(U + C, td)}
+                                   "roofline_encode": roof(U + C, te, f"fastlz_l{level}", "encode"),
+                                   "roofline_decode": roof(U + C, td, f"fastlz_l{level}", "decode")}
     del fout
     lcap = (B.lzf_max_compressed_length(CH) + 15) // 16 * 16
     lout = torch.empty(n * lcap, dtype=torch.uint8, device=dev)
@@ -823,7 +863,8 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2, hc_n: int = 1024):
     res["lzf"] = {"encode_gib_s": round(U / te * 1e3 / 2**30, 3),
                   "decode_gib_s": round(Ud / td * 1e3 / 2**30, 3) if idx.numel() else None,
                   "decoded_chunks": int(idx.numel()), "ratio": round(Cl / U, 4), "verified": ok,
-                  "roofline_encode": roof(U + Cl, te), "roofline_decode": roof(Ud + Cd, td) if idx.numel() else None}
+                  "roofline_encode": roof(U + Cl, te, "lzf", "encode"),
+                  "roofline_decode": roof(Ud + Cd, td, "lzf", "decode") if idx.numel() else None}
     del lout
     # LZ4 blocks (§8f row 4): GPU block encoder, then decode through the parse/expand kernels
     zcap = (B.lz4_max_compressed_length(CH) + 15) // 16 * 16
@@ -845,7 +886,7 @@ def bench_alt_codecs(torch, B, dev, n: int, reps: int = 2, hc_n: int = 1024):
     Cz = int(zlen.to(torch.int64).sum())
     res["lz4"] = {"encode_gib_s": round(U / te * 1e3 / 2**30, 3), "decode_gib_s": round(U / td * 1e3 / 2**30, 3),
                   "ratio": round(Cz / U, 4), "verified": ok,
-                  "roofline_encode": roof(U + Cz, te), "roofline_decode": roof(U + Cz, td)}
+                  "roofline_encode": roof(U + Cz, te, "lz4", "encode"), "roofline_decode": roof(U + Cz, td, "lz4", "decode")}
     # LZ4 HC (Lz4FrameEncoder(highCompressor = true): LZ4_compress_HC level 9, one lane per block with
     # 256 KiB of hash/chain tables in HBM) on the first hc_n chunks of the same mix; decoded back
     hn = min(n, hc_n)

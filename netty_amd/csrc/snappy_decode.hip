@@ -40,6 +40,7 @@
 // read once (4 B per tag) + output written once (+ far-copy re-reads, mostly served from MALL).
 #include <stddef.h>
 #include <stdlib.h>
+#include <type_traits>
 #include <string.h>
 #include <algorithm>
 #include <map>
@@ -808,6 +809,70 @@ struct BurstWinT {
 using BurstWin = BurstWinT<4>;
 static_assert(BurstWin::kStride == kWinDw, "k_parse window stride");
 
+// Line window (NX_PARSE_LINE): the 128-byte line holding the lane's next tag header plus the 16 bytes
+// before it, [B - 16, B + 128) with B a multiple of 128 (origin-relative).  Streaming forward, a reload
+// keeps the previous window's last 16 bytes (an LDS move, not a load) and reads exactly one new line,
+// so each line of the chunk is fetched once; the 64-byte burst window above re-reads the line it sits
+// in at every reload (3.1x read amplification in round 4's PMC).  Twice the bytes per reload, half
+// the reloads.
+struct BurstWinLine {
+    static constexpr int kStride = 37;
+    const uint8_t* origin;
+    uint32_t pad, end;
+    uint32_t lb;  // B: the window is origin-relative [B - 16, B + 128), w[0..3] holding [B - 16, B)
+    uint32_t* w;
+    __device__ __forceinline__ void init(const uint8_t* in, uint32_t length, uint32_t* lds) {
+        origin = reinterpret_cast<const uint8_t*>((uintptr_t)in & ~(uintptr_t)15);
+        pad = (uint32_t)((uintptr_t)in & 15u);
+        end = pad + length;
+        lb = 0xFFFFFF00u;
+        w = lds;
+    }
+    __device__ __forceinline__ bool has(uint32_t p) const {
+        const uint32_t q = p + pad;
+        return q + 16u >= lb && (q + 5u <= lb + 128u || lb + 128u >= end);
+    }
+    __device__ __forceinline__ void load(uint32_t p) {
+        const uint32_t B = (p + pad + 16u) & ~127u;
+        const uint32_t last = (end - 1u) & ~15u;
+        const bool carry = B != 0u && lb + 128u == B;  // streaming on: the carry block is in LDS
+        v4u x[9];
+#pragma unroll
+        for (uint32_t k = 1; k < 9; ++k) {
+            const uint32_t o = B + 16u * (k - 1u);
+            x[k] = *(const gv4u*)(origin + (o <= last ? o : last));
+        }
+        if (carry) {
+            x[0].x = w[32];
+            x[0].y = w[33];
+            x[0].z = w[34];
+            x[0].w = w[35];
+        } else if (B != 0u) {
+            x[0] = *(const gv4u*)(origin + (B - 16u <= last ? B - 16u : last));
+        } else {  // B = 0: nothing precedes the chunk (p >= 0 = B, so these bytes are never read)
+            x[0] = v4u{0u, 0u, 0u, 0u};
+        }
+        lb = B;
+#pragma unroll
+        for (uint32_t k = 0; k < 9; ++k) {
+            w[4 * k] = x[k].x;
+            w[4 * k + 1] = x[k].y;
+            w[4 * k + 2] = x[k].z;
+            w[4 * k + 3] = x[k].w;
+        }
+    }
+    __device__ __forceinline__ uint64_t get8(uint32_t p) const {
+        const uint32_t off = p + pad + 16u - lb;
+        const uint32_t i = off >> 2, s = off & 3u;
+        const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2];
+        return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
+    }
+};
+#ifndef NX_PARSE_LINE
+#define NX_PARSE_LINE 0
+#endif
+using ParseWin = std::conditional_t<NX_PARSE_LINE != 0, BurstWinLine, BurstWin>;
+
 // Record writer: a lane's records gather 16 at a time in its LDS queue row and leave as one 64-byte
 // run (four back-to-back 16-byte stores), so the record slot is written in half-lines the L2 merges
 // instead of scattered partial-line writes.  The row is LDS, not registers: a register queue needs a
@@ -850,7 +915,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
                                                        uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
                                                        uint32_t* __restrict__ out_len, uint32_t* __restrict__ consumed_a,
                                                        int32_t* __restrict__ status, uint32_t n) {
-    __shared__ uint32_t wins[kParseBlock * kWinDw + 4];
+    __shared__ uint32_t wins[kParseBlock * ParseWin::kStride + 4];
     __shared__ __attribute__((aligned(16))) uint32_t recq[kParseBlock * kQDw];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
@@ -861,8 +926,8 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
         status[c] = kNeedFused;
         return;
     }
-    BurstWin win;
-    win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
+    ParseWin win;
+    win.init(in + in_off[c], in_len, &wins[threadIdx.x * ParseWin::kStride]);
     RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
     uint32_t ip = 0, op = 0;
     int32_t st = NX_OK;

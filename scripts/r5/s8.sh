@@ -24,6 +24,8 @@ export TMPDIR=/tmp
 (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$ROOT/$O/trace" -o tr -- \
     "$ROOT/netty_amd/e2e_capi" 256 256 65535 1 0 512 > "$ROOT/$O/trace.log" 2>&1); rc=$?; echo "trace $rc" >> $O/steps.log
 unset GPU_MAX_HW_QUEUES
+N=262144 timeout -k 10 700 bash scripts/pmc_alt_traffic.sh; rc=$?; echo "alt_pmc $rc" >> $O/steps.log; fatal $rc alt_pmc
+mv gpurun_out/alt_traffic.json gpurun_out/alt_traffic_* $O/ 2>/dev/null
 NX_HIP_DEBUG=1 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
     > $O/pytest_gpu.log 2>&1; rc=$?; echo "pytest_gpu $rc" >> $O/steps.log; fatal $rc pytest_gpu
 exit 0
