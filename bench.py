@@ -625,13 +625,15 @@ def device_info(torch, dev):
     return info
 
 
-def e2e_capi(channels: int, messages: int, timeout: float = 240.0, dec_flush_mib: int = 512):
+def e2e_capi(channels: int, messages: int, timeout: float = 240.0, dec_flush_mib: int = 64):
     """Host-to-host Snappy frame round trip through the asynchronous batcher C-ABI
     (netty_amd/tools/e2e_capi.cpp): `channels` SnappyFrameEncoder/Decoder pairs, `messages` 65535-byte
     text messages each in registered host memory; encode in one flush, decode auto-flushed every
     `dec_flush_mib` MiB (the batches rotate over four streams and take disjoint record slots, so one
     batch's PCIe gather and decode overlap the previous one's result writes; round 4, one box:
-    23.3 GiB/s with one flush, 25.3 at 256 MiB, 26.6 at 512 MiB, 23.1 at 1 GiB).  Workspaces and pinned arenas are reserved before the timed rounds;
+    23.3 GiB/s with one flush, 25.3 at 256 MiB, 26.6 at 512 MiB, 23.1 at 1 GiB; round 5, with batches
+    of <= 32 768 frames on the wave-parallel fused decoder: 30.9-31.0 at 64 MiB, 27.5-30.1 at 128,
+    27.3-28.7 at 256, 25.6-26.3 at 512, profiles/r05/s8, s10).  Workspaces and pinned arenas are reserved before the timed rounds;
     `arena_allocs_after_round0` counts pinned allocations after the first round (0: none on the submit
     path).  Run as a child process (its own HIP context); returns its JSON, or the failure."""
     import subprocess

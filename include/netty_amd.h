@@ -443,7 +443,8 @@ int32_t nx_batcher_reserve(nx_batcher* b, uint32_t kinds);
 int32_t nx_batcher_reserve_arenas(nx_batcher* b, uint32_t nbatches, size_t staging_bytes, size_t out_bytes);
 int32_t nx_batcher_arena_stats(nx_batcher* b, uint64_t* allocs, uint64_t* bytes, uint32_t* batches);
 /* Flushes whose results went to host memory by one DMA copy from a device mirror (large batches of
- * decoded messages) instead of through the finish kernels' mapped stores, and the bytes copied. */
+ * decoded messages; one mirror per batcher stream, grown to the largest such flush and kept until
+ * nx_batcher_free) instead of through the finish kernels' mapped stores, and the bytes copied. */
 int32_t nx_batcher_dma_stats(nx_batcher* b, uint64_t* dma_flushes, uint64_t* dma_bytes);
 
 /* The FastLZ, LZF and LZ4 handlers as batcher jobs, with the Snappy jobs' contract (one launch per

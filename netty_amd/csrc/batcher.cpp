@@ -77,7 +77,9 @@ struct DecAct {  // one UNCOMPRESSED_DATA (kind 1) or COMPRESSED_DATA (kind 2) c
     uint32_t cap;     // bytes reserved for its message: kind 2 the preamble's length (capped by the bound)
     uint32_t pad;
 };
-constexpr uint64_t kSpilled = ~0ull;  // DecRes::off of a message longer than its chunk's preamble said
+constexpr uint64_t kSpilled = ~0ull;  // DecRes::off of a message longer than its chunk's preamble said that
+                                      // did not fit the flush's spill area (apply copies it from the slot)
+constexpr uint64_t kSpillBytes = 1ull << 20;  // a flush's spill area (bytes; at most 64 KiB per compressed chunk)
 struct DecJob {
     uint64_t out_off;
     uint32_t a0, na;
@@ -211,7 +213,8 @@ __global__ void __launch_bounds__(256) k_dec_finish(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ dlen, const uint32_t* __restrict__ dcons,
                                                     const int32_t* __restrict__ dstat, const uint32_t* __restrict__ dcrc,
                                                     const uint32_t* __restrict__ ucrc, uint8_t* __restrict__ out,
-                                                    DecRes* __restrict__ res) {
+                                                    DecRes* __restrict__ res, uint64_t spill_off, uint32_t spill_cap,
+                                                    uint32_t* __restrict__ spill_cur) {
     const int lane = threadIdx.x & 63;
     for (uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6); j < njobs; j += gridDim.x * 4) [&] {
         const DecJob J = jobs[j];
@@ -237,13 +240,27 @@ __global__ void __launch_bounds__(256) k_dec_finish(const uint8_t* __restrict__ 
                     R.crc = f[0] | (f[1] << 8) | (f[2] << 16) | ((uint32_t)f[3] << 24);
                 }
                 // a chunk that decodes past its preamble's length (Java allows it up to 65 536 bytes,
-                // SnappyFrameDecoder.java:203) has no room here: apply() copies it from the slot
-                if (R.status == NX_OK && R.len > A.cap) R.off = kSpilled;
-                else if (R.status == NX_OK) wave_copy(out + pos, slots + dslot[A.chunk], R.len, lane);
+                // SnappyFrameDecoder.java:203) has no room here: it goes to the flush's spill area, or,
+                // when that is full, apply() copies it from the slot
+                if (R.status == NX_OK && R.len > A.cap) {
+                    uint32_t at = 0;
+                    if (lane == 0) at = atomicAdd(spill_cur, R.len);
+                    at = (uint32_t)__shfl((int)at, 0);
+                    if ((uint64_t)at + R.len <= spill_cap) {
+                        R.off = spill_off + at;
+                        wave_copy(out + R.off, slots + dslot[A.chunk], R.len, lane);
+                    } else {
+                        R.off = kSpilled;
+                    }
+                    if (lane == 0) res[a] = R;
+                    continue;  // the message reservation holds nothing of it: pos stays
+                } else if (R.status == NX_OK) {
+                    wave_copy(out + pos, slots + dslot[A.chunk], R.len, lane);
+                }
             }
             if (lane == 0) res[a] = R;
             if (R.status != NX_OK) break;
-            if (R.off != kSpilled) pos += R.len;
+            pos += R.len;
         }
     }();
 }
@@ -548,7 +565,7 @@ struct Batch {
     // reservation).  When the known bytes fill most of a large arena the finish kernels write a device
     // mirror instead and one DMA copy moves it (launch_inner).
     uint64_t est_out = 0;
-    nx::h::DevBuf dout;
+    uint64_t res_spill = 0;  // the flush's spill area (decoded messages longer than their preamble said)
     std::vector<uint64_t> dslot_off;  // decode slot of each compressed chunk (device, from slots + eslots)
     std::vector<Job*> jobs;
     nx::h::DevBuf din, slots;
@@ -576,7 +593,7 @@ struct Batch {
         du_off.clear();
         du_len.clear();
         du_direct.clear();
-        out_used = res_enc = res_dec = res_alt = 0;
+        out_used = res_enc = res_dec = res_alt = res_spill = 0;
         est_out = 0;
         dslot_off.clear();
         apc.clear();
@@ -637,6 +654,9 @@ constexpr int kStreams = NX_BATCHER_STREAMS;
 struct nx_batcher {
     std::mutex mu;
     hipStream_t s[kStreams] = {};
+    // DMA result path: one device mirror per stream (flushes on one stream are ordered, so the next
+    // flush on it reuses the mirror after the previous result copy), not one per batch object
+    nx::h::DevBuf dmirror[kStreams];
     int dev = 0;
     uint32_t held = 0;  // bit per nx::WsKind whose shared workspace the batcher holds (workspace.hpp)
     std::deque<Batch*> all;  // every batch object (collecting, in flight, or done)
@@ -1002,6 +1022,12 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
         if (!bt->reserve_out(sizeof(nx::bt::AltRes) * nap + 8, &bt->res_alt)) return NX_ERR_HIP;
     }
     if (!bt->reserve_out(8ull * nej + 8, &bt->res_enc) || !bt->reserve_out(sizeof(DecRes) * nda + 8, &bt->res_dec)) return NX_ERR_HIP;
+    // spill area: a chunk that decodes longer than its preamble said (Java grows its buffer up to
+    // 65 536, SnappyFrameDecoder.java:203) has no room in its message reservation; k_dec_finish moves
+    // it here, so apply() need not copy it from the device (only spills beyond this area do)
+    const uint32_t spill_cap = (uint32_t)std::min<uint64_t>(nx::bt::kSpillBytes, 65536ull * ndc);
+    if (ndc && !bt->reserve_out(spill_cap, &bt->res_spill)) return NX_ERR_HIP;
+    const uint64_t o_spc = Ld.put(4);
     // Where the finish kernels write: straight into the mapped arena (their stores cross PCIe), or,
     // when the expected bytes fill most of a large arena (decoded messages: lengths known from the
     // preambles), into a device mirror that one DMA copy then moves.  The copy engine does not hold
@@ -1009,8 +1035,9 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
     // the finish kernel's host writes ran at 53 GB/s and slowed a concurrent k_parse 2-3x).
     const uint64_t est = bt->est_out + 8ull * nej + sizeof(DecRes) * nda + sizeof(nx::bt::AltRes) * (naj ? bt->apc.size() : 0);
     const bool dma_out = bt->out_used >= nx::bt::kDmaOutMin && est * 5 >= bt->out_used * 4;
-    if (dma_out && !bt->dout.ensure(bt->out_used)) return NX_ERR_HIP;
-    uint8_t* const ob = dma_out ? bt->dout.as<uint8_t>() : bt->out.d;
+    nx::h::DevBuf& mirror = b->dmirror[b->flushes % kStreams];
+    if (dma_out && !mirror.ensure(bt->out_used)) return NX_ERR_HIP;
+    uint8_t* const ob = dma_out ? mirror.as<uint8_t>() : bt->out.d;
     if (!bt->din.ensure(d0 + bt->direct_used + 16) || !bt->slots.ensure(bt->eslots + dslot_bytes + bt->aslots + Ld.at + 128)) return NX_ERR_HIP;
     uint8_t* din = bt->din.as<uint8_t>();
     uint8_t* slots = bt->slots.as<uint8_t>();
@@ -1077,11 +1104,12 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
             if (r != NX_OK) return r;
             b->launches += 1;
         }
+        if (ndc) NX_HIP_CHECK(hipMemsetAsync(D + o_spc, 0, 4, s));
         hipLaunchKernelGGL(nx::bt::k_dec_finish, nx::bt::pcie_grid(ndj), dim3(256), 0, s, din, dslots, (const uint64_t*)(A + o_dslot),
                            (const DecAct*)(A + o_dact),
                            (const DecJob*)(A + o_djob), ndj, (const uint32_t*)(D + o_dlen), (const uint32_t*)(D + o_dcons),
                            (const int32_t*)(D + o_dst), (const uint32_t*)(D + o_dcrc), (const uint32_t*)(D + o_ducrc), ob,
-                           (DecRes*)(ob + bt->res_dec));
+                           (DecRes*)(ob + bt->res_dec), bt->res_spill, ndc ? spill_cap : 0u, (uint32_t*)(D + o_spc));
         NX_HIP_CHECK(hipGetLastError());
         b->launches += 1;
         b->chunks += ndc + ndu;
@@ -1305,7 +1333,7 @@ void apply(nx_batcher* b, Batch* bt) {
                 failed = true;
                 break;
             }
-            if (R.off == nx::bt::kSpilled) {  // longer than its preamble said: from the decode slot (rare, blocking)
+            if (R.off == nx::bt::kSpilled) {  // longer than its preamble said, beyond the spill area: from the decode slot (blocking)
                 j->owned.emplace_back(R.len);
                 const uint8_t* src = bt->slots.as<uint8_t>() + bt->eslots + bt->dslot_off[A.chunk];
                 if (hipMemcpy(j->owned.back().data(), src, R.len, hipMemcpyDeviceToHost) != hipSuccess) {

@@ -573,3 +573,56 @@ def test_batcher_chunk_longer_than_its_preamble(oracle):
         b.wait(t)
         assert b.result(t) == [x, good]
         assert nx.SnappyFrameDecoder(validate).channel_read(stream) == [x, good]
+
+
+def _lying_chunk(oracle, seed, n):
+    """A COMPRESSED_DATA chunk whose preamble declares 10 bytes but whose tags decode to n."""
+    x = oracle.textgen_chunk(seed, n)
+    block = oracle.snappy_encode(x)
+    plen = 1 + (n >= 128) + (n >= 16384)
+    return x, _chunk(0, bytes([10]) + block[plen:], oracle.snappy_checksum(x))
+
+
+def test_batcher_spills_beyond_the_spill_area(oracle):
+    """chunks longer than their preamble go to the flush's 1 MiB spill area in k_dec_finish
+    (no device copy at apply); more than that in one flush falls back to apply's copy from the decode
+    slot.  20 such 64 KiB chunks (1.25 MiB) across channels, between ordinary chunks, in one flush:
+    every message equals the oracle's, both paths taken."""
+    import netty_amd as nx
+    from oracle import frame_decoders as F
+    b = nx.Batcher()
+    chans = []
+    for i in range(20):
+        x, lie = _lying_chunk(oracle, 500 + i, 65536)
+        good = oracle.textgen_chunk(600 + i, 9000)
+        stream = STREAM_ID + lie + oracle.snappy_frame_encode(good, started=True)[0]
+        want = F.run(F.SnappyFrameDecoder(True), [stream])
+        assert want == ([x, good], None)
+        chans.append((nx.SnappyFrameDecoder(True), stream, [x, good]))
+    tickets = [b.submit_decode(d, s) for d, s, _ in chans]
+    b.flush()
+    for (d, s, want), t in zip(chans, tickets):
+        b.wait(t)
+        assert b.result(t) == want
+
+
+def test_batcher_spill_in_a_dma_result_flush(oracle):
+    """a chunk longer than its preamble inside a flush whose results go to host memory by
+    the DMA copy of the stream's device mirror: the spill area is part of the mirror, so the message
+    arrives with the others."""
+    import random
+    import netty_amd as nx
+    rng = random.Random(12)
+    b = nx.Batcher()
+    chans = []
+    for i in range(8):  # ~75 MiB of 64 KiB-chunk messages: the DMA result path
+        data = b"".join(oracle.textgen_chunk(rng.randrange(1 << 20), 65536) for _ in range(150))
+        chans.append((nx.SnappyFrameDecoder(True), oracle.snappy_frame_encode(data)[0], [data]))
+    x, lie = _lying_chunk(oracle, 901, 40000)
+    chans.append((nx.SnappyFrameDecoder(True), STREAM_ID + lie, [x]))
+    tickets = [b.submit_decode(d, s) for d, s, _ in chans]
+    b.flush()
+    for (d, s, want), t in zip(chans, tickets):
+        b.wait(t)
+        assert b"".join(b.result(t)) == b"".join(want)
+    assert b.stats()["dma_flushes"] == 1
