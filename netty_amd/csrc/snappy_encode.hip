@@ -235,8 +235,8 @@ struct StreamWin {
     uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
     uint32_t f0, f1, f2, f3;  // the block after the window (wb + 32), loaded one slide ahead
     __device__ __forceinline__ void init(const uint8_t* in, int32_t length) {
-        origin = reinterpret_cast<const uint8_t*>((uintptr_t)in & ~(uintptr_t)15);
         pad = (uint32_t)((uintptr_t)in & 15u);
+        origin = in - pad;  // pointer arithmetic, not an integer cast: keeps an LDS chunk's address space
         end = pad + (uint32_t)length;
         wb = 0x80000000u;  // empty: q - wb > 27 for every position
     }
