@@ -86,7 +86,8 @@ __global__ void __launch_bounds__(256)
     k_expand_f(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
                uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ rec,
                const uint32_t* __restrict__ nrec, uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-               const uint32_t* __restrict__ expect, uint32_t* __restrict__ crc_out, uint32_t n, const CrcTables* __restrict__ tabs) {
+               const uint32_t* __restrict__ expect, uint32_t* __restrict__ crc_out, uint32_t n, const CrcTables* __restrict__ tabs,
+               uint32_t* __restrict__ need_fused) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const bool do_crc = (expect != nullptr) || (crc_out != nullptr);
     uint32_t* const sT = reinterpret_cast<uint32_t*>(smem);
@@ -122,7 +123,10 @@ __global__ void __launch_bounds__(256)
             if (st == kNeedFused) skip = true;
         }
         if (!skip && Ofin > kFxOut) {  // larger than the window: the fused fallback decodes it
-            if (loader && lane == 0) status[c] = kNeedFused;
+            if (loader && lane == 0) {
+                status[c] = kNeedFused;
+                if (need_fused) *need_fused = 1u;
+            }
             skip = true;
         }
         if (!skip && loader) {

@@ -728,7 +728,10 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
                    uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
                    uint32_t* __restrict__ out_len, uint32_t* __restrict__ consumed, int32_t* __restrict__ status,
                    const uint32_t* __restrict__ expect, uint32_t* __restrict__ crc_out, uint32_t n, const CrcTables* __restrict__ tabs,
-                   int filter) {
+                   int filter, const uint32_t* __restrict__ need) {
+    // the fallback launch of a batch in which no frame was handed over returns at once (need: the
+    // batch's flag, set by whichever kernel marked a frame kNeedFused)
+    if (filter && need && __builtin_nontemporal_load(need) == 0u) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const bool do_crc = (expect != nullptr) || (crc_out != nullptr);
     const WaveSetup s = wave_setup(smem, tabs, do_crc);
@@ -914,7 +917,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
                                                        const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ out_cap,
                                                        uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
                                                        uint32_t* __restrict__ out_len, uint32_t* __restrict__ consumed_a,
-                                                       int32_t* __restrict__ status, uint32_t n) {
+                                                       int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ need_fused) {
     __shared__ uint32_t wins[kParseBlock * ParseWin::kStride + 4];
     __shared__ __attribute__((aligned(16))) uint32_t recq[kParseBlock * kQDw];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -924,6 +927,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
     cap = cap < (1u << 24) ? cap : (1u << 24);
     if (in_len >= (1u << 25)) {  // literal positions need 25 bits
         status[c] = kNeedFused;
+        if (need_fused) *need_fused = 1u;
         return;
     }
     ParseWin win;
@@ -1018,6 +1022,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
     }
     if (st == kNeedFused) {
         status[c] = kNeedFused;
+        if (need_fused) *need_fused = 1u;
         return;
     }
     rw.finish();
@@ -1566,12 +1571,12 @@ static int expander_choice() {
 // one launch of the record expander over m frames
 static hipError_t launch_expand(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
                                 const uint32_t* rec, const uint32_t* nrec, uint32_t* out_len, int32_t* status, const uint32_t* expect,
-                                uint32_t* crc_out, uint32_t m, int cus, hipStream_t st) {
+                                uint32_t* crc_out, uint32_t m, int cus, hipStream_t st, uint32_t* need_fused) {
     using namespace nx::dec;
     if (expander_choice() == 2) {  // one workgroup (two frame windows) per CU
         const uint64_t need = (m + 1u) / 2u, want = (uint64_t)cus;
         hipLaunchKernelGGL(k_expand_f, dim3((unsigned)(need < want ? need : want)), dim3(256), kFxLds, st, in, in_off, in_len, out,
-                           out_off, rec, nrec, out_len, status, expect, crc_out, m, nx::crc_tables_dev());
+                           out_off, rec, nrec, out_len, status, expect, crc_out, m, nx::crc_tables_dev(), need_fused);
         return hipGetLastError();
     }
     if (expander_choice() == 1) {
@@ -1627,7 +1632,7 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
     const bool fused_only = mode == kDecodeFused || (mode == kDecodeAuto && n <= kFusedMaxFrames);
     if (fused_only) {
         hipLaunchKernelGGL(k_decode_fused, dim3(wave_grid(n)), dim3(kWaves * 64), lds, st, in, in_off, in_len, out, out_off, out_cap,
-                           out_len, consumed, status, expected_masked_crc, crc_out, n, nx::crc_tables_dev(), 0);
+                           out_len, consumed, status, expected_masked_crc, crc_out, n, nx::crc_tables_dev(), 0, nullptr);
         NX_HIP_CHECK(hipGetLastError());
         return NX_OK;
     }
@@ -1638,18 +1643,20 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
     const uint32_t sb = n < W.frames ? n : W.frames;  // a held workspace caps the sub-batch
     for (uint32_t base = 0; base < n; base += sb) {
         const uint32_t m = n - base < sb ? n - base : sb;
+        // W.olen[0] (unused by this path): set when any frame of the sub-batch is handed to the fallback
+        NX_HIP_CHECK(hipMemsetAsync(W.olen, 0, sizeof(uint32_t), st));
         hipLaunchKernelGGL(k_parse, dim3((m + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, st, in, in_off + base, in_len + base,
                            out_cap ? out_cap + base : nullptr, W.rec, W.nrec, out_len + base, consumed ? consumed + base : nullptr,
-                           status + base, m);
+                           status + base, m, W.olen);
         NX_HIP_CHECK(hipGetLastError());
         NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W.rec, W.nrec, out_len + base, status + base,
                                    expected_masked_crc ? expected_masked_crc + base : nullptr, crc_out ? crc_out + base : nullptr, m,
-                                   cus, st));
+                                   cus, st, W.olen));
         // frames k_parse could not slot (more than kRecCap records, or input >= 32 MiB)
         hipLaunchKernelGGL(k_decode_fused, dim3(wave_grid(m)), dim3(kWaves * 64), lds, st, in, in_off + base, in_len + base, out,
                            out_off + base, out_cap ? out_cap + base : nullptr, out_len + base, consumed ? consumed + base : nullptr,
                            status + base, expected_masked_crc ? expected_masked_crc + base : nullptr,
-                           crc_out ? crc_out + base : nullptr, m, nx::crc_tables_dev(), 1);
+                           crc_out ? crc_out + base : nullptr, m, nx::crc_tables_dev(), 1, W.olen);
         NX_HIP_CHECK(hipGetLastError());
     }
     return NX_OK;
@@ -1715,7 +1722,7 @@ extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off
         (void)need;
         (void)want;
         NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W->rec, W->nrec, W->olen, status + base, nullptr,
-                                   nullptr, m, cus, st));
+                                   nullptr, m, cus, st, nullptr));
         hipLaunchKernelGGL(k_lz4_serial, dim3((m + 255) / 256), dim3(256), 0, st, in, in_off + base, in_len + base, out_len + base,
                            out, out_off + base, status + base, m);
         NX_HIP_CHECK(hipGetLastError());
@@ -1755,7 +1762,7 @@ int32_t nx::dec::decode_records(RecCodec codec, const uint8_t* in, const uint64_
                                status + base, m);
         NX_HIP_CHECK(hipGetLastError());
         NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W.rec, W.nrec, W.olen, status + base, nullptr,
-                                   nullptr, m, cus, st));
+                                   nullptr, m, cus, st, nullptr));
         NX_HIP_CHECK(after(base, m, W.olen, ctx, st));
     }
     return NX_OK;

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 5 session 15: the pair decode's fallback launch returns at once unless k_parse handed a frame
+# over (a per-sub-batch flag); decoy-chain long-scan test; decode timing; then the main and alt-codec
+# PMC traffic passes again for the changed decoder source.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+ROOT=$(pwd)
+O=gpurun_out/r5s15
+mkdir -p $O
+fatal() { case $1 in 124|134|137|139) echo "fatal rc $1 in $2" >> $O/steps.log; exit $1;; esac; }
+timeout -k 10 500 python -u -m pytest -x -q -p no:cacheprovider --timeout 120 --timeout-method thread tests/test_gpu_snappy.py \
+    tests/test_gpu_decode_fuzz.py tests/test_gpu_frame_scan.py tests/test_gpu_batcher.py tests/test_gpu_lz4.py tests/test_gpu_fastlz_lzf.py \
+    > $O/pytest.log 2>&1; rc=$?; echo "pytest $rc" >> $O/steps.log; fatal $rc pytest; [ $rc -ne 0 ] && exit $rc
+for i in 1 2; do timeout -k 10 120 python -u scripts/dec_time.py 262144 4 > $O/time_$i.log 2>&1; rc=$?; fatal $rc time; done
+CHUNKS=262144 timeout -k 10 700 bash scripts/pmc_traffic.sh; rc=$?; echo "pmc_traffic $rc" >> $O/steps.log; fatal $rc pmc
+mv gpurun_out/pmc_traffic.json gpurun_out/traffic_*.log $O/ 2>/dev/null
+for c in FETCH_SIZE WRITE_SIZE; do mv gpurun_out/traffic_$c $O/ 2>/dev/null; done
+N=262144 timeout -k 10 700 bash scripts/pmc_alt_traffic.sh; rc=$?; echo "alt_pmc $rc" >> $O/steps.log; fatal $rc alt_pmc
+mv gpurun_out/alt_traffic.json gpurun_out/alt_traffic_* $O/ 2>/dev/null
+exit 0

@@ -275,3 +275,62 @@ def test_frame_scan_long_equals_lane_walk(dev, B, oracle):
     got, _, _, _, _ = _scan_long(B, dev, buf, 0, 1 << 16)
     _, r, cnt, per, states = _scan(B, dev, [(buf, 0)], 1 << 16)
     assert [(e[1], e[2], e[3], e[4]) for e in got] == [(e[1], e[2], e[3], e[4]) for e in per[0]]
+
+
+def test_frame_scan_long_decoy_chains(dev, B, oracle):
+    """Guesses that land on chains that are not the stream's: a 2.5 MiB skippable chunk whose payload
+    is itself a valid frame stream (segments inside it guess, walk and link up among themselves), and
+    uncompressed chunks straddling segment starts whose payloads carry chunk headers from the segment
+    start on (each such guess is a plausible 4-hop run, rejected by the stitch's re-walk).  The list,
+    consumed position and state equal the oracle's, and the lane walk's."""
+    rng = random.Random(21)
+    seg = 1 << 20
+
+    def fake(n):
+        """a valid frame stream (no identifier) of about n bytes"""
+        out = b""
+        while len(out) < n:
+            d = oracle.textgen_chunk(rng.randrange(1 << 20), rng.randint(3000, 9000))
+            out += oracle.snappy_frame_encode(d, started=True)[0]
+        return out
+
+    parts = [ID]
+    size = len(ID)
+
+    def add(b):
+        nonlocal size
+        parts.append(b)
+        size += len(b)
+
+    # ordinary chunks, then a skippable chunk whose payload is a frame stream spanning segments
+    while size < seg + 5000:
+        add(oracle.snappy_frame_encode(oracle.textgen_chunk(rng.randrange(1 << 20), 60000), started=True)[0])
+    decoy = fake((5 << 20) // 2)
+    add(bytes([0x9A]) + len(decoy).to_bytes(3, "little") + decoy)
+    # uncompressed chunks whose payload starts d bytes before a segment start and holds chunk headers
+    # from there on
+    for k in range(4):
+        boundary = (size // seg + 1) * seg
+        d = 3 + k
+        p = boundary - 8 - d
+        while p - size < 4 + 70000:  # ordinary chunks up to within one uncompressed chunk of p
+            add(oracle.snappy_frame_encode(oracle.textgen_chunk(rng.randrange(1 << 20), 60000), started=True)[0])
+            boundary = (size // seg + 1) * seg
+            p = boundary - 8 - d
+        gap = p - size - 4
+        while gap > 0xFFFFFF:
+            add(_skippable(0x85, 0xFFFFFF - 8))
+            gap = p - size - 4
+        add(_skippable(0x85, gap))
+        assert size == p
+        payload = bytes(range(d)) + fake(50000)[:65536 - d]
+        add(bytes([1]) + (len(payload) + 4).to_bytes(3, "little") + oracle.snappy_checksum(payload).to_bytes(4, "little")
+            + payload)
+    end = size // seg * seg + seg + 100000
+    while size < end:
+        add(oracle.snappy_frame_encode(oracle.textgen_chunk(rng.randrange(1 << 20), 60000), started=True)[0])
+    buf = b"".join(parts)
+    got, _ = _check_long(B, dev, oracle, buf)
+    _, r, cnt, per, states = _scan(B, dev, [(buf, 0)], 1 << 16)
+    assert [(e[1], e[2], e[3], e[4]) for e in got] == [(e[1], e[2], e[3], e[4]) for e in per[0]]
+    assert len(got) > 100
