@@ -1500,7 +1500,10 @@ extern "C" void nx_batcher_free(nx_batcher* b) {
     if (!b) return;
     for (int i = 0; i < kStreams; ++i) (void)hipStreamSynchronize(b->s[i]);
     for (Batch* x : b->all) delete x;
-    for (int i = 0; i < kStreams; ++i) (void)hipStreamDestroy(b->s[i]);
+    for (int i = 0; i < kStreams; ++i) {
+        nx::ws_forget_stream(b->s[i]);  // no workspace event may outlive its stream
+        (void)hipStreamDestroy(b->s[i]);
+    }
     for (int k = 0; k < (int)nx::WsKind::Count; ++k)
         if ((b->held >> k) & 1u) nx::ws_unhold((nx::WsKind)k, b->dev);
     delete b;

@@ -61,7 +61,10 @@ struct Gpu {
         if (s) (void)hipStreamSynchronize(s);
         for (int k = 0; k < (int)WsKind::Count; ++k)
             if (held & (1u << k)) ws_unhold((WsKind)k, dev);
-        if (s) (void)hipStreamDestroy(s);
+        if (s) {
+            ws_forget_stream(s);
+            (void)hipStreamDestroy(s);
+        }
     }
     bool h2d(void* d, const void* h, size_t n) { return n == 0 || hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s) == hipSuccess; }
     bool d2h(void* h, const void* d, size_t n) { return n == 0 || hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s) == hipSuccess; }

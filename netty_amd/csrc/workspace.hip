@@ -43,6 +43,7 @@ hipError_t ws_mark(SharedWs& W, hipStream_t st) {
         if (e != hipSuccess) return e;
     }
     W.used = true;
+    W.ev_st = st;
     return hipEventRecord(W.ev, st);
 }
 
@@ -121,7 +122,7 @@ WsLease::~WsLease() {
                 else W_.uses[k++] = u;
             }
             W_.uses.resize(k);
-            W_.uses.push_back({a_, b_, ev});
+            W_.uses.push_back({a_, b_, ev, st_});
             return;
         }
         if (ev) W_.spare.push_back(ev);
@@ -177,6 +178,25 @@ hipError_t WsLease::acquire_part(size_t want, size_t* first, size_t* count) {
         if (e != hipSuccess) return e;
     }
     return W_.used ? hipStreamWaitEvent(st_, W_.ev, 0) : hipSuccess;
+}
+
+void ws_forget_stream(hipStream_t st) {
+    if (!st) return;
+    for (int k = 0; k < (int)WsKind::Count; ++k)
+        for (int d = 0; d < kMaxDevices; ++d) {
+            SharedWs& W = g_ws[k][d];
+            std::lock_guard<std::mutex> lk(W.mu);
+            size_t j = 0;
+            for (const WsUse& u : W.uses) {
+                if (u.st == st) W.spare.push_back(u.ev);
+                else W.uses[j++] = u;
+            }
+            W.uses.resize(j);
+            if (W.used && W.ev_st == st) {
+                W.used = false;  // its work is complete: nothing later needs to wait for it
+                W.ev_st = nullptr;
+            }
+        }
 }
 
 int32_t ws_hold(WsKind k, int dev, uint32_t units, hipStream_t st) {

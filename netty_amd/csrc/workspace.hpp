@@ -38,6 +38,7 @@ constexpr uint32_t kDecMaxFrames = 262144;           // frames per parse/expand 
 struct WsUse {  // an in-flight part lease: slots [a, b), done when ev completes
     size_t a, b;
     hipEvent_t ev;
+    hipStream_t st;  // the stream ev was recorded on (ws_forget_stream)
 };
 struct SharedWs {
     std::mutex mu;
@@ -48,6 +49,7 @@ struct SharedWs {
     size_t slots = 0;    // tables (lanes or waves) or frames
     uint32_t stamp = 0;  // encoders: last stamp used
     hipEvent_t ev = nullptr;
+    hipStream_t ev_st = nullptr;  // the stream ev was last recorded on
     bool used = false;   // ev has been recorded
     int owners = 0;      // batchers and handles holding it
     bool kept = false;   // grown by the standalone API or a reserve: kept until nx_workspaces_trim
@@ -95,6 +97,11 @@ class WsLease {
 // Owners: hold at creation (grows to `units` now), unhold at destruction (the last one frees).
 int32_t ws_hold(WsKind k, int dev, uint32_t units, hipStream_t st);
 void ws_unhold(WsKind k, int dev);
+// A stream the library created is about to be destroyed, and its work is complete (the caller has
+// synchronized it): forget the workspace events recorded on it, so that no later wait or drop
+// touches an event whose stream no longer exists (the HIP runtime looks at that stream's capture
+// state in hipEventSynchronize / hipStreamWaitEvent).
+void ws_forget_stream(hipStream_t st);
 
 // Owner sizes: a handle encodes a message of up to 1024 slices without waiting on another slot; a
 // batcher flush of up to 16384 slices / frames runs at full grid.

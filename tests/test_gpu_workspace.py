@@ -190,3 +190,29 @@ def test_record_part_leases_overlap_streams(nx, B, oracle):
         assert int((res["status"] != 0).sum()) == 0
         assert torch.equal(o[a:b], src[a:b]), part
     B.workspaces_trim()
+
+
+def test_trim_after_batchers_and_handles_are_freed(nx, B, oracle):
+    """Workspace events recorded on a batcher's or a handle's own stream are forgotten when that
+    stream is destroyed (ws_forget_stream): a later trim, grow or lease never waits on an event
+    whose stream is gone (round 5, profiles/r05/s6-s7: nx_workspaces_trim failed with "operation not
+    permitted when stream is capturing" after earlier tests' batchers were freed).  LZ4 frames decode
+    through the record workspace (k_parse_lz4 + the expander) on the batcher's and the handle's
+    streams; each round frees both, then trims."""
+    data = oracle.textgen_chunk(5, 300000)
+    enc = nx.Lz4FrameEncoder(65536)
+    framed = enc.encode(data) + enc.finish_encode()
+    for _ in range(12):
+        b = nx.Batcher()
+        d = nx.Lz4FrameDecoder(True)
+        t = b.submit_decode(d, framed)
+        b.flush()
+        b.wait(t)
+        assert b"".join(b.result(t)) == data
+        h = nx.Lz4FrameDecoder(True)
+        assert b"".join(h.channel_read(framed)) == data
+        del b, d, h
+        _collect(B)
+        B.workspaces_trim()
+        _, owners = B.workspace_info(B.WS_DEC_RECORDS)
+        assert owners == 0
