@@ -63,7 +63,11 @@ int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const 
  * max_chunks chunks now (a server calls it at start-up, before allocating its own buffers, so the
  * placement choice has memory to draw candidates from); kept until trimmed.
  * nx_workspaces_trim frees, on the current device, every workspace no batcher or handle holds.
- * nx_workspace_info reports the bytes and owners of one kind (NX_WS_*). */
+ * nx_workspace_info reports the bytes and owners of one kind (NX_WS_*).
+ * The workspaces remember an event on the stream of each batch call that used them (later batches
+ * wait on it).  A caller that destroys a stream it passed to a batch call first calls
+ * nx_workspaces_forget_stream(stream): it waits for the stream and drops those events, so no later
+ * call waits on an event whose stream is gone.  Batchers and handles do this for their own streams. */
 #define NX_WS_SNAPPY_ENC 0
 #define NX_WS_LZ4_ENC 1
 #define NX_WS_FASTLZ_ENC 2
@@ -72,6 +76,7 @@ int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const 
 #define NX_WS_LZ4HC_ENC 5
 int32_t nx_snappy_encoder_reserve(uint32_t max_chunks, void* stream);
 int32_t nx_workspaces_trim(void);
+int32_t nx_workspaces_forget_stream(void* stream);
 int32_t nx_workspace_info(int32_t kind, uint64_t* bytes, int32_t* owners);
 
 /* Diagnostics (no reference counterpart): the probe times in ms of the candidate workspace placements

@@ -122,6 +122,7 @@ _SIGS = {
     "nx_snappy_encoder_reserve": (i32, [u32, vp]),
     "nx_snappy_encode_placement": (i32, [C.POINTER(C.c_float), i32, C.POINTER(i32), C.POINTER(i32)]),
     "nx_workspaces_trim": (i32, []),
+    "nx_workspaces_forget_stream": (i32, [vp]),
     "nx_workspace_info": (i32, [i32, C.POINTER(C.c_uint64), C.POINTER(i32)]),
     "nx_lzf_decoder_new": (vp, []),
     "nx_lzf_decoder_free": (None, [vp]),

@@ -237,6 +237,15 @@ extern "C" int32_t nx_workspaces_trim(void) {
     return r;
 }
 
+// Before a caller destroys a stream it passed to batch calls (netty_amd.h): wait for it, then drop
+// the workspace events recorded on it.
+extern "C" int32_t nx_workspaces_forget_stream(void* stream) {
+    if (!stream) return NX_OK;  // the null stream is never destroyed
+    NX_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    nx::ws_forget_stream((hipStream_t)stream);
+    return NX_OK;
+}
+
 // Bytes of the workspace of `kind` (NX_WS_* in netty_amd.h) on the current device and its owners.
 extern "C" int32_t nx_workspace_info(int32_t kind, uint64_t* bytes, int32_t* owners) {
     if (kind < 0 || kind >= (int32_t)nx::WsKind::Count || !bytes || !owners) return NX_ERR_INVALID_ARG;
