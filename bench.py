@@ -56,6 +56,8 @@ def parse(argv=None):
                     help="chunks per GPU of the separate configs[1]+[2] leg (0 = skip)")
     ap.add_argument("--weak-steps", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--parity-sample", type=int, default=32768,
+                    help="first-sub-batch chunks the cpu_baseline leg checks against the oracle byte for byte")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (H2D/D2H) end-to-end measurement")
     ap.add_argument("--e2e-channels", type=int, default=256, help="C-ABI end-to-end: channels (handler pairs)")
@@ -87,11 +89,50 @@ def host_cores() -> int:
     return max(1, n)
 
 
-def cpu_baseline(seconds: float):
+def take_gpu_sample(torch, B, leg, k: int):
+    """Every (m // k)-th chunk of the leg's first sub-batch as the GPU left it (compressed bytes and
+    masked CRC32C), on the host: the input of cpu_baseline's parity check.  No oracle here."""
+    lo, m = next(leg.batches())
+    k = max(1, min(k, m))
+    step = m // k
+    idx = torch.arange(0, step * k, step, dtype=torch.int64, device=leg.dev)
+    leg.run_sub(lo, m)  # the first sub-batch's outputs, as the timed steps produce them
+    packed, poff = B.gather(leg.enc, leg.eoff[idx], leg.elen[lo + idx])
+    torch.cuda.synchronize()
+    return {"first": leg.first + lo, "step": step, "index": idx.cpu().tolist(), "bytes": packed.cpu().numpy().tobytes(),
+            "off": poff.cpu().tolist(), "len": leg.elen[lo + idx].cpu().tolist(),
+            "crc": [c & 0xFFFFFFFF for c in leg.crc[lo + idx].cpu().tolist()]}
+
+
+def parity_check(O, sample, threads: int):
+    """The oracle's Snappy.encode and masked CRC32C of each sampled chunk (regenerated from its index,
+    include/netty_amd_textgen.h) against the GPU's bytes, on `threads` host threads."""
+    from concurrent.futures import ThreadPoolExecutor
+    idx, buf = sample["index"], sample["bytes"]
+
+    def one(j):
+        src = O.textgen_chunk(sample["first"] + idx[j], CHUNK)
+        want = O.snappy_encode(src)
+        got = buf[sample["off"][j]:sample["off"][j] + sample["len"][j]]
+        return (got != want), (O.snappy_checksum(src) != sample["crc"][j])
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        res = list(ex.map(one, range(len(idx))))
+    bad = sum(1 for a, _ in res if a)
+    badc = sum(1 for _, c in res if c)
+    return {"chunks": len(idx), "stride": sample["step"], "compressed_bytes": len(buf), "encode_mismatches": bad,
+            "crc_mismatches": badc, "verified": bad == 0 and badc == 0, "seconds": round(time.perf_counter() - t0, 2),
+            "note": "bench workload chunks (first sub-batch, every stride-th) encoded by the GPU in the timed path "
+                    "vs the oracle's Snappy.encode and masked CRC32C, byte for byte"}
+
+
+def cpu_baseline(seconds: float, gpu_sample=None):
     """The oracle (C restatement of Snappy.encode/decode + Crc32c, byte-at-a-time CRC like Crc32c.java)
     timed on this host: encode+CRC then decode+CRC-verify of text-like 64 KiB chunks, one thread per
     available core; plus configs[0] (1 MiB java.util.Random(42) frame round trip) and a per-codec
-    configs[3] sample, single-thread."""
+    configs[3] sample, single-thread.  With `gpu_sample` (take_gpu_sample) the oracle also checks
+    those GPU outputs (`gpu_parity_sample`)."""
     import ctypes as C
     from concurrent.futures import ThreadPoolExecutor
 
@@ -129,12 +170,15 @@ def cpu_baseline(seconds: float):
         counts = list(ex.map(work, [t0 + seconds / 2] * threads))
     t1 = time.perf_counter()
     multi = sum(counts) * CHUNK / (t1 - t0) / 2**30
-    return {"value": round(multi, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/netty_oracle.c encode+CRC32C then decode+verify of text-like 64 KiB chunks, "
-                      f"{sum(counts)} chunks on {threads} threads in {t1 - t0:.1f}s (+ {d1} chunks single-thread)",
-            "single_thread_value": round(single, 4),
-            "config1_frame_round_trip": config1_cpu(O, seconds / 8),
-            "config4_per_codec": config4_cpu(O, seconds / 8)}
+    out = {"value": round(multi, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/netty_oracle.c encode+CRC32C then decode+verify of text-like 64 KiB chunks, "
+                     f"{sum(counts)} chunks on {threads} threads in {t1 - t0:.1f}s (+ {d1} chunks single-thread)",
+           "single_thread_value": round(single, 4),
+           "config1_frame_round_trip": config1_cpu(O, seconds / 8),
+           "config4_per_codec": config4_cpu(O, seconds / 8)}
+    if gpu_sample is not None:
+        out["gpu_parity_sample"] = parity_check(O, gpu_sample, threads)
+    return out
 
 
 def config1_cpu(O, seconds: float):
@@ -582,6 +626,9 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
         leg = wk
     if gpu and rank == 0 and world == 1:
         from netty_amd import batch as B
+        # a strided sample of the first sub-batch's GPU outputs (compressed bytes, masked CRCs), taken to
+        # the host now; the cpu_baseline leg checks it against the oracle byte for byte
+        gpu_sample = None if args.no_cpu_baseline else take_gpu_sample(torch, B, leg, args.parity_sample)
         if not args.no_frame_scan:
             line["frame_scan"] = bench_frame_scan(torch, B, dev, leg, args.scan_chunks, args.scan_per_stream)
             ok = ok and line["frame_scan"]["verified"]
@@ -603,7 +650,8 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
             from netty_amd import pipeline as P
             line["end_to_end_torch_pipeline"] = P.measure(dev, n=args.e2e_chunks, sub=args.e2e_sub)
         if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, gpu_sample)
+            ok = ok and line["cpu_baseline"].get("gpu_parity_sample", {}).get("verified", True)
         line["verified"] = ok
     if rank == 0:
         emit(json.dumps(line))
