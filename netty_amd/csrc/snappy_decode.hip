@@ -874,44 +874,99 @@ struct BurstWinLine {
 #ifndef NX_PARSE_LINE
 #define NX_PARSE_LINE 0
 #endif
-using ParseWin = std::conditional_t<NX_PARSE_LINE != 0, BurstWinLine, BurstWin>;
+#ifndef NX_PARSE_DEFER
+#define NX_PARSE_DEFER 0
+#endif
+#ifndef NX_PARSE_RELOAD_K  // 0: reload when every running lane is out of window (rounds 2-5)
+#define NX_PARSE_RELOAD_K 16
+#endif
 
-// Record writer: a lane's records gather 16 at a time in its LDS queue row and leave as one 64-byte
-// run (four back-to-back 16-byte stores), so the record slot is written in half-lines the L2 merges
-// instead of scattered partial-line writes.  The row is LDS, not registers: a register queue needs a
-// 16-way select per record (32 VALU: v_cmp + v_cndmask per entry), an LDS row one ds_write.
-constexpr int kQDw = 20;  // queue row stride in dwords (16 records; 16-byte aligned rows)
-struct RecWriter {
+
+// Record writer: a lane's records gather QR at a time in its LDS queue row and leave as one run of
+// QR/4 back-to-back 16-byte stores (QR = 16: a 64-byte half-line the L2 merges) instead of scattered
+// partial-line writes.  The row is LDS, not registers: a register queue needs a 16-way select per
+// record (32 VALU: v_cmp + v_cndmask per entry), an LDS row one ds_write.  Rows of QR = 16 are
+// 16-byte aligned (stride 20 dwords); smaller rows take an odd stride (QR + 1: conflict-free writes)
+// and are read back dword by dword.  DEFER: the full row is read into registers at its last record
+// and stored at the next put (or at finish), so the lane does not wait on those LDS reads alone: the
+// next window read's wait covers them (LDS returns in order).
+template <uint32_t QR, bool DEFER = false>
+struct RecWriterT {
+    static_assert(QR == 4 || QR == 8 || QR == 16, "record row");
+    static constexpr uint32_t kStride = QR == 16 ? 20u : QR + 1u;
+    static constexpr uint32_t kV = QR / 4;  // 16-byte stores per row
     uint4* slot;
     uint32_t* q;  // this lane's LDS row
     uint32_t n;   // records emitted
-    __device__ __forceinline__ void flush16(uint32_t base) {
-        const uint4* qq = reinterpret_cast<const uint4*>(q);
-        uint4* d = slot + (base >> 2);
-        d[0] = qq[0];
-        d[1] = qq[1];
-        d[2] = qq[2];
-        d[3] = qq[3];
+    v4u p0, p1, p2, p3;  // DEFER: the row being flushed (native vectors: uint4 members went to scratch)
+    uint32_t pend_at;    // DEFER: its first record index, all ones when none
+    __device__ __forceinline__ RecWriterT(uint4* s, uint32_t* row) : slot(s), q(row), n(0), pend_at(0xFFFFFFFFu) {}
+    __device__ __forceinline__ v4u row(uint32_t k) const {
+        if constexpr (QR == 16) {
+            return reinterpret_cast<const v4u*>(q)[k];
+        } else {
+            return v4u{q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]};
+        }
+    }
+    __device__ __forceinline__ void drain() {
+        if constexpr (DEFER) {
+            if (pend_at != 0xFFFFFFFFu) {
+                v4u* d = reinterpret_cast<v4u*>(slot + (pend_at >> 2));
+                d[0] = p0;
+                if constexpr (kV > 1) d[1] = p1;
+                if constexpr (kV > 2) {
+                    d[2] = p2;
+                    d[3] = p3;
+                }
+                pend_at = 0xFFFFFFFFu;
+            }
+        }
     }
     __device__ __forceinline__ bool put(uint32_t r) {
         if (n >= kRecCap) return false;
-        q[n & 15u] = r;
-        if ((n & 15u) == 15u) flush16(n - 15u);
+        drain();
+        q[n & (QR - 1u)] = r;
+        if ((n & (QR - 1u)) == QR - 1u) {
+            if constexpr (DEFER) {
+                p0 = row(0);
+                if constexpr (kV > 1) p1 = row(1);
+                if constexpr (kV > 2) {
+                    p2 = row(2);
+                    p3 = row(3);
+                }
+                pend_at = n - (QR - 1u);
+            } else {
+                v4u* d = reinterpret_cast<v4u*>(slot + ((n - (QR - 1u)) >> 2));
+#pragma unroll
+                for (uint32_t k = 0; k < kV; ++k) d[k] = row(k);
+            }
+        }
         ++n;
         return true;
     }
     __device__ __forceinline__ void finish() {
-        const uint32_t k = n & 15u;
+        drain();
+        const uint32_t k = n & (QR - 1u);
         if (k) {
-            const uint4* qq = reinterpret_cast<const uint4*>(q);
-            uint4* d = slot + ((n - k) >> 2);
-            d[0] = qq[0];
-            if (k > 4) d[1] = qq[1];
-            if (k > 8) d[2] = qq[2];
-            if (k > 12) d[3] = qq[3];
+            v4u* d = reinterpret_cast<v4u*>(slot + ((n - k) >> 2));
+#pragma unroll
+            for (uint32_t j = 0; j < kV; ++j)
+                if (4u * j < k) d[j] = row(j);
         }
     }
 };
+using RecWriter = RecWriterT<16>;
+constexpr int kQDw = (int)RecWriter::kStride;
+#ifndef NX_PARSE_QR
+#define NX_PARSE_QR 16
+#endif
+#ifndef NX_PARSE_NB
+#define NX_PARSE_NB 4
+#endif
+// k_parse's window and record row (build options; the alt-codec parses keep BurstWin and RecWriter)
+using ParseRec = RecWriterT<NX_PARSE_QR, NX_PARSE_DEFER != 0>;
+using ParseBurst = BurstWinT<NX_PARSE_NB>;
+using ParseWin = std::conditional_t<NX_PARSE_LINE != 0, BurstWinLine, ParseBurst>;
 
 __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ out_cap,
@@ -919,7 +974,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
                                                        uint32_t* __restrict__ out_len, uint32_t* __restrict__ consumed_a,
                                                        int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ need_fused) {
     __shared__ uint32_t wins[kParseBlock * ParseWin::kStride + 4];
-    __shared__ __attribute__((aligned(16))) uint32_t recq[kParseBlock * kQDw];
+    __shared__ __attribute__((aligned(16))) uint32_t recq[kParseBlock * ParseRec::kStride];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
     const uint32_t in_len = in_len_a[c];
@@ -932,7 +987,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
     }
     ParseWin win;
     win.init(in + in_off[c], in_len, &wins[threadIdx.x * ParseWin::kStride]);
-    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
+    ParseRec rw(reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * ParseRec::kStride]);
     uint32_t ip = 0, op = 0;
     int32_t st = NX_OK;
     bool run = false;
@@ -961,64 +1016,76 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
         }
     }
     // ---- tags (:328-392, decodeLiteral :454-494, decodeCopyWith*ByteOffset :509-626, validateOffset :637-650)
+    // one tag at ip (in the window), branch-free: both interpretations are computed and selected by the type
+    auto step = [&]() {
+        const uint64_t v = win.get8(ip);
+        const uint32_t tag = (uint32_t)v & 0xFFu;
+        const uint32_t ops = (uint32_t)(v >> 8);  // operand bytes (valid where < in_len)
+        const uint32_t after_tag = ip + 1u;
+        const uint32_t avail = in_len - after_tag;
+        const uint32_t type = tag & 3u;
+        const bool isl = type == 0u;
+        const uint32_t code = tag >> 2;
+        // literal (decodeLiteral): nb length bytes after the tag, Java int length + 1
+        const uint32_t nb = (isl && code >= 60u) ? code - 59u : 0u;
+        const uint32_t fmask = nb >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
+        const uint32_t lj = nb == 0u ? code + 1u : (ops & fmask) + 1u;
+        // copy (decodeCopyWith{1,2,4}ByteOffset)
+        const uint32_t csize = type == 1u ? 1u : (type == 2u ? 2u : 4u);
+        const uint32_t clen = type == 1u ? 4u + (code & 7u) : 1u + code;
+        const uint32_t coff = type == 1u ? (((tag & 0xe0u) << 3) | (ops & 0xFFu)) : (type == 2u ? (ops & 0xFFFFu) : ops);
+        const uint32_t hdr = isl ? nb : csize;
+        const uint32_t dpos = after_tag + hdr;
+        const bool lneg = isl && (int32_t)lj < 0;
+        // NOT_ENOUGH_INPUT (silent stop, the tag byte consumed): operands, or the literal's bytes
+        const bool nei = avail < hdr || (isl && !lneg && in_len - dpos < lj);
+        const uint32_t len = isl ? lj : clen;
+        // any error: a negative literal length; an offset of zero, negative or beyond the output
+        // (coff - 1 >= op covers all three: op <= cap < 2^31); the output limit (op <= cap: no wrap)
+        const bool bad = (uint32_t)(isl ? lneg : coff - 1u >= op) | (uint32_t)(len > cap - op);  // (no short circuit: selects)
+        if (nei | bad) {  // rare: the frame stops here, with Java's check order for the error code
+            const int32_t cerr = coff == 0u ? NX_ERR_SNAPPY_OFFSET_ZERO
+                                            : ((int32_t)coff < 0 ? NX_ERR_SNAPPY_OFFSET_NEGATIVE : (coff > op ? NX_ERR_SNAPPY_OFFSET_BEYOND : 0));
+            const int32_t terr = isl ? (lneg ? NX_ERR_SNAPPY_LITERAL_LEN_INVALID : 0) : cerr;
+            ip = nei ? after_tag : dpos;
+            st = nei ? NX_OK : (terr != 0 ? terr : NX_ERR_SNAPPY_OUTPUT_OVERFLOW);
+            run = false;
+            return;
+        }
+        const uint32_t m0 = lj < 64u ? lj : 64u;
+        const uint32_t r = isl ? (((m0 - 1u) << 25) | dpos) : (0x80000000u | ((clen - 1u) << 25) | coff);
+        bool fit = (isl && lj == 0u) || rw.put(r);  // a zero-length literal (field 0xFFFFFFFF) emits nothing
+        if (isl && lj > 64u) {  // literals longer than 64 bytes: one record per 64 bytes
+            for (uint32_t k = 64u; k < lj && fit; k += 64u) {
+                const uint32_t m = lj - k < 64u ? lj - k : 64u;
+                fit = rw.put(((m - 1u) << 25) | (dpos + k));
+            }
+        }
+        if (!fit) {
+            st = kNeedFused;
+            run = false;
+            return;
+        }
+        ip = dpos + (isl ? lj : 0u);
+        op += len;
+        run = ip < in_len;
+    };
     for (;;) {
         run = run && ip < in_len;
         if (!__any(run)) break;
         if (run && !win.has(ip)) win.load(ip);  // burst reload: one wait for the whole wave
-        while (run && win.has(ip)) {
-            // one tag, branch-free: both interpretations are computed and selected by the type
-            const uint64_t v = win.get8(ip);
-            const uint32_t tag = (uint32_t)v & 0xFFu;
-            const uint32_t ops = (uint32_t)(v >> 8);  // operand bytes (valid where < in_len)
-            const uint32_t after_tag = ip + 1u;
-            const uint32_t avail = in_len - after_tag;
-            const uint32_t type = tag & 3u;
-            const bool isl = type == 0u;
-            const uint32_t code = tag >> 2;
-            // literal (decodeLiteral): nb length bytes after the tag, Java int length + 1
-            const uint32_t nb = (isl && code >= 60u) ? code - 59u : 0u;
-            const uint32_t fmask = nb >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
-            const uint32_t lj = nb == 0u ? code + 1u : (ops & fmask) + 1u;
-            // copy (decodeCopyWith{1,2,4}ByteOffset)
-            const uint32_t csize = type == 1u ? 1u : (type == 2u ? 2u : 4u);
-            const uint32_t clen = type == 1u ? 4u + (code & 7u) : 1u + code;
-            const uint32_t coff = type == 1u ? (((tag & 0xe0u) << 3) | (ops & 0xFFu)) : (type == 2u ? (ops & 0xFFFFu) : ops);
-            const uint32_t hdr = isl ? nb : csize;
-            const uint32_t dpos = after_tag + hdr;
-            const bool lneg = isl && (int32_t)lj < 0;
-            // NOT_ENOUGH_INPUT (silent stop, the tag byte consumed): operands, or the literal's bytes
-            const bool nei = avail < hdr || (isl && !lneg && in_len - dpos < lj);
-            const uint32_t len = isl ? lj : clen;
-            // Java's check order as selects (no divergent branches): literal length, then offset zero /
-            // negative / beyond, then the output limit (op <= cap, so cap - op cannot wrap)
-            const int32_t cerr = coff == 0u ? NX_ERR_SNAPPY_OFFSET_ZERO
-                                            : ((int32_t)coff < 0 ? NX_ERR_SNAPPY_OFFSET_NEGATIVE : (coff > op ? NX_ERR_SNAPPY_OFFSET_BEYOND : 0));
-            const int32_t terr = isl ? (lneg ? NX_ERR_SNAPPY_LITERAL_LEN_INVALID : 0) : cerr;
-            const int32_t err = terr != 0 ? terr : (len > cap - op ? NX_ERR_SNAPPY_OUTPUT_OVERFLOW : 0);
-            if (nei || err != 0) {  // rare: the frame stops here
-                ip = nei ? after_tag : dpos;
-                st = nei ? NX_OK : err;
-                run = false;
-                continue;
-            }
-            const uint32_t m0 = lj < 64u ? lj : 64u;
-            const uint32_t r = isl ? (((m0 - 1u) << 25) | dpos) : (0x80000000u | ((clen - 1u) << 25) | coff);
-            bool fit = (isl && lj == 0u) || rw.put(r);  // a zero-length literal (field 0xFFFFFFFF) emits nothing
-            if (isl && lj > 64u) {  // literals longer than 64 bytes: one record per 64 bytes
-                for (uint32_t k = 64u; k < lj && fit; k += 64u) {
-                    const uint32_t m = lj - k < 64u ? lj - k : 64u;
-                    fit = rw.put(((m - 1u) << 25) | (dpos + k));
-                }
-            }
-            if (!fit) {
-                st = kNeedFused;
-                run = false;
-                continue;
-            }
-            ip = dpos + (isl ? lj : 0u);
-            op += len;
-            run = ip < in_len;
+#if NX_PARSE_RELOAD_K
+        // early reload: the wave leaves the tag loop as soon as NX_PARSE_RELOAD_K of its running lanes
+        // have run out of window (instead of when all have), so lanes idle less between reloads; the
+        // lanes whose window still holds their next tag keep it (no load) and go on after the reload
+        for (;;) {
+            const bool act = run && win.has(ip);
+            if (!__any(act) || __popcll(__ballot(run && !act)) >= NX_PARSE_RELOAD_K) break;
+            if (act) step();
         }
+#else
+        while (run && win.has(ip)) step();
+#endif
     }
     if (st == kNeedFused) {
         status[c] = kNeedFused;
@@ -1168,7 +1235,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lz4(const uint8_t* __rest
     }
     BurstWin win;
     win.init(in + in_off[c], in_len, &wins[threadIdx.x * kWinDw]);
-    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
+    RecWriter rw(reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw]);
     uint32_t ip = 0, op = 0;
     int32_t st = NX_OK;
     bool fit = true;
@@ -1359,7 +1426,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
     }
     Win win;
     win.init(in + in_off[c], in_len, &wins[threadIdx.x * Win::kStride]);
-    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
+    RecWriter rw(reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw]);
     win.load(0);
     const uint32_t b0 = (uint32_t)win.get8(0) & 0xFFu;
     const uint32_t level = (b0 >> 5) + 1u;  // (in[0] >> 5) + 1 on the signed byte: 5..8 for b0 >= 0x80
@@ -1477,7 +1544,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lzf(const uint8_t* __rest
     }
     Win win;
     win.init(in + in_off[c], in_len, &wins[threadIdx.x * Win::kStride]);
-    RecWriter rw{reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw], 0};
+    RecWriter rw(reinterpret_cast<uint4*>(rec + (size_t)c * kRecCap), &recq[threadIdx.x * kQDw]);
     uint32_t ip = 0, op = 0;
     bool ok = true, run = true;  // run: op < lim, and the next control byte at ip < in_len
     for (;;) {
