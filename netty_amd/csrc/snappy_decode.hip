@@ -968,6 +968,26 @@ using ParseRec = RecWriterT<NX_PARSE_QR, NX_PARSE_DEFER != 0>;
 using ParseBurst = BurstWinT<NX_PARSE_NB>;
 using ParseWin = std::conditional_t<NX_PARSE_LINE != 0, BurstWinLine, ParseBurst>;
 
+// The wave's steps between burst reloads: every lane whose window holds its next header takes a step,
+// until no lane's does, or (K > 0) as soon as K running lanes wait for a reload, so that lanes idle
+// less between reloads (those whose window still holds their next header keep it and go on after the
+// reload).  `step` clears `run` when its lane stops.
+template <int K, class Has, class Step>
+__device__ __forceinline__ void burst_steps(const bool& run, Has has, Step step) {
+    if constexpr (K > 0) {
+        for (;;) {
+            const bool act = run && has();
+            if (!__any(act) || __popcll(__ballot(run && !act)) >= K) break;
+            if (act) step();
+        }
+    } else {
+        while (run && has()) step();
+    }
+}
+#ifndef NX_ALT_RELOAD_K  // the FastLZ / LZF parses: the all-lanes rule measured best (round 5 s27)
+#define NX_ALT_RELOAD_K 0
+#endif
+
 __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len_a, const uint32_t* __restrict__ out_cap,
                                                        uint32_t* __restrict__ rec, uint32_t* __restrict__ nrec,
@@ -1074,18 +1094,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
         run = run && ip < in_len;
         if (!__any(run)) break;
         if (run && !win.has(ip)) win.load(ip);  // burst reload: one wait for the whole wave
-#if NX_PARSE_RELOAD_K
-        // early reload: the wave leaves the tag loop as soon as NX_PARSE_RELOAD_K of its running lanes
-        // have run out of window (instead of when all have), so lanes idle less between reloads; the
-        // lanes whose window still holds their next tag keep it (no load) and go on after the reload
-        for (;;) {
-            const bool act = run && win.has(ip);
-            if (!__any(act) || __popcll(__ballot(run && !act)) >= NX_PARSE_RELOAD_K) break;
-            if (act) step();
-        }
-#else
-        while (run && win.has(ip)) step();
-#endif
+        burst_steps<NX_PARSE_RELOAD_K>(run, [&] { return win.has(ip); }, step);
     }
     if (st == kNeedFused) {
         status[c] = kNeedFused;
@@ -1437,7 +1446,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
     for (;;) {
         if (!__any(run)) break;
         if (run && !win.has(ip)) win.load(ip);  // burst reload: one wait for the whole wave
-        while (run && win.has(ip)) {
+        burst_steps<NX_ALT_RELOAD_K>(run, [&] { return win.has(ip); }, [&] {
             const uint64_t v = win.get8(ip);
             const uint32_t ctrl = (uint32_t)v & 0xFFu;
             uint32_t adv, len, dist;
@@ -1446,7 +1455,8 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
                 const uint32_t k = ctrl + 1u;
                 if (op + k > lim || ip + 1u + k > in_len) {
                     ok = false;
-                    break;
+                    run = false;
+                    return;
                 }
                 put_ok = rw.put(((k - 1u) << 25) | (ip + 1u));
                 adv = 1u + k;
@@ -1467,7 +1477,8 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
                     if (code == 255u || ip + p + 2u >= in_len + 0u) {
                         // ran off the block (or too close to its end for the code/far bytes): serial
                         ok = false;
-                        break;
+                        run = false;
+                        return;
                     }
                     const uint32_t cd = win_byte(win, ip + p);
                     ++p;
@@ -1493,7 +1504,8 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
                 // every header byte inside the block; Java: op + len + 3 > outLength -> 0, ref - 1 < 0 -> 0
                 if (ip + p > in_len || op + len + 3u > lim || dist > op) {
                     ok = false;
-                    break;
+                    run = false;
+                    return;
                 }
                 len += 3u;
                 put_ok = put_copy(rw, len, dist);
@@ -1501,12 +1513,13 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_fastlz(const uint8_t* __r
             }
             if (!put_ok) {
                 ok = false;
-                break;
+                run = false;
+                return;
             }
             ip += adv;
             op += len;
             run = ip < in_len;  // Java: a control byte follows while ip < inLength
-        }
+        });
         if (!ok) run = false;
     }
     if (!ok) {
@@ -1550,7 +1563,7 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lzf(const uint8_t* __rest
     for (;;) {
         if (!__any(run)) break;
         if (run && !win.has(ip)) win.load(ip);
-        while (run && win.has(ip)) {
+        burst_steps<NX_ALT_RELOAD_K>(run, [&] { return win.has(ip); }, [&] {
             const uint64_t v = win.get8(ip);
             const uint32_t ctrl = (uint32_t)v & 0xFFu, b1 = (uint32_t)(v >> 8) & 0xFFu, b2 = (uint32_t)(v >> 16) & 0xFFu;
             const bool lit = ctrl < 32u;
@@ -1562,14 +1575,15 @@ __global__ void __launch_bounds__(kParseBlock) k_parse_lzf(const uint8_t* __rest
             const bool bad = lit ? (ip + 1u + k > in_len || op + k > lim) : (ip + hdr > in_len || dist > op || op + len > lim);
             if (bad || !(lit ? rw.put(((k - 1u) << 25) | (ip + 1u)) : put_copy(rw, len, dist))) {
                 ok = false;
-                break;
+                run = false;
+                return;
             }
             ip += lit ? 1u + k : hdr;
             op += len;
             run = op < lim;
             if (run && ip >= in_len) ok = false;  // more output wanted, no control byte left
             run = run && ok;
-        }
+        });
         if (!ok) run = false;
     }
     if (!ok) {

@@ -56,6 +56,23 @@ def main():
                                               for i in range(0, n, n // k))
         out[f"fastlz_l{level}"] = {"ms": round(t, 3), "gib_s": round(U / (t / 1e3) / 2**30, 2), "ok": ok}
     del fo
+    # LZF: the compressed ("ZV" type 1) blocks of lzf_encode's chunk stream, body at +7 (bench.py's leg)
+    lcap = (B.lzf_max_compressed_length(CH) + 15) // 16 * 16
+    lo = torch.empty(n * lcap, dtype=torch.uint8, device=dev)
+    loff = torch.arange(n, dtype=torch.int64, device=dev) * lcap
+    B.lzf_encode(src, off, ln, lo, loff)
+    idx = torch.nonzero(lo[loff + 2] == 1).flatten()
+    boff = loff[idx] + 7
+    blen = (lo[loff[idx] + 3].to(torch.int32) << 8) | lo[loff[idx] + 4].to(torch.int32)
+    uo, ul = off[idx], ln[idx]
+    dec.zero_()
+    t = best(lambda: B.lzf_decode(lo, boff, blen, dec, uo, ul))
+    r = B.lzf_decode(lo, boff, blen, dec, uo, ul)
+    sel = idx[::max(1, idx.numel() // 4096)].tolist()
+    ok = int((r != 0).sum()) == 0 and all(bool(torch.equal(dec[i * CH:i * CH + int(ln[i])], src[i * CH:i * CH + int(ln[i])])) for i in sel)
+    Ul = int(ul.to(torch.int64).sum())
+    out["lzf"] = {"ms": round(t, 3), "blocks": int(idx.numel()), "gib_s": round(Ul / (t / 1e3) / 2**30, 2), "ok": ok}
+    del lo
     zcap = (B.lz4_max_compressed_length(CH) + 15) // 16 * 16
     zo = torch.empty(n * zcap, dtype=torch.uint8, device=dev)
     zoff = torch.arange(n, dtype=torch.int64, device=dev) * zcap

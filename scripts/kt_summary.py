@@ -29,7 +29,8 @@ def main():
         if os.path.exists(log):
             for line in open(log):
                 if line.startswith("{"):
-                    r["decode_ms"].append(json.loads(line)["decode_ms"])
+                    j = json.loads(line)
+                    r["decode_ms"].append(j.get("decode_ms") or {k: v["ms"] for k, v in j.items() if isinstance(v, dict)})
     out = []
     for v, r in rows.items():
         e = {"variant": v, "decode_ms": r["decode_ms"]}
