@@ -645,7 +645,17 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
             torch.cuda.empty_cache()
         if not args.no_e2e:
             # host memory in, host memory out, through the C-ABI a JNI caller binds (never `value`)
+            link = link_budget(torch, dev)
             line["end_to_end"] = e2e_capi(args.e2e_channels, args.e2e_messages)
+            e2e = line["end_to_end"]
+            if "decode_gib_s" in e2e and e2e.get("compressed_bytes") and e2e.get("uncompressed_bytes"):
+                r = e2e["compressed_bytes"] / e2e["uncompressed_bytes"]
+                # every decoded byte crosses the link once, with r compressed bytes the other way
+                link["decode_bound_gib_s"] = round(link["both_gb_s_total"] * 1e9 / (1 + r) / 2**30, 2)
+                link["decode_frac_of_bound"] = round(e2e["decode_gib_s"] / link["decode_bound_gib_s"], 3)
+                link["encode_bound_gib_s"] = link["decode_bound_gib_s"]  # the same bytes, the other way round
+                link["encode_frac_of_bound"] = round(e2e["encode_gib_s"] / link["encode_bound_gib_s"], 3)
+            e2e["link"] = link
             # the same round trip driven from torch (pinned tensors, two streams): netty_amd/pipeline.py
             from netty_amd import pipeline as P
             line["end_to_end_torch_pipeline"] = P.measure(dev, n=args.e2e_chunks, sub=args.e2e_sub)
@@ -671,6 +681,51 @@ def device_info(torch, dev):
     info = {"name": p.name, "arch": p.gcnArchName, "cus": p.multi_processor_count, "hbm_gib": round(p.total_memory / 2**30, 1),
             "pci_bus_id": getattr(p, "pci_bus_id", None)}
     return info
+
+
+def link_budget(torch, dev, mib: int = 512, reps: int = 3):
+    """The host link the end-to-end legs share: pinned host -> device and device -> host copy rates
+    alone and issued together on two streams.  On the pool's boxes the two directions share one
+    ~57 GB/s budget (together they take the sum of their times alone: profiles/r05/s31), so a decode
+    that moves r compressed bytes in per decoded byte out is bounded by budget / (1 + r)."""
+    import time
+    n = mib << 20
+    hs = torch.empty(n, dtype=torch.uint8).pin_memory()
+    hd = torch.empty(n, dtype=torch.uint8).pin_memory()
+    da = torch.empty(n, dtype=torch.uint8, device=dev)
+    db = torch.zeros(n, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def timed(fn):
+        best = None
+        for _ in range(reps + 1):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            best = dt if best is None else min(best, dt)
+        return best
+
+    def h2d():
+        with torch.cuda.stream(s1):
+            da.copy_(hs, non_blocking=True)
+
+    def d2h():
+        with torch.cuda.stream(s2):
+            hd.copy_(db, non_blocking=True)
+
+    def both():
+        h2d()
+        d2h()
+
+    th, td, tb = timed(h2d), timed(d2h), timed(both)
+    del hs, hd, da, db
+    torch.cuda.empty_cache()
+    gb = n / 1e9
+    return {"h2d_gb_s": round(gb / th, 2), "d2h_gb_s": round(gb / td, 2), "both_gb_s_total": round(2 * gb / tb, 2),
+            "both_over_sum_of_alone": round(tb / (th + td), 3), "bytes_per_copy": n,
+            "note": "pinned copies on two streams; both_over_sum_of_alone ~1 means the directions share one budget"}
 
 
 def e2e_capi(channels: int, messages: int, timeout: float = 240.0, dec_flush_mib: int = 64):
