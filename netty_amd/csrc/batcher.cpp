@@ -775,7 +775,7 @@ int32_t enqueue_dec(Batch* bt, Job* j, const uint8_t* S, size_t walked, const ui
         } else {
             uint8_t* st = bt->stage(a.dlen, &off);
             if (!st) return fail(NX_ERR_HIP);
-            memcpy(st, S + a.data, a.dlen);
+            nx::copy_bytes(st, S + a.data, a.dlen);
         }
         const uint8_t dir = dS ? 1 : 0;
         bt->dact_direct.push_back(dir);
@@ -1572,7 +1572,7 @@ extern "C" int64_t nx_snappy_frame_encoder_submit(nx_snappy_frame_encoder* e, nx
                 delete j;
                 return NX_ERR_HIP;
             }
-            memcpy(st, in, n);
+            nx::copy_bytes(st, in, n);
         }
         auto add = [&](uint64_t off, uint32_t len, bool comp) {
             EncSlice S{base + off, bt->eslots, len, comp ? 1u : 0u};
@@ -1666,7 +1666,7 @@ int64_t decoder_submit(nx_snappy_frame_decoder* d, nx_batcher* b, const uint8_t*
             delete j;
             return NX_ERR_HIP;
         }
-        memcpy(st, S, walked);
+        nx::copy_bytes(st, S, walked);
         staged = (int64_t)off;
     }
     if (enqueue_dec(bt, j, S, walked, dS, staged) != NX_OK) {
@@ -1813,7 +1813,7 @@ int64_t alt_decoder_submit(D* d, St& st, nx_batcher* b, const uint8_t* in, size_
             delete j;
             return NX_ERR_HIP;
         }
-        memcpy(stg, in + lo, hi - lo);
+        nx::copy_bytes(stg, in + lo, hi - lo);
         j->astage = off - lo;  // block b's payload is at staging offset astage + b.data
         for (const nx::af::Blk& k : j->ablk) {
             AltPiece P{};
@@ -1904,7 +1904,7 @@ extern "C" int64_t nx_fastlz_frame_encoder_submit(nx_fastlz_frame_encoder* e, nx
             delete j;
             return NX_ERR_HIP;
         }
-        memcpy(stg, buf + r0, n);
+        nx::copy_bytes(stg, buf + r0, n);
         std::vector<nx::af::FlzPlan> plan;
         nx::af::flz_plan(r0, n, plan);
         for (const nx::af::FlzPlan& q : plan) {
@@ -1945,7 +1945,7 @@ extern "C" int64_t nx_lzf_encoder_submit(nx_lzf_encoder* e, nx_batcher* b, const
             delete j;
             return NX_ERR_HIP;
         }
-        memcpy(stg, in, n);
+        nx::copy_bytes(stg, in, n);
     }
     const bool comp = (int64_t)n >= e->threshold;
     size_t ip = 0;
@@ -2004,7 +2004,7 @@ extern "C" int64_t nx_lz4_frame_encoder_submit(nx_lz4_frame_encoder* e, nx_batch
             uint64_t off = 0;
             uint8_t* stg = bt->stage(n, &off);
             if (!stg) return fail(NX_ERR_HIP);
-            memcpy(stg, in, n);
+            nx::copy_bytes(stg, in, n);
             AltPiece P{};
             P.kind = nx::bt::AK_RAW;
             P.src = off;
@@ -2021,8 +2021,8 @@ extern "C" int64_t nx_lz4_frame_encoder_submit(nx_lz4_frame_encoder* e, nx_batch
             uint8_t* stg = bt->stage(full, &off);
             if (!stg) return fail(NX_ERR_HIP);
             const size_t from_buf = have < full ? have : full;
-            memcpy(stg, e->buf.data(), from_buf);
-            if (full > from_buf) memcpy(stg + from_buf, in, full - from_buf);
+            nx::copy_bytes(stg, e->buf.data(), from_buf);
+            if (full > from_buf) nx::copy_bytes(stg + from_buf, in, full - from_buf);
             for (size_t q = 0; q < full; q += bs) {
                 const uint32_t len = (uint32_t)((full - q) < bs ? (full - q) : bs);
                 AltPiece P{};

@@ -151,7 +151,7 @@ extern "C" int64_t nx_snappy_frame_encoder_encode(nx_snappy_frame_encoder* e, co
             out[op++] = (uint8_t)(cl >> 16);
             memcpy(out + op, &crc[i], 4);
             op += 4;
-            memcpy(out + op, in + sl[i].off, sl[i].len);
+            nx::copy_bytes(out + op, in + sl[i].off, sl[i].len);
             op += sl[i].len;
         }
     }
@@ -404,7 +404,7 @@ extern "C" int64_t nx_fastlz_frame_encoder_encode(nx_fastlz_frame_encoder* e, co
         } else {
             blockType = 0;
             chunkLength = length;
-            memcpy(out + outputOffset + 2, in + ioff[i], length);
+            nx::copy_bytes(out + outputOffset + 2, in + ioff[i], length);
         }
         out[outputOffset] = (uint8_t)(length >> 8);
         out[outputOffset + 1] = (uint8_t)length;
@@ -630,7 +630,7 @@ extern "C" int64_t nx_lzf_encoder_encode(nx_lzf_encoder* e, const uint8_t* in, s
             out[op + 2] = 0;
             out[op + 3] = (uint8_t)(len >> 8);
             out[op + 4] = (uint8_t)len;
-            memcpy(out + op + 5, in + ip, len);
+            nx::copy_bytes(out + op + 5, in + ip, len);
             op += 5 + len;
             ip += len;
         } while (ip < n);

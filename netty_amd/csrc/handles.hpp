@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 #include <atomic>
 #include <deque>
 #include <set>
@@ -13,6 +14,13 @@
 #include "workspace.hpp"
 
 namespace nx {
+
+// memcpy of n bytes that may be zero with a null source (an empty message or cumulation: memcpy's
+// arguments must be valid pointers even for n = 0; found by the UBSan run, profiles/r05/s35)
+inline void copy_bytes(void* dst, const void* src, size_t n) {
+    if (n) memcpy(dst, src, n);
+}
+
 namespace h {
 
 // ------------------------------------------------------------------ device context

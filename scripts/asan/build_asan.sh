@@ -8,7 +8,8 @@
 set -eu
 cd "$(dirname "$0")/../.."
 H=/opt/rocm/bin/hipcc
-F="-O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -munsafe-fp-atomics -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer"
+SAN=${SAN:-address}  # SAN=address,undefined adds UBSan (host side too)
+F="-O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -munsafe-fp-atomics -Xarch_host -fsanitize=$SAN -Xarch_host -fno-omit-frame-pointer"
 O=netty_amd/build_asan
 mkdir -p $O
 objs=""
@@ -21,7 +22,7 @@ for f in netty_amd/csrc/*.hip netty_amd/csrc/*.cpp; do
 done
 wait
 $H $F -x hip -c netty_amd/tools/e2e_capi.cpp -o $O/e2e_capi.o
-$H --offload-arch=gfx950 -Xarch_host -fsanitize=address -o $O/e2e_capi_asan $O/e2e_capi.o $objs
+$H --offload-arch=gfx950 -Xarch_host -fsanitize=$SAN -o $O/e2e_capi_asan $O/e2e_capi.o $objs
 $H $F -x hip -c scripts/asan/capi_tour.cpp -o $O/capi_tour.o
-$H --offload-arch=gfx950 -Xarch_host -fsanitize=address -o $O/capi_tour_asan $O/capi_tour.o $objs
+$H --offload-arch=gfx950 -Xarch_host -fsanitize=$SAN -o $O/capi_tour_asan $O/capi_tour.o $objs
 echo $O/e2e_capi_asan $O/capi_tour_asan
