@@ -73,6 +73,41 @@ def test_lz4_decode_malformed(dev, B, oracle):
             assert outs[i] == obytes
 
 
+def test_lz4_decode_fuzz_corrupted(dev, B, oracle):
+    """Seeded corruptions of valid blocks (byte flips, 255-runs in length fields, truncation, extra
+    bytes) and wrong expected lengths, against the oracle's orc_lz4_decompress: same status, and the
+    same bytes where it succeeds."""
+    rng = random.Random(2024)
+    base = [oracle.textgen_chunk(900 + i, n) for i, n in enumerate((300, 4096, 20000, 65536))]
+    base += [bytes(rng.getrandbits(8) for _ in range(3000)), bytes((i % 5) * 40 for i in range(9000))]
+    blocks, wants = [], []
+    for k in range(480):
+        d = base[k % len(base)]
+        z = bytearray(oracle.lz4_compress(d))
+        kind = k % 6
+        if kind == 0:
+            for _ in range(1 + rng.randrange(3)):
+                z[rng.randrange(len(z))] ^= 1 << rng.randrange(8)
+        elif kind == 1:
+            p = rng.randrange(len(z))
+            z[p:p + 1 + rng.randrange(6)] = b"\xff" * (1 + rng.randrange(6))
+        elif kind == 2:
+            z = z[:rng.randrange(len(z) + 1)]
+        elif kind == 3:
+            z += bytes(rng.getrandbits(8) for _ in range(1 + rng.randrange(8)))
+        elif kind == 4:
+            z[rng.randrange(len(z))] = rng.getrandbits(8)
+        w = len(d) + (rng.randrange(-3, 4) if kind == 5 else 0)
+        blocks.append(bytes(z))
+        wants.append(max(w, 0))
+    st, outs = _run(B, dev, blocks, wants)
+    for i, (blk, w) in enumerate(zip(blocks, wants)):
+        ost, obytes = oracle.lz4_decompress(blk, w)
+        assert st[i] == ost, (i, w)
+        if ost == 0:
+            assert outs[i] == obytes, i
+
+
 def test_lz4_record_overflow_falls_back(dev, B, oracle):
     """A block of 20 000 one-literal + 4-byte-match sequences needs 40 000 records (> 16 384 per slot):
     it is decoded by the lane-serial kernel, with the same result."""
