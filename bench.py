@@ -37,11 +37,10 @@ CHUNK = 65536
 CONFIG5_CHUNKS = 1638400  # 100 GiB of 64 KiB chunks
 # kernels whose PMC traffic backs roofline.traffic; the summary must have been taken on these sources
 PMC_SOURCES = ("netty_amd/csrc/snappy_encode.hip", "netty_amd/csrc/snappy_decode.hip", "netty_amd/csrc/crc32c.hip",
-               "netty_amd/csrc/nx_common.hpp", "netty_amd/csrc/expand_units.hpp", "netty_amd/csrc/expand_frame.hpp")
+               "netty_amd/csrc/nx_common.hpp")
 # the alt-codec legs' kernels (their parses share the Snappy decoder's translation unit and expander)
 ALT_PMC_SOURCES = ("netty_amd/csrc/fastlz.hip", "netty_amd/csrc/lzf.hip", "netty_amd/csrc/lz4.hip",
-                   "netty_amd/csrc/snappy_decode.hip", "netty_amd/csrc/nx_common.hpp", "netty_amd/csrc/expand_units.hpp",
-                   "netty_amd/csrc/expand_frame.hpp")
+                   "netty_amd/csrc/snappy_decode.hip", "netty_amd/csrc/nx_common.hpp")
 
 
 def parse(argv=None):
@@ -51,7 +50,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--total-chunks", type=int, default=CONFIG5_CHUNKS,
                     help="64 KiB chunks of the whole job, split across ranks (configs[4]: 1 638 400 = 100 GiB)")
-    ap.add_argument("--sub-chunks", type=int, default=262144, help="chunks per device-resident sub-batch")
+    ap.add_argument("--sub-chunks", type=int, default=0,
+                    help="chunks per encode and decode call (0: the library's encode plan, decode calls of 262 144)")
     ap.add_argument("--weak-chunks", type=int, default=1 << 20,
                     help="chunks per GPU of the separate configs[1]+[2] leg (0 = skip)")
     ap.add_argument("--weak-steps", type=int, default=1)
@@ -90,14 +90,13 @@ def host_cores() -> int:
 
 
 def take_gpu_sample(torch, B, leg, k: int):
-    """Every (m // k)-th chunk of the leg's first sub-batch as the GPU left it (compressed bytes and
+    """Every (m // k)-th chunk of the leg's first decode call as the GPU left it (compressed bytes and
     masked CRC32C), on the host: the input of cpu_baseline's parity check.  No oracle here."""
-    lo, m = next(leg.batches())
+    lo, m = leg.run_prefix()  # the first decode call's chunks, encoded as the timed steps encode them
     k = max(1, min(k, m))
     step = m // k
     idx = torch.arange(0, step * k, step, dtype=torch.int64, device=leg.dev)
-    leg.run_sub(lo, m)  # the first sub-batch's outputs, as the timed steps produce them
-    packed, poff = B.gather(leg.enc, leg.eoff[idx], leg.elen[lo + idx])
+    packed, poff = B.gather(leg.enc, leg.eoff[lo + idx], leg.elen[lo + idx])
     torch.cuda.synchronize()
     return {"first": leg.first + lo, "step": step, "index": idx.cpu().tolist(), "bytes": packed.cpu().numpy().tobytes(),
             "off": poff.cpu().tolist(), "len": leg.elen[lo + idx].cpu().tolist(),
@@ -302,31 +301,65 @@ def load_traffic():
 
 
 # ---------------------------------------------------------------------------------------- the GPU leg
+DEC_SUB = 262144  # frames per decode call: one k_parse / k_expand pair (snappy_decode.hip kSubBatch)
+
+
 class SnappyRoundTrip:
     """One rank's shard [first, first + n) of text-like 64 KiB chunks: the whole shard's inputs are
-    generated on the device up front; a step runs CRC32C + encode + decode/verify over them in
-    sub-batches whose output buffers are reused (the compressed bytes of every chunk are kept only as
-    per-chunk lengths, the decoded bytes are checked against the inputs after the timed region)."""
+    generated on the device up front; a step runs CRC32C + encode and decode/verify over them as a
+    schedule of calls (`ops`) whose buffers are reused.
 
-    def __init__(self, torch, dev, first: int, n: int, sub: int):
+    Encode calls follow the library's launch plan (nx_snappy_encode_plan: equal full-occupancy
+    launches, e.g. 5 x 327 680 chunks per 100 GiB on 256 CUs; round 6), so each
+    call is one launch of the dense encoder.  Decode calls take DEC_SUB frames at a time as soon as
+    that many are encoded (one parse/expand pair each; the last call takes the rest), reading the
+    compressed chunks from a ring of encode slots that holds every chunk between its encode and its
+    decode.  `sub` (tests, --sub-chunks) fixes both sizes instead.  The compressed bytes of every chunk
+    are kept only as per-chunk lengths; the decoded bytes are checked against the inputs after the
+    timed region."""
+
+    def __init__(self, torch, dev, first: int, n: int, sub: int = 0, dec_sub: int = DEC_SUB, enc_sizes=None):
         from netty_amd import batch as B
-        self.torch, self.B, self.dev = torch, B, dev
-        self.first, self.n, self.sub = first, n, max(1, min(sub, n))
-        self.cap = (B.snappy_max_compressed_length(CHUNK) + 15) // 16 * 16
-        s = self.sub
-        # place the encoder's table workspace before the shard's buffers take the memory its
-        # placement choice draws candidates from (as a server would at start-up; DESIGN.md §3)
         from netty_amd import _lib
-        rc = _lib.load().nx_snappy_encoder_reserve(s, torch.cuda.current_stream(dev).cuda_stream)
+        self.torch, self.B, self.dev = torch, B, dev
+        self.first, self.n = first, n
+        self.cap = (B.snappy_max_compressed_length(CHUNK) + 15) // 16 * 16
+        L = _lib.load()
+        st = torch.cuda.current_stream(dev).cuda_stream
+        if enc_sizes:  # tests: an explicit schedule
+            assert sum(enc_sizes) == n
+            self.enc_sizes, self.dec_sub = list(enc_sizes), max(1, min(dec_sub, n))
+        elif sub:
+            sub = max(1, min(sub, n))
+            self.enc_sizes = [min(sub, n - lo) for lo in range(0, n, sub)]
+            self.dec_sub = sub
+        else:
+            self.enc_sizes = encode_plan(n)
+            self.dec_sub = max(1, min(dec_sub, n))
+        # place the encoder's table workspace before the shard's buffers take the memory its
+        # placement choice draws candidates from (as a server would at start-up; DESIGN.md §3).  This
+        # process owns the device, so the placement may draw as many candidates as memory allows.
+        assert L.nx_workspace_placement_config(2**64 - 1, 0) == 0
+        rc = L.nx_snappy_encoder_reserve(max(self.enc_sizes), st)
         assert rc == 0, f"nx_snappy_encoder_reserve: {rc}"
+        if not sub and not enc_sizes:
+            assert encode_plan(n) == self.enc_sizes, "the plan changed with the reserved workspace"
+        self.ops = schedule(self.enc_sizes, self.dec_sub)
+        self.sub = next(m for kind, _, m in self.ops if kind == "dec")  # the first decode call's frames
+        # encode ring: chunk c's compressed bytes live in slot c mod R until their decode
+        R = min(n, max(self.enc_sizes) + self.dec_sub - 1)
+        self.ring = R
         self.src = torch.empty(n * CHUNK, dtype=torch.uint8, device=dev)
-        for lo in range(0, n, s):  # textgen in pieces keeps its temporaries small
-            B.textgen(self.src[lo * CHUNK:], first + lo, min(s, n - lo), CHUNK)
-        self.off = torch.arange(s, dtype=torch.int64, device=dev) * CHUNK
-        self.ln = torch.full((s,), CHUNK, dtype=torch.int32, device=dev)
-        self.enc = torch.empty(s * self.cap, dtype=torch.uint8, device=dev)
-        self.eoff = torch.arange(s, dtype=torch.int64, device=dev) * self.cap
-        self.dec = torch.empty(s * CHUNK, dtype=torch.uint8, device=dev)
+        tg = max(self.enc_sizes)
+        for lo in range(0, n, tg):  # textgen in pieces keeps its temporaries small
+            B.textgen(self.src[lo * CHUNK:], first + lo, min(tg, n - lo), CHUNK)
+        w = max(max(self.enc_sizes), self.dec_sub)
+        self.off = torch.arange(w, dtype=torch.int64, device=dev) * CHUNK
+        self.soff = torch.arange(n, dtype=torch.int64, device=dev) * CHUNK  # chunk c's input at c * CHUNK
+        self.ln = torch.full((w,), CHUNK, dtype=torch.int32, device=dev)
+        self.enc = torch.empty(R * self.cap, dtype=torch.uint8, device=dev)
+        self.eoff = (torch.arange(n, dtype=torch.int64, device=dev) % R) * self.cap
+        self.dec = torch.empty(self.dec_sub * CHUNK, dtype=torch.uint8, device=dev)
         self.elen = torch.empty(n, dtype=torch.int32, device=dev)
         self.est = torch.empty(n, dtype=torch.int32, device=dev)
         self.crc = torch.empty(n, dtype=torch.int32, device=dev)
@@ -335,35 +368,67 @@ class SnappyRoundTrip:
         self.ev = {k: [] for k in ("crc", "enc", "dec")}
         torch.cuda.synchronize(dev)
 
-    def batches(self):
-        for lo in range(0, self.n, self.sub):
-            yield lo, min(self.sub, self.n - lo)
+    def plan_info(self):
+        return {"encode_calls": self.enc_sizes, "decode_calls": [m for kind, _, m in self.ops if kind == "dec"],
+                "encode_ring_slots": self.ring}
 
-    def run_sub(self, lo, m, record=False, expected=None):
+    def batches(self):
+        """the encode calls' chunk ranges"""
+        for kind, lo, m in self.ops:
+            if kind == "enc":
+                yield lo, m
+
+    def enc_op(self, lo, m, record=False):
         torch, B = self.torch, self.B
-        src = self.src[lo * CHUNK:(lo + m) * CHUNK]
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if record else None
         if record:
             e[0].record()
-        B.crc32c_masked(src, self.off[:m], self.ln[:m], out=self.crc[lo:lo + m])
+        B.crc32c_masked(self.src, self.soff[lo:lo + m], self.ln[:m], out=self.crc[lo:lo + m])
         if record:
             e[1].record()
-        B.snappy_encode(src, self.off[:m], self.ln[:m], self.enc, self.eoff[:m], out_len=self.elen[lo:lo + m],
+        B.snappy_encode(self.src, self.soff[lo:lo + m], self.ln[:m], self.enc, self.eoff[lo:lo + m], out_len=self.elen[lo:lo + m],
                         status=self.est[lo:lo + m])
         if record:
             e[2].record()
-        B.snappy_decode(self.enc, self.eoff[:m], self.elen[lo:lo + m], self.dec, self.off[:m],
+            self.ev["crc"].append((e[0], e[1]))
+            self.ev["enc"].append((e[1], e[2]))
+
+    def dec_op(self, lo, m, record=False, expected=None):
+        torch, B = self.torch, self.B
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if record else None
+        if record:
+            e[0].record()
+        B.snappy_decode(self.enc, self.eoff[lo:lo + m], self.elen[lo:lo + m], self.dec, self.off[:m],
                         expected_crc=self.crc[lo:lo + m] if expected is None else expected,
                         out_len=self.dlen[lo:lo + m], status=self.dst[lo:lo + m])
         if record:
-            e[3].record()
-            self.ev["crc"].append((e[0], e[1]))
-            self.ev["enc"].append((e[1], e[2]))
-            self.ev["dec"].append((e[2], e[3]))
+            e[1].record()
+            self.ev["dec"].append((e[0], e[1]))
+
+    def run_op(self, op, record=False, expected=None):
+        kind, lo, m = op
+        if kind == "enc":
+            self.enc_op(lo, m, record)
+        else:
+            self.dec_op(lo, m, record, expected)
+
+    def run_sub(self, lo, m):
+        """encode then decode chunks [lo, lo + m) (m <= the decode buffer's frames), outside the schedule"""
+        assert m <= self.dec_sub and m <= self.ring
+        self.enc_op(lo, m)
+        self.dec_op(lo, m)
+
+    def run_prefix(self, expected=None):
+        """the schedule up to and including its first decode call (its frames' compressed bytes are then
+        in the ring and their decoded bytes in `dec`); `expected` replaces that call's CRCs"""
+        for op in self.ops:
+            self.run_op(op, expected=expected if op[0] == "dec" else None)
+            if op[0] == "dec":
+                return op[1], op[2]
 
     def step(self, record=False):
-        for lo, m in self.batches():
-            self.run_sub(lo, m, record)
+        for op in self.ops:
+            self.run_op(op, record)
 
     def kernel_ms_per_step(self, steps: int):
         def tot(pairs):
@@ -375,23 +440,55 @@ class SnappyRoundTrip:
         chunk, and a 2 % subset with corrupted expected CRCs flagged (and nothing else)."""
         torch = self.torch
         ok = True
-        for lo, m in self.batches():
-            self.run_sub(lo, m)
-            ok = ok and bool(torch.equal(self.dec[:m * CHUNK], self.src[lo * CHUNK:(lo + m) * CHUNK]))
+        for op in self.ops:
+            self.run_op(op)
+            kind, lo, m = op
+            if kind == "dec":
+                ok = ok and bool(torch.equal(self.dec[:m * CHUNK], self.src[lo * CHUNK:(lo + m) * CHUNK]))
         ok = (ok and int((self.est != 0).sum()) == 0 and int((self.dst != 0).sum()) == 0
               and bool(torch.equal(self.dlen, torch.full_like(self.dlen, CHUNK))))
-        lo, m = 0, min(self.sub, self.n)
+        m = self.sub
         g = torch.Generator(device=self.dev).manual_seed(77 + rank)
         bad = torch.rand(m, device=self.dev, generator=g) < 0.02
         crc = self.crc[:m].clone()
-        self.run_sub(lo, m, expected=torch.where(bad, crc ^ 1, crc))
+        self.run_prefix(expected=torch.where(bad, crc ^ 1, crc))
         d = self.dst[:m]
         detect = bool(torch.equal(d != 0, bad)) and bool(torch.equal(d[bad], torch.full_like(d[bad], -7)))
-        self.run_sub(lo, m)  # leave the first sub-batch's buffers decoded with the right CRCs
+        self.run_prefix()  # leave the first decode call's buffers decoded with the right CRCs
         return ok and detect, detect
 
     def comp_bytes(self) -> int:
         return int(self.elen.to(self.torch.int64).sum().item())
+
+
+def encode_plan(n: int):
+    """The library's encode launches for n chunks on the current device (nx_snappy_encode_plan)."""
+    import ctypes
+    from netty_amd import _lib
+    L = _lib.load()
+    cap = 4096
+    sizes = (ctypes.c_uint32 * cap)()
+    cnt = ctypes.c_uint32(0)
+    assert L.nx_snappy_encode_plan(n, sizes, cap, ctypes.byref(cnt)) == 0
+    assert 0 < cnt.value <= cap
+    out = [sizes[i] for i in range(cnt.value)]
+    assert sum(out) == n
+    return out
+
+
+def schedule(enc_sizes, dec_sub: int):
+    """The step's calls in order: each encode call, then a decode call of dec_sub frames whenever that
+    many are encoded and not yet decoded, the rest after the last encode.  [(kind, first chunk, chunks)]"""
+    ops, enc_done, dec_done = [], 0, 0
+    for m in enc_sizes:
+        ops.append(("enc", enc_done, m))
+        enc_done += m
+        while enc_done - dec_done >= dec_sub:
+            ops.append(("dec", dec_done, dec_sub))
+            dec_done += dec_sub
+    if enc_done > dec_done:
+        ops.append(("dec", dec_done, enc_done - dec_done))
+    return ops
 
 
 def copy_rate_gbs(torch, a, b):
@@ -434,7 +531,7 @@ ENC_INSERTS_PER_CHUNK = 7724
 ENC_CANDIDATE_LOADS_PER_CHUNK = 4275
 
 
-def probe_ceiling(torch, dev, lanes=262144, steps=16384):
+def probe_ceiling(torch, dev, lanes=None, steps=16384):
     """The random-access ceiling of the encoder's request pattern on this GPU (netty_amd/tools/
     probe_ceiling.hip: per lane a serial chain of 64-bit table exchanges + the encoder's share of
     dependent input loads over its own regions, with and without the encoder's share of insert
@@ -444,6 +541,8 @@ def probe_ceiling(torch, dev, lanes=262144, steps=16384):
     path = os.path.join(ROOT, "netty_amd", "libnx_probe_ceiling.so")
     if not os.path.exists(path):
         return None
+    if lanes is None:  # the encoder's resident lanes: 20 waves per CU (snappy_encode.hip)
+        lanes = torch.cuda.get_device_properties(dev).multi_processor_count * 20 * 64
     lib = ctypes.CDLL(path)
     lib.nx_probe_ceiling.restype = ctypes.c_int32
     lib.nx_probe_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
@@ -474,6 +573,7 @@ def probe_ceiling(torch, dev, lanes=262144, steps=16384):
     torch.cuda.empty_cache()
     if best:
         best["placements_gprobes_per_s"] = per  # with inserts, one per table placement tried
+        best["lanes"] = lanes
     return best or None
 
 
@@ -550,7 +650,7 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
     my_off, total_comp, totals_all = S.exchange_offsets(comp_bytes, device=cdev)
     t_crc, t_enc, t_dec = leg.kernel_ms_per_step(args.steps)
     U, C_ = n * CHUNK, comp_bytes
-    copy_gbs = copy_rate_gbs(torch, leg.src[:min(n, leg.sub) * CHUNK], leg.dec) if gpu else None
+    copy_gbs = copy_rate_gbs(torch, leg.src[:min(n, leg.dec_sub) * CHUNK], leg.dec[:min(n, leg.dec_sub) * CHUNK]) if gpu else None
     traffic = load_traffic() if gpu else (None, "cpu test leg")
     r_dec = roofline(C_ + U, t_dec, n, DEC_KERNELS, traffic, copy_gbs)  # decode: C_in + U_out per chunk
     r_enc = roofline(U + C_, t_enc, n, ENC_KERNELS, traffic, copy_gbs)  # encode: U_in + C_out per chunk
@@ -571,8 +671,8 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
             "ceiling_placements_gprobes_per_s": ceil.get("placements_gprobes_per_s"),
             "ceiling_source": "netty_amd/tools/probe_ceiling.hip, the same request mix without compute (exchanges, "
                               "insert stores and candidate loads in the census proportions; and without the stores), "
-                              "262144 lanes, timed live, fastest of up to 6 table placements (as the encoder chooses its "
-                              "workspace), drawn after the job's buffers are freed at N=1"}
+                              f"{ceil.get('lanes')} lanes (the encoder's resident lanes), timed live, fastest of up to 6 table "
+                              "placements (as the encoder chooses its workspace), drawn after the job's buffers are freed at N=1"}
 
     want_ceiling = bool(gpu and t_enc and not args.no_probe_ceiling)
     if want_ceiling and not (rank == 0 and world == 1):
@@ -591,7 +691,7 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
                                f"{args.total_chunks} text-like 64 KiB chunks ({args.total_chunks * CHUNK / 2**30:.0f} GiB) "
                                f"split across {world} GPU(s), device-resident",
                    "chunk_bytes": CHUNK, "global_chunks": args.total_chunks, "chunks_per_gpu": n,
-                   "sub_batch_chunks": leg.sub,
+                   "calls": leg.plan_info() if hasattr(leg, "plan_info") else None,
                    "parallelism": f"dp{world} (independent chunk shards, no data-path collective)"},
         "roofline": dominant,
         "roofline_decode": r_dec, "roofline_encode": r_enc,
@@ -773,6 +873,8 @@ def bench_frame_scan(torch, B, dev, leg, m: int, per_stream: int, reps: int = 3)
     payload), one stream per connection cumulation; nx_snappy_frame_scan_batch lists their chunks and
     nx_snappy_decode_batch decodes straight from that list with CRC verification."""
     m = min(m, leg.sub, leg.n)
+    if hasattr(leg, "run_prefix"):
+        leg.run_prefix()  # the first decode call's chunks: compressed in the ring, decoded in `dec`
     src, enc, eoff, elen, crc, dec = leg.src, leg.enc, leg.eoff, leg.elen, leg.crc, leg.dec
     ns = (m + per_stream - 1) // per_stream
     fs = elen[:m].to(torch.int64) + 8

@@ -75,6 +75,22 @@ int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_off, const 
 #define NX_WS_DEC_RECORDS 4
 #define NX_WS_LZ4HC_ENC 5
 int32_t nx_snappy_encoder_reserve(uint32_t max_chunks, void* stream);
+/* The same with a bound (round 6): max_bytes caps the Snappy table workspace for good (0: no cap; 128
+ * KiB per lane, whole blocks of 256 lanes above 16 384): batches of any size then run on those lanes
+ * and the standalone calls never grow it past the cap until nx_workspaces_trim frees it.  Returns
+ * NX_ERR_INVALID_ARG when max_bytes holds no lane or the workspace is already larger.  *bytes = the
+ * workspace's bytes, *peak = the most bytes its placement held at once (both nullable). */
+int32_t nx_snappy_encoder_reserve_ex(uint32_t max_chunks, uint64_t max_bytes, void* stream,
+                                     uint64_t* bytes, uint64_t* peak);
+/* Placement bound of every later large (>= 2 GiB) encoder workspace: peak_bytes = the
+ * bytes its candidate allocations may hold at once (0: half of the device's memory, the default;
+ * UINT64_MAX: all but 8 GiB of free memory), max_candidates = candidates drawn in all (0: 24). */
+int32_t nx_workspace_placement_config(uint64_t peak_bytes, int32_t max_candidates);
+/* The launches nx_snappy_encode_batch makes for n chunks on the current device and its present
+ * Snappy workspace: *count launches of sizes[0..*count) chunks (at most cap written).  Equal
+ * full-occupancy launches (1 638 400 chunks: 5 x 327 680 on 256 CUs); a caller cutting a large job
+ * into calls (bench.py) makes each call one of them. */
+int32_t nx_snappy_encode_plan(uint32_t n, uint32_t* sizes, uint32_t cap, uint32_t* count);
 int32_t nx_workspaces_trim(void);
 int32_t nx_workspaces_forget_stream(void* stream);
 int32_t nx_workspace_info(int32_t kind, uint64_t* bytes, int32_t* owners);
@@ -213,8 +229,10 @@ int32_t nx_lz4_encode_batch(const uint8_t* in, const uint64_t* in_off, const uin
 /* Same contract for lz4-java's highCompressor() (Lz4FrameEncoder(highCompressor = true),
  * Lz4FrameEncoder.java:123-125,161-163): liblz4's LZ4_compress_HC at level 9 (hash-chain match finder,
  * 256 candidates, pattern analysis, lazy three-match parse), bit-exact with the oracle's restatement,
- * which is pinned byte-for-byte against pyarrow's liblz4 at level 9.  One lane per block with 256 KiB
- * of tables in HBM (NX_WS_LZ4HC_ENC): a compatibility path, far slower than the fast compressor. */
+ * which is pinned byte-for-byte against pyarrow's liblz4 at level 9.  One block per wave (lane 0) with
+ * 256 KiB of tables in HBM per wave, on at most 2 waves per CU: the NX_WS_LZ4HC_ENC workspace never
+ * exceeds CUs x 2 x 256 KiB (128 MiB on 256 CUs).  A compatibility path, far slower than the fast
+ * compressor (below a 16-core host's liblz4; INTEGRATION.md keeps HC on the JVM). */
 int32_t nx_lz4hc_encode_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                               const uint64_t* out_off, uint32_t* out_len, int32_t* status, uint32_t n, void* stream);
 

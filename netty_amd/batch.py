@@ -25,7 +25,7 @@ def _chk(rc, what):
 
 
 # Shared device workspaces (include/netty_amd.h NX_WS_*; csrc/workspace.hpp)
-WS_SNAPPY_ENC, WS_LZ4_ENC, WS_FASTLZ_ENC, WS_LZF_ENC, WS_DEC_RECORDS = range(5)
+WS_SNAPPY_ENC, WS_LZ4_ENC, WS_FASTLZ_ENC, WS_LZF_ENC, WS_DEC_RECORDS, WS_LZ4HC_ENC = range(6)
 
 
 def workspace_info(kind: int) -> tuple[int, int]:
@@ -39,6 +39,22 @@ def workspace_info(kind: int) -> tuple[int, int]:
 def workspaces_trim():
     """Free the current device's workspaces that no batcher or handle holds."""
     _chk(_lib.load().nx_workspaces_trim(), "nx_workspaces_trim")
+
+
+def snappy_encoder_reserve(max_chunks: int, max_bytes: int = 0) -> tuple[int, int]:
+    """nx_snappy_encoder_reserve_ex: place the Snappy table workspace now, capped at max_bytes for good
+    (0: no cap).  Returns (workspace bytes, most bytes its placement held at once)."""
+    import ctypes as C
+    b, p = C.c_uint64(0), C.c_uint64(0)
+    _chk(_lib.load().nx_snappy_encoder_reserve_ex(max_chunks, max_bytes, _stream(), C.byref(b), C.byref(p)),
+         "nx_snappy_encoder_reserve_ex")
+    return b.value, p.value
+
+
+def workspace_placement_config(peak_bytes: int = 0, max_candidates: int = 0):
+    """nx_workspace_placement_config: the bytes a large workspace's placement candidates may hold at once
+    (0: half the device; 2**64 - 1: all but 8 GiB free) and the candidates drawn in all (0: 24)."""
+    _chk(_lib.load().nx_workspace_placement_config(peak_bytes, max_candidates), "nx_workspace_placement_config")
 
 
 def snappy_max_compressed_length(n: int) -> int:

@@ -1051,11 +1051,8 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
     // previous batch's 500 MB result copy held this batch's gather (and, for an op list in pageable
     // memory, the submitting thread) until that copy ended (round 4 e2e trace).  A large staging
     // arena (payloads copied at submit) still goes by one DMA copy.
-    static const uint64_t stage_max = [] {  // NX_GATHER_STAGE_MAX_MIB: A/B of the copied-payload upload path
-        const char* e = getenv("NX_GATHER_STAGE_MAX_MIB");
-        return e ? (uint64_t)strtoull(e, nullptr, 10) << 20 : nx::bt::kGatherStageMax;
-    }();
-    const bool dma_in = bt->direct.empty() && bt->st_used > stage_max;
+    // (round 5 measured the whole staging arena through the gather as well, profiles/r05/s10: no better)
+    const bool dma_in = bt->direct.empty() && bt->st_used > nx::bt::kGatherStageMax;
     if (dma_in) {
         NX_HIP_CHECK(hipMemcpyAsync(din, bt->staging.h, bt->st_used, hipMemcpyHostToDevice, s));
     } else if (bt->st_used || !bt->direct.empty()) {

@@ -178,6 +178,20 @@ constexpr size_t kPlaceMinBytes = (size_t)2 << 30;  // smaller workspaces (handl
 constexpr int kPlaceCandidates = 6;  // drawn at once (each while the others are held, so each lands elsewhere)
 constexpr int kPlaceRounds = 4;      // draws; the best so far is held through the next draw
 constexpr uint32_t kPlaceSteps = 256;
+constexpr size_t kPlaceFreeReserve = (size_t)8 << 30;  // a candidate is drawn only while this much stays free
+
+// Process-wide bound on the placement (nx_workspace_placement_config): the bytes the candidates of one
+// workspace may hold at once (0: half of the device's memory; ~0: everything but kPlaceFreeReserve, the
+// round-5 behaviour) and the candidates drawn in all (0: kPlaceCandidates * kPlaceRounds).  A server
+// sharing its GPU keeps the default; a process that owns the device (bench.py) may lift it.
+inline uint64_t& placement_peak_cap() {
+    static uint64_t v = 0;
+    return v;
+}
+inline int& placement_max_candidates() {
+    static int v = 0;
+    return v;
+}
 
 // Allocate a zeroed workspace of `lanes` tables of 2^lg entries each.  A large one is the fastest of
 // kPlaceRounds draws of up to kPlaceCandidates allocations under k_ws_probe: within a draw the
@@ -186,11 +200,14 @@ constexpr uint32_t kPlaceSteps = 256;
 // candidates were all slow, profiles/r03/s6, left the encoder ~4 % slower; scripts/experiments/
 // placement_redraw.py shows later draws reaching the fast placements; round 4: a box whose twelve
 // candidates in two draws held no fast one ran the encoder at 55.3 GiB/s against 57.0-57.8 elsewhere,
-// profiles/r04/s5, so four draws of six).  A candidate is only drawn while 8 GiB stay free.
+// profiles/r04/s5, so four draws of six).  A candidate is only drawn while kPlaceFreeReserve stays
+// free and while the candidates held at once stay within placement_peak_cap() (round 6: by default
+// half of the device, so reserving a workspace never takes all free HBM, even for a moment).
 struct PlacementReport {
     int n = 0;      // candidates probed (0: allocated directly, below kPlaceMinBytes)
     int pick = -1;  // the one kept
     float ms[kPlaceCandidates * kPlaceRounds] = {};
+    uint64_t peak = 0;  // most bytes the candidates held at once
 };
 template <typename E>
 inline hipError_t alloc_placed_workspace(size_t lanes, uint32_t lg, hipStream_t st, E** out, PlacementReport* rep = nullptr) {
@@ -199,27 +216,43 @@ inline hipError_t alloc_placed_workspace(size_t lanes, uint32_t lg, hipStream_t 
     if (bytes < kPlaceMinBytes || lanes % 256 != 0) {
         hipError_t e = hipMalloc(out, bytes);
         if (e == hipSuccess) e = hipMemsetAsync(*out, 0, bytes, st);
+        if (e == hipSuccess && rep) {
+            *rep = PlacementReport{};
+            rep->peak = bytes;
+        }
         return e;
     }
+    uint64_t peak_cap = placement_peak_cap();
+    if (peak_cap == 0) {
+        size_t free_b = 0, total_b = 0;
+        peak_cap = hipMemGetInfo(&free_b, &total_b) == hipSuccess ? total_b / 2 : 4 * (uint64_t)bytes;
+    }
+    const int max_cand = placement_max_candidates() > 0 ? placement_max_candidates() : kPlaceCandidates * kPlaceRounds;
     hipEvent_t a = nullptr, b = nullptr;
     hipError_t e = hipEventCreate(&a);
     if (e == hipSuccess) e = hipEventCreate(&b);
     E* best_p = nullptr;
     float best_ms = 3.4e38f;
     int n_all = 0, pick = -1;
+    uint64_t peak = 0;
     float all_ms[kPlaceCandidates * kPlaceRounds];
-    for (int round = 0; round < kPlaceRounds && e == hipSuccess; ++round) {
+    for (int round = 0; round < kPlaceRounds && e == hipSuccess && n_all < max_cand; ++round) {
         E* cand[kPlaceCandidates];
         float ms[kPlaceCandidates];
         int nc = 0;
-        while (nc < kPlaceCandidates && e == hipSuccess) {
+        uint64_t held = best_p ? (uint64_t)bytes : 0;
+        while (nc < kPlaceCandidates && n_all + nc < max_cand && e == hipSuccess) {
             size_t free_b = 0, total_b = 0;
-            if ((nc > 0 || best_p) && (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + ((size_t)8 << 30))) break;
+            if ((nc > 0 || best_p) &&
+                (held + bytes > peak_cap || hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + kPlaceFreeReserve))
+                break;
             E* p = nullptr;
             if (hipMalloc(&p, bytes) != hipSuccess) {
                 (void)hipGetLastError();  // no memory for another candidate: choose among those drawn
                 break;
             }
+            held += bytes;
+            if (held > peak) peak = held;
             cand[nc] = p;
             ms[nc] = 3.4e38f;
             ++nc;
@@ -259,6 +292,7 @@ inline hipError_t alloc_placed_workspace(size_t lanes, uint32_t lg, hipStream_t 
         rep->n = n_all;
         rep->pick = pick;
         for (int k = 0; k < n_all; ++k) rep->ms[k] = all_ms[k];
+        rep->peak = peak;
     }
     return hipMemsetAsync(*out, 0, bytes, st);  // the probe wrote entries: back to a zeroed table
 }

@@ -1190,8 +1190,6 @@ __global__ void __launch_bounds__(kExpandWaves * 64, kExpandStaged ? 6 : 3)
 }
 
 
-#include "expand_units.hpp"
-#include "expand_frame.hpp"
 
 
 // =====================================================================================
@@ -1628,45 +1626,15 @@ static hipError_t wave_kernel_attrs(size_t lds) {
         attr_err = hipFuncSetAttribute((const void*)nx::dec::k_decode_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (attr_err == hipSuccess)
             attr_err = hipFuncSetAttribute((const void*)nx::dec::k_expand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kExpandLds);
-        if (attr_err == hipSuccess)
-            attr_err = hipFuncSetAttribute((const void*)nx::dec::k_expand_u, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nx::dec::kUxLds);
-        if (attr_err == hipSuccess)
-            attr_err = hipFuncSetAttribute((const void*)nx::dec::k_expand_f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nx::dec::kFxLds);
     });
     return attr_err;
-}
-
-// Which record expander launch_expand runs: the piece expander k_expand (0), or one of the round-5
-// experiments kept for same-box A/B runs (DESIGN.md §4 "Round 5"): the unit-lane k_expand_u
-// (NX_EXPANDER=units, 1) or the frame-window k_expand_f (NX_EXPANDER=frame, 2).  Read once per process.
-static int expander_choice() {
-    static const int which = [] {
-        const char* e = getenv("NX_EXPANDER");
-        if (e && strcmp(e, "units") == 0) return 1;
-        if (e && strcmp(e, "frame") == 0) return 2;
-        return 0;
-    }();
-    return which;
 }
 
 // one launch of the record expander over m frames
 static hipError_t launch_expand(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
                                 const uint32_t* rec, const uint32_t* nrec, uint32_t* out_len, int32_t* status, const uint32_t* expect,
-                                uint32_t* crc_out, uint32_t m, int cus, hipStream_t st, uint32_t* need_fused) {
+                                uint32_t* crc_out, uint32_t m, int cus, hipStream_t st) {
     using namespace nx::dec;
-    if (expander_choice() == 2) {  // one workgroup (two frame windows) per CU
-        const uint64_t need = (m + 1u) / 2u, want = (uint64_t)cus;
-        hipLaunchKernelGGL(k_expand_f, dim3((unsigned)(need < want ? need : want)), dim3(256), kFxLds, st, in, in_off, in_len, out,
-                           out_off, rec, nrec, out_len, status, expect, crc_out, m, nx::crc_tables_dev(), need_fused);
-        return hipGetLastError();
-    }
-    if (expander_choice() == 1) {
-        const uint64_t per_cu = 160 * 1024 / kUxLds;
-        const uint64_t want = (uint64_t)cus * per_cu, need = (m + kUxWaves - 1) / kUxWaves;
-        hipLaunchKernelGGL(k_expand_u, dim3((unsigned)(need < want ? need : want)), dim3(kUxWaves * 64), kUxLds, st, in, in_off, in_len,
-                           out, out_off, rec, nrec, out_len, status, expect, crc_out, m, nx::crc_tables_dev());
-        return hipGetLastError();
-    }
 #ifdef NX_EXPAND_BLOCKS_PER_CU
     const uint64_t per_cu = NX_EXPAND_BLOCKS_PER_CU;
 #else
@@ -1703,13 +1671,6 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
     // one lane, ~4-7 ms for any batch that does not fill the chip, while k_decode_fused parses each
     // frame wave-parallel (0.85 ms for one frame, 1.9 ms for 4 096, 5.6 ms for 16 384, against 4.3 /
     // 7.4 / 9.1 for the pair).  The pair wins from ~34 K frames on (65 536: 16.4 vs 20.5 ms).
-    static const int forced = [] {  // NX_DECODE_MODE=pair|fused overrides "auto" (A/B runs of callers such as the batcher)
-        const char* e = getenv("NX_DECODE_MODE");
-        if (e && strcmp(e, "pair") == 0) return (int)kDecodePair;
-        if (e && strcmp(e, "fused") == 0) return (int)kDecodeFused;
-        return (int)kDecodeAuto;
-    }();
-    if (mode == kDecodeAuto) mode = forced;
     const bool fused_only = mode == kDecodeFused || (mode == kDecodeAuto && n <= kFusedMaxFrames);
     if (fused_only) {
         hipLaunchKernelGGL(k_decode_fused, dim3(wave_grid(n)), dim3(kWaves * 64), lds, st, in, in_off, in_len, out, out_off, out_cap,
@@ -1732,7 +1693,7 @@ static int32_t decode_batch(const uint8_t* in, const uint64_t* in_off, const uin
         NX_HIP_CHECK(hipGetLastError());
         NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W.rec, W.nrec, out_len + base, status + base,
                                    expected_masked_crc ? expected_masked_crc + base : nullptr, crc_out ? crc_out + base : nullptr, m,
-                                   cus, st, W.olen));
+                                   cus, st));
         // frames k_parse could not slot (more than kRecCap records, or input >= 32 MiB)
         hipLaunchKernelGGL(k_decode_fused, dim3(wave_grid(m)), dim3(kWaves * 64), lds, st, in, in_off + base, in_len + base, out,
                            out_off + base, out_cap ? out_cap + base : nullptr, out_len + base, consumed ? consumed + base : nullptr,
@@ -1803,7 +1764,7 @@ extern "C" int32_t nx_lz4_decode_batch(const uint8_t* in, const uint64_t* in_off
         (void)need;
         (void)want;
         NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W->rec, W->nrec, W->olen, status + base, nullptr,
-                                   nullptr, m, cus, st, nullptr));
+                                   nullptr, m, cus, st));
         hipLaunchKernelGGL(k_lz4_serial, dim3((m + 255) / 256), dim3(256), 0, st, in, in_off + base, in_len + base, out_len + base,
                            out, out_off + base, status + base, m);
         NX_HIP_CHECK(hipGetLastError());
@@ -1843,7 +1804,7 @@ int32_t nx::dec::decode_records(RecCodec codec, const uint8_t* in, const uint64_
                                status + base, m);
         NX_HIP_CHECK(hipGetLastError());
         NX_HIP_CHECK(launch_expand(in, in_off + base, in_len + base, out, out_off + base, W.rec, W.nrec, W.olen, status + base, nullptr,
-                                   nullptr, m, cus, st, nullptr));
+                                   nullptr, m, cus, st));
         NX_HIP_CHECK(after(base, m, W.olen, ctx, st));
     }
     return NX_OK;

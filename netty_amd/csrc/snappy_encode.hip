@@ -3,8 +3,8 @@
 // Netty's greedy matcher is a serial state machine whose output depends on the exact probe order
 // (the `skip++ >> 5` heuristic, :107-115) and on an evolving 16384-entry hash table (:97-100,
 // 126-128, 148-152).  There is no safe intra-chunk speculation, so each chunk is one lane's serial
-// state machine and the parallelism is the thousands of independent chunks of a batch (16 waves
-// per CU → 262 144 chunks in flight on 256 CUs).  What the kernel optimises is the memory side of
+// state machine and the parallelism is the thousands of independent chunks of a batch (20 waves
+// per CU → 327 680 chunks in flight on 256 CUs).  What the kernel optimises is the memory side of
 // each lane's dependency chain:
 //   * every 4-byte window is one unaligned dword load (Java's big-endian getInt = bswap), and the
 //     bytes at the probe position are reused from the hash computation that loaded them;
@@ -541,16 +541,19 @@ done:
     return w.pos();
 }
 
-// __launch_bounds__(256, 4): at least 4 blocks of 256 (16 waves) per CU, the residency the host
-// launches for, so the kernel stays within 128 VGPRs per lane.
+// __launch_bounds__(256, 5): at least 5 blocks of 256 (20 waves, 5 per SIMD) per CU, the residency
+// the host launches for, so the kernel stays within 96 VGPRs per lane; with the 16-dword output stage
+// (17 KiB of LDS per block) five blocks fit a CU.  Round 6 (profiles/r06/s1, placement-controlled,
+// scripts/experiments/enc_curve.cpp): 313.6 ms per 327 680 chunks (0.957 us per chunk) against
+// 261.6 ms per 262 144 (0.998) for the round-5 kernel at 4 blocks per CU with a 32-dword stage.
 //
 // SPREAD = false: lane t encodes chunks t, t + lanes, ... (throughput form, every lane of a wave busy).
 // SPREAD = true: one chunk per WAVE, lane 0 only (small batches: lanes of different chunks never share
 // a wave's divergent control flow, which otherwise serialises a wave's 64 matchers: 64 chunks in one
 // wave take 6x as long as one).  Lane/wave w owns table slot w of the workspace in either form.
-constexpr int kStageDw = 32;  // dense form: 128-byte output units staged in LDS (33 KiB per 256 lanes)
+constexpr int kStageDw = 16;  // dense form: 64-byte output units staged in LDS (17 KiB per 256 lanes)
 template <bool SWAP, bool SPREAD>
-__global__ void __launch_bounds__(256, 4) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+__global__ void __launch_bounds__(256, 5) k_snappy_encode(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                        const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
                                                        int32_t* __restrict__ status, uint32_t n, uint64_t* __restrict__ workspace,
@@ -657,27 +660,116 @@ namespace {
 constexpr unsigned kEncBlock = 256;
 constexpr uint32_t kMaxStamp = 63;  // 6-bit stamps 1..63
 static_assert(nx::kWsSpec[(int)nx::WsKind::SnappyEnc].entry_bytes == sizeof(uint64_t) &&
-                  nx::kWsSpec[(int)nx::WsKind::SnappyEnc].lg == 14 && nx::kWsSpec[(int)nx::WsKind::SnappyEnc].waves_per_cu == 16,
-              "Snappy table geometry: 16384 64-bit entries, 16 waves per CU");
+                  nx::kWsSpec[(int)nx::WsKind::SnappyEnc].lg == 14 && nx::kWsSpec[(int)nx::WsKind::SnappyEnc].waves_per_cu == 20,
+              "Snappy table geometry: 16384 64-bit entries, 20 waves per CU");
+}  // namespace
+
+namespace {
+constexpr size_t kEncTableBytes = 16384u * sizeof(uint64_t);  // one lane's table (128 KiB)
+
+// Launch sizes of the dense form for n chunks over `slots` resident lanes, one chunk per lane per
+// launch (round 6).  A lane's chain runs faster the fewer waves share its SIMD,
+// so a launch that does not fill the chip is not proportionally shorter: on 256 CUs the round-5
+// kernel took 152 ms for 65 536 chunks and 261.6 for 262 144 (profiles/r06/s1/enc_curve.log), and
+// the bench's 6.25 launches of 262 144 per 100 GiB paid ~90 ms for the quarter launch.  The plan
+// therefore splits n into k = ceil(n / slots) launches as equal as possible in steps of half a block
+// per CU (cus * 128 lanes), the remainder below one step going to the last launch: 1 638 400
+// chunks -> 5 x 327 680; 819 200 -> 294 912 + 2 x 262 144; 409 600 -> 196 608 + 212 992.
+size_t enc_plan(size_t n, size_t slots, int cus, uint32_t* sizes, size_t cap) {
+    auto put = [&](size_t i, size_t v) {
+        if (sizes && i < cap) sizes[i] = (uint32_t)v;
+    };
+    if (n == 0) return 0;
+    if (n <= slots) {
+        put(0, n);
+        return 1;
+    }
+    const size_t k = (n + slots - 1) / slots;
+    const size_t G = (size_t)cus * 128u;
+    const size_t s = n / k / G * G;
+    const size_t rem = n - k * s, plus = rem / G, last = rem - plus * G;  // plus < k
+    if (s > 0 && (plus == 0 || s + G <= slots) && s + last <= slots) {
+        for (size_t i = 0; i < k; ++i) put(i, s + (i < plus ? G : 0) + (i + 1 == k ? last : 0));
+        return k;
+    }
+    const size_t e = (n + k - 1) / k;  // a capped workspace: plain equal launches
+    for (size_t i = 0; i < k; ++i) put(i, std::min(e, n - i * e));
+    return k;
+}
 }  // namespace
 
 // Place and zero the device's encoder table workspace for batches of up to max_chunks chunks now, so
 // a server sets it up at start-up, before its own buffers take the memory the placement choice draws
 // candidates from.  Kept until nx_workspaces_trim.  Optional: the standalone batch
 // API grows it on demand; batchers and handles hold their own share from creation.
-extern "C" int32_t nx_snappy_encoder_reserve(uint32_t max_chunks, void* stream) {
+//
+// _ex (round 6): max_bytes caps the workspace for good (0: no cap; the tables of
+// max_bytes / 128 KiB lanes, whole blocks of 256 above kSpreadMaxChunks lanes): later batches of any
+// size run on those lanes (more launches, or one chunk per wave below kSpreadMaxChunks lanes) and the
+// standalone calls never grow it past the cap until it is trimmed.  *bytes (nullable) = the
+// workspace's bytes, *peak (nullable) = the most bytes its placement held at once
+// (nx_workspace_placement_config bounds that).
+extern "C" int32_t nx_snappy_encoder_reserve_ex(uint32_t max_chunks, uint64_t max_bytes, void* stream, uint64_t* bytes, uint64_t* peak) {
     int dev = 0, cus = 256;
     NX_HIP_CHECK(hipGetDevice(&dev));
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (bytes) *bytes = 0;
+    if (peak) *peak = 0;
     if (max_chunks <= (uint32_t)cus) return NX_OK;  // the LDS form needs no workspace
-    const int32_t r = nx::ws_hold(nx::WsKind::SnappyEnc, dev, max_chunks, (hipStream_t)stream);
+    nx::SharedWs& W = nx::shared_ws(nx::WsKind::SnappyEnc, dev);
+    uint32_t units = max_chunks;
+    if (max_bytes) {
+        size_t lanes = (size_t)(max_bytes / kEncTableBytes);
+        if (lanes > nx::kSpreadMaxChunks) lanes = lanes / 256 * 256;
+        if (lanes == 0) return NX_ERR_INVALID_ARG;
+        std::lock_guard<std::mutex> lk(W.mu);
+        if (W.p && W.slots > lanes) return NX_ERR_INVALID_ARG;  // already larger than the cap: trim first
+        W.cap = lanes;
+        if (units > lanes) units = (uint32_t)lanes;
+    }
+    const int32_t r = nx::ws_hold(nx::WsKind::SnappyEnc, dev, units, (hipStream_t)stream);
     if (r != NX_OK) return r;
     {
-        nx::SharedWs& W = nx::shared_ws(nx::WsKind::SnappyEnc, dev);
         std::lock_guard<std::mutex> lk(W.mu);
         W.kept = true;
+        if (bytes) *bytes = (uint64_t)W.slots * kEncTableBytes;
+        if (peak) *peak = W.place.peak;
     }
     nx::ws_unhold(nx::WsKind::SnappyEnc, dev);
+    return NX_OK;
+}
+
+extern "C" int32_t nx_snappy_encoder_reserve(uint32_t max_chunks, void* stream) {
+    return nx_snappy_encoder_reserve_ex(max_chunks, 0, stream, nullptr, nullptr);
+}
+
+// The launches nx_snappy_encode_batch makes for n chunks on the current device with its present
+// workspace (the one a batch of n would grow to when there is none yet): *count launches of
+// sizes[0..] chunks (at most `cap` written).  A caller that cuts a large job into encode calls uses
+// it so that each call is one full-occupancy launch (bench.py).
+extern "C" int32_t nx_snappy_encode_plan(uint32_t n, uint32_t* sizes, uint32_t cap, uint32_t* count) {
+    if (!count || (cap && !sizes)) return NX_ERR_INVALID_ARG;
+    int dev = 0, cus = 256;
+    NX_HIP_CHECK(hipGetDevice(&dev));
+    NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    *count = 0;
+    if (n == 0) return NX_OK;
+    if (n <= (uint32_t)cus) {  // the LDS form: one launch
+        if (cap) sizes[0] = n;
+        *count = 1;
+        return NX_OK;
+    }
+    nx::SharedWs& W = nx::shared_ws(nx::WsKind::SnappyEnc, dev);
+    std::lock_guard<std::mutex> lk(W.mu);
+    const size_t want = nx::ws_capped(W, nx::ws_want(nx::WsKind::SnappyEnc, n, cus));
+    const size_t have = W.p && W.slots >= want ? W.slots : std::max(want, W.p ? W.slots : (size_t)0);
+    const nx::LaneGrid g = nx::ws_grid(nx::WsKind::SnappyEnc, n, cus, have);
+    if (g.spread) {
+        if (cap) sizes[0] = n;
+        *count = 1;
+        return NX_OK;
+    }
+    *count = (uint32_t)enc_plan(n, g.slots, cus, sizes, cap);
     return NX_OK;
 }
 
@@ -705,31 +797,43 @@ extern "C" int32_t nx_snappy_encode_batch(const uint8_t* in, const uint64_t* in_
         NX_HIP_CHECK(hipGetLastError());
         return NX_OK;
     }
-    const size_t per = 16384u * sizeof(uint64_t);
     nx::WsLease lease(nx::WsKind::SnappyEnc, dev, st);
     NX_HIP_CHECK(lease.acquire(nx::ws_want(nx::WsKind::SnappyEnc, n, cus)));
     nx::SharedWs& W = lease.ws();
     const nx::LaneGrid g = nx::ws_grid(nx::WsKind::SnappyEnc, n, cus, W.slots);
     uint64_t* ws = static_cast<uint64_t*>(W.p);
-    // Each launch gives a table slot at most kMaxStamp - 1 chunks (one stamp each).
-    const size_t per_launch = g.slots * (kMaxStamp - 1);
-    for (size_t base = 0; base < n; base += per_launch) {
-        const uint32_t m = (uint32_t)std::min<size_t>(per_launch, n - base);
-        const uint32_t iters = (uint32_t)((m + g.slots - 1) / g.slots);
-        if (W.stamp + iters >= kMaxStamp) {
-            NX_HIP_CHECK(hipMemsetAsync(ws, 0, W.slots * per, st));
-            W.stamp = 0;
-        }
-        if (g.spread) {
+    auto stamps = [&](uint32_t iters) -> hipError_t {  // 6-bit stamps: re-zero the tables before a wrap
+        if (W.stamp + iters < kMaxStamp) return hipSuccess;
+        W.stamp = 0;
+        return hipMemsetAsync(ws, 0, W.slots * kEncTableBytes, st);
+    };
+    if (g.spread) {  // one chunk per wave; a wave takes at most kMaxStamp - 1 chunks per launch
+        const size_t per_launch = g.slots * (kMaxStamp - 1);
+        for (size_t base = 0; base < n; base += per_launch) {
+            const uint32_t m = (uint32_t)std::min<size_t>(per_launch, n - base);
+            const uint32_t iters = (uint32_t)((m + g.slots - 1) / g.slots);
+            NX_HIP_CHECK(stamps(iters));
             const size_t waves = std::min<size_t>(g.slots, m);
             hipLaunchKernelGGL((nx::enc::k_snappy_encode<true, true>), dim3((unsigned)waves), dim3(64), 0, st, in, in_off + base,
                                in_len + base, out, out_off + base, out_len + base, status + base, m, ws, W.stamp);
-        } else {
-            hipLaunchKernelGGL((nx::enc::k_snappy_encode<true, false>), dim3((unsigned)(g.slots / kEncBlock)), dim3(kEncBlock), 0, st, in,
-                               in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, ws, W.stamp);
+            NX_HIP_CHECK(hipGetLastError());
+            W.stamp += iters;
         }
+        return NX_OK;
+    }
+    // the dense form: one chunk per lane per launch, launches planned by enc_plan
+    const size_t k = enc_plan(n, g.slots, cus, nullptr, 0);
+    std::vector<uint32_t> sizes(k);
+    enc_plan(n, g.slots, cus, sizes.data(), k);
+    size_t base = 0;
+    for (size_t i = 0; i < k; ++i) {
+        const uint32_t m = sizes[i];
+        NX_HIP_CHECK(stamps(1));
+        hipLaunchKernelGGL((nx::enc::k_snappy_encode<true, false>), dim3((m + kEncBlock - 1) / kEncBlock), dim3(kEncBlock), 0, st, in,
+                           in_off + base, in_len + base, out, out_off + base, out_len + base, status + base, m, ws, W.stamp);
         NX_HIP_CHECK(hipGetLastError());
-        W.stamp += iters;
+        W.stamp += 1;
+        base += m;
     }
     return NX_OK;
 }

@@ -77,13 +77,27 @@ hipError_t ws_grow(WsKind k, SharedWs& W, size_t slots, hipStream_t st) {
 
 SharedWs& shared_ws(WsKind k, int dev) { return g_ws[(int)k][dev < 0 || dev >= kMaxDevices ? 0 : dev]; }
 
+// LZ4 HC: always one block per wave on at most cus * waves_per_cu waves (128 MiB of
+// tables on 256 CUs).  Its dense form would hold 32 768 lanes x 256 KiB = 8 GiB (and draw placement
+// candidates of that size) for a compatibility path whose 256-candidate chains run no faster dense.
+size_t hc_slots(uint32_t n, int cus) { return std::min<size_t>(n, (size_t)cus * kWsSpec[(int)WsKind::Lz4HcEnc].waves_per_cu); }
+
 size_t ws_want(WsKind k, uint32_t n, int cus) {
     if (k == WsKind::DecRecords) return std::min<uint32_t>(n, kDecMaxFrames);
+    if (k == WsKind::Lz4HcEnc) return hc_slots(n, cus);
     return lane_grid(n, cus, kWsSpec[(int)k].waves_per_cu).slots;
 }
 
 LaneGrid ws_grid(WsKind k, uint32_t n, int cus, size_t have) {
     const unsigned wpcu = kWsSpec[(int)k].waves_per_cu;
+    if (k == WsKind::Lz4HcEnc) {
+        LaneGrid g;
+        g.spread = true;
+        g.block = 64;
+        g.slots = std::max<size_t>(1, std::min(hc_slots(n, cus), have));
+        g.grid = (unsigned)g.slots;
+        return g;
+    }
     LaneGrid g = lane_grid(n, cus, wpcu);
     if (g.slots <= have) return g;
     if (!g.spread && have >= kSpreadMaxChunks) {
@@ -135,6 +149,7 @@ WsLease::~WsLease() {
 }
 
 hipError_t WsLease::acquire(size_t want) {
+    want = ws_capped(W_, want);
     if (!W_.p || (!t_no_grow && W_.slots < want)) {
         const hipError_t e = ws_grow(k_, W_, std::max(want, W_.slots), st_);
         if (e != hipSuccess) return e;
@@ -149,6 +164,7 @@ hipError_t WsLease::acquire(size_t want) {
 }
 
 hipError_t WsLease::acquire_part(size_t want, size_t* first, size_t* count) {
+    want = ws_capped(W_, want);
     if (!W_.p || (!t_no_grow && W_.slots < want)) {
         const hipError_t e = ws_grow(k_, W_, std::max(want, W_.slots), st_);
         if (e != hipSuccess) return e;
@@ -204,7 +220,7 @@ int32_t ws_hold(WsKind k, int dev, uint32_t units, hipStream_t st) {
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     SharedWs& W = shared_ws(k, dev);
     std::lock_guard<std::mutex> lk(W.mu);
-    NX_HIP_CHECK(ws_grow(k, W, std::max(ws_want(k, units, cus), W.slots), st));
+    NX_HIP_CHECK(ws_grow(k, W, std::max(ws_capped(W, ws_want(k, units, cus)), W.slots), st));
     W.owners += 1;
     return NX_OK;
 }
@@ -230,6 +246,7 @@ extern "C" int32_t nx_workspaces_trim(void) {
         std::lock_guard<std::mutex> lk(W.mu);
         W.kept = false;
         if (W.owners == 0) {
+            W.cap = 0;  // a reserve's cap lasts until its workspace is freed
             const hipError_t e = nx::ws_drop(W);
             if (e != hipSuccess) r = nx_hip_fail(e, __FILE__, __LINE__ + k * 1000);  // line + 1000 * kind under NX_HIP_DEBUG
         }
@@ -256,5 +273,16 @@ extern "C" int32_t nx_workspace_info(int32_t kind, uint64_t* bytes, int32_t* own
     const nx::WsSpec& s = nx::kWsSpec[kind];
     *bytes = kind == (int32_t)nx::WsKind::DecRecords ? W.slots * nx::kDecSlotBytes : W.slots * ((size_t)s.entry_bytes << s.lg);
     *owners = W.owners;
+    return NX_OK;
+}
+
+// The placement bound of every later large workspace (nx_common.hpp placement_peak_cap /
+// placement_max_candidates): peak_bytes = the bytes the candidates of one workspace may hold at once
+// (0: half of the device's memory, the default; UINT64_MAX: all but 8 GiB of free memory), and
+// max_candidates = the candidates drawn in all (0: the default 24; 1: no placement choice).
+extern "C" int32_t nx_workspace_placement_config(uint64_t peak_bytes, int32_t max_candidates) {
+    if (max_candidates < 0) return NX_ERR_INVALID_ARG;
+    nx::placement_peak_cap() = peak_bytes;
+    nx::placement_max_candidates() = max_candidates;
     return NX_OK;
 }

@@ -29,9 +29,10 @@ struct WsSpec {
     uint32_t lg;
     unsigned waves_per_cu;
 };
+// SnappyEnc: 20 waves per CU (5 blocks of 256, 327 680 lanes on 256 CUs: 40 GiB of tables; round 6).
 // Lz4HcEnc: 2^15 x 8 bytes = liblz4's HC tables per lane (u32 hashTable[2^15] + u16 chainTable[2^16]),
-// 2 waves per CU (a dense launch holds 32 768 lanes, 8 GiB).
-constexpr WsSpec kWsSpec[] = {{8, 14, 16}, {8, 13, 16}, {8, 13, 8}, {8, 14, 8}, {0, 0, 0}, {8, 15, 2}};
+// 2 waves per CU, always one block per wave (kHcMaxSlots: at most cus * 2 tables, 128 MiB on 256 CUs).
+constexpr WsSpec kWsSpec[] = {{8, 14, 20}, {8, 13, 16}, {8, 13, 8}, {8, 14, 8}, {0, 0, 0}, {8, 15, 2}};
 constexpr size_t kDecSlotBytes = 16384u * 4u + 8u;  // records of one frame + its count and length
 constexpr uint32_t kDecMaxFrames = 262144;           // frames per parse/expand launch pair
 
@@ -53,8 +54,11 @@ struct SharedWs {
     bool used = false;   // ev has been recorded
     int owners = 0;      // batchers and handles holding it
     bool kept = false;   // grown by the standalone API or a reserve: kept until nx_workspaces_trim
+    size_t cap = 0;      // most slots it may ever grow to (nx_snappy_encoder_reserve_ex; 0: no cap)
     PlacementReport place;
 };
+// the slots a grow to `want` may take under W's cap
+inline size_t ws_capped(const SharedWs& W, size_t want) { return W.cap && want > W.cap ? W.cap : want; }
 
 SharedWs& shared_ws(WsKind k, int dev);
 // slots a batch of n units asks for: the encoders' lane_grid slots, the decoder's frames per launch

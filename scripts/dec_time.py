@@ -43,7 +43,7 @@ def main():
     ok = bool(torch.equal(dec, src)) and int((r["status"] != 0).sum()) == 0 and int((est != 0).sum()) == 0
     C = int(elen.to(torch.int64).sum())
     ms = min(ts)
-    print(json.dumps({"expander": os.environ.get("NX_EXPANDER", "pieces"), "chunks": n, "decode_ms": round(ms, 3),
+    print(json.dumps({"chunks": n, "decode_ms": round(ms, 3),
                       "all_ms": [round(t, 2) for t in ts], "gib_s": round(n * L / (ms / 1e3) / 2**30, 1),
                       "algo_gbs": round((C + n * L) / (ms / 1e3) / 1e9, 1), "verified": ok}))
 

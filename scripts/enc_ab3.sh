@@ -2,7 +2,8 @@
 # Build the placement-controlled encoder A/B (scripts/experiments/enc_ab3.cpp) for a pair of kernel
 # sources: A = the product's snappy_encode.hip, B = $1 (a modified copy).  Each is amalgamated with
 # nx_common.hpp (kernel part only: cut before the host entry points) so both builds live in their own
-# namespace in one binary.  Output: scripts/experiments/bin/enc_ab3_$2.
+# namespace in one binary.  Output: scripts/experiments/bin/enc_ab3_$2 (MAIN=enc_curve: the
+# chunks-per-launch curve harness instead, scripts/experiments/enc_curve.cpp).
 set -eu
 cd "$(dirname "$0")/.."
 B=${1:?variant source}
@@ -36,8 +37,8 @@ cat > scripts/experiments/bin/prelude_$TAG.cpp <<EOF
 #include "../../../include/netty_amd_status.h"
 #define ENC_A "bin/encA.hip"
 #define ENC_B "bin/encB_$TAG.hip"
-#include "../enc_ab3.cpp"
+#include "../${MAIN:-enc_ab3}.cpp"
 EOF
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics -I netty_amd/csrc \
-    -o scripts/experiments/bin/enc_ab3_$TAG scripts/experiments/bin/prelude_$TAG.cpp
-echo built scripts/experiments/bin/enc_ab3_$TAG
+    -o scripts/experiments/bin/${MAIN:-enc_ab3}_$TAG scripts/experiments/bin/prelude_$TAG.cpp
+echo built scripts/experiments/bin/${MAIN:-enc_ab3}_$TAG

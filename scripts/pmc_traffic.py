@@ -1,6 +1,9 @@
 """Summarise the FETCH_SIZE / WRITE_SIZE passes of scripts/pmc_traffic.sh per kernel: HBM bytes per
-dispatch and per 64 KiB chunk.  The passes run bench.py with --total-chunks = --sub-chunks = CHUNKS,
-so every dispatch of the CRC / encode / decode kernels covers exactly CHUNKS chunks.  FETCH_SIZE is
+64 KiB chunk.  The passes run bench.py over --total-chunks CHUNKS with the bench's own call shapes (round
+6: one encode launch of CHUNKS = 327 680, decode calls of 262 144 + 65 536 frames).  Every pass over
+the chunks (the timed step, verify's pass and its first-call re-runs) runs one CRC32C dispatch per
+encode call, with the encode and decode of the same chunks beside it, so a kernel's bytes per chunk =
+its total bytes / (CHUNKS x CRC dispatches / encode calls per pass).  FETCH_SIZE is
 doubled as MI355X_MICROARCH.md's HBM section prescribes for gfx950 (it tallies 128-B read requests
 at 64 B); WRITE_SIZE is taken as is.  The summary records the digest of the kernel sources it was
 taken on (bench.source_digest()); bench.py uses a summary only when that digest matches.  Units: bytes."""
@@ -19,15 +22,23 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
                 continue
             agg[name][r["Counter_Name"]] += float(r["Counter_Value"]) * 1024.0  # KiB -> bytes
             disp[(name, c)].add(r["Dispatch_Id"])
+calls = 1  # encode calls per pass: from the bench line the pass printed
+for line in open(f"{root}/traffic_FETCH_SIZE.log", errors="ignore"):
+    if line.startswith("{"):
+        calls = len(json.loads(line)["config"]["calls"]["encode_calls"])
+crc = [k for k in agg if k.startswith("nx::k_crc32c_masked")]
+passes = max(len(disp[(crc[0], "FETCH_SIZE")]), 1) / calls if crc else 1.0
 out = {"source": f"rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE; bench.py --total-chunks {chunks} "
-                 f"--sub-chunks {chunks} --steps 1 --warmup 0 --weak-chunks 0",
-       "source_digest": bench.source_digest(), "fetch_correction": 2.0, "chunks_per_dispatch": chunks, "kernels": {}}
+                 f"--steps 1 --warmup 0 --weak-chunks 0 (the bench's call shapes)",
+       "source_digest": bench.source_digest(), "fetch_correction": 2.0, "chunks_per_pass": chunks, "passes": passes,
+       "kernels": {}}
 for name, d in agg.items():
     nd = max(len(disp[(name, "FETCH_SIZE")]), len(disp[(name, "WRITE_SIZE")]), 1)
     fetch, write = d.get("FETCH_SIZE", 0.0), d.get("WRITE_SIZE", 0.0)
+    per = chunks * passes
     out["kernels"][name] = {"dispatches": nd, "fetch_bytes": fetch, "write_bytes": write,
                             "hbm_bytes_total": 2.0 * fetch + write,
-                            "read_bytes_per_chunk": 2.0 * fetch / (chunks * nd),
-                            "write_bytes_per_chunk": write / (chunks * nd),
-                            "hbm_bytes_per_chunk": (2.0 * fetch + write) / (chunks * nd)}
+                            "read_bytes_per_chunk": 2.0 * fetch / per,
+                            "write_bytes_per_chunk": write / per,
+                            "hbm_bytes_per_chunk": (2.0 * fetch + write) / per}
 print(json.dumps(out, indent=1))

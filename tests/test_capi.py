@@ -58,3 +58,19 @@ def test_product_has_no_oracle_dependency():
                                      flags=re.M), f
     out = subprocess.check_output(["ldd", os.path.join(pkg, "libnetty_amd.so")], text=True)
     assert "oracle" not in out
+
+
+def test_one_decode_path_no_environment_kernel_selection():
+    """the library's kernel choice never depends on the environment.  The only
+    getenv calls left in netty_amd/csrc are diagnostics (error text, a fault trace, scan statistics)."""
+    allowed = {"NX_HIP_DEBUG", "NX_SEGV_TRACE", "NX_SCAN_STATS"}
+    src = os.path.join(ROOT, "netty_amd", "csrc")
+    seen = set()
+    for f in os.listdir(src):
+        txt = open(os.path.join(src, f), errors="ignore").read()
+        for name in re.findall(r'getenv\("([A-Z0-9_]+)"\)', txt):
+            seen.add(name)
+            assert name in allowed, (f, name)
+    assert "NX_EXPANDER" not in seen and "NX_DECODE_MODE" not in seen
+    for f in ("expand_units.hpp", "expand_frame.hpp"):
+        assert not os.path.exists(os.path.join(src, f))

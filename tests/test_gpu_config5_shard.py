@@ -53,10 +53,59 @@ def test_rank3_of_8_shard_sub_batches(dev, oracle):
         torch.cuda.synchronize()
         el = leg.elen[lo:lo + m].cpu().tolist()
         for k in sorted({0, m // 2, m - 1}):
-            got = leg.enc[k * leg.cap:k * leg.cap + el[k]].cpu().numpy().tobytes()
+            o = int(leg.eoff[lo + k])
+            got = leg.enc[o:o + el[k]].cpu().numpy().tobytes()
             assert got == oracle.snappy_encode(oracle.textgen_chunk(first + lo + k, CHUNK)), (lo, k)
         assert torch.equal(leg.dec[:m * CHUNK], leg.src[lo * CHUNK:(lo + m) * CHUNK])
     assert int((leg.dst != 0).sum()) == 0 and int((leg.est != 0).sum()) == 0
+
+
+def test_ring_schedule_encode_decode_calls_differ(dev, oracle):
+    """Round 6: encode calls and decode calls of different sizes over a ring of encode slots smaller
+    than the shard (bench.SnappyRoundTrip as the 100 GiB job runs it: 5 x 327 680 encodes, 262 144-frame
+    decodes).  Encodes 96 / 96 / 108, decodes of 64 over a 171-slot ring: the ring wraps, decode calls
+    straddle encode calls, the last decode takes the rest."""
+    import bench
+    first, n = 1000, 300
+    leg = bench.SnappyRoundTrip(torch, dev, first, n, dec_sub=64, enc_sizes=[96, 96, 108])
+    assert leg.ring == 108 + 63 and leg.ring < n
+    assert leg.ops == bench.schedule([96, 96, 108], 64)
+    assert [m for k, _, m in leg.ops if k == "dec"] == [64, 64, 64, 64, 44]
+    leg.step()
+    ok, detect = leg.verify(0)
+    assert ok and detect
+    leg.step()
+    torch.cuda.synchronize()
+    # after a step the ring holds the chunks of the last ring-full: their bytes are the oracle's
+    el = leg.elen.cpu().tolist()
+    for c in (n - leg.ring, n - 100, n - 1):
+        o = int(leg.eoff[c])
+        assert o == (c % leg.ring) * leg.cap
+        got = leg.enc[o:o + el[c]].cpu().numpy().tobytes()
+        assert got == oracle.snappy_encode(oracle.textgen_chunk(first + c, CHUNK)), c
+    want = [len(oracle.snappy_encode(oracle.textgen_chunk(first + i, CHUNK))) for i in range(n)]
+    assert el == want
+
+
+def test_encode_plan_launch_sizes(dev):
+    """nx_snappy_encode_plan: equal full-occupancy launches in steps of half a block per CU (DESIGN.md §6
+    launch table).  On a 256-CU MI355X: the 100 GiB job at N = 1/2/4/8 per rank, and the 1 M weak leg."""
+    import bench
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    full = cus * 1280  # 20 waves per CU
+    assert bench.encode_plan(full) == [full]
+    assert bench.encode_plan(100) == [100]
+    for n in (1638400, 819200, 409600, 204800, 1048576, 5 * full + 1, 3 * full - 256):
+        p = bench.encode_plan(n)
+        assert sum(p) == n and max(p) <= full
+        assert len(p) == (n + full - 1) // full
+        assert max(p) - min(p) <= cus * 128 + cus * 128  # equal up to one step (+ the last launch's rest)
+    if cus == 256:
+        assert bench.encode_plan(1638400) == [327680] * 5
+        assert bench.encode_plan(819200) == [294912, 262144, 262144]
+        assert bench.encode_plan(409600) == [196608, 212992]
+        assert bench.encode_plan(204800) == [204800]
+        assert bench.encode_plan(1048576) == [262144] * 4
 
 
 def test_run_rank_world1_small_job(dev):

@@ -180,3 +180,28 @@ def test_lz4hc_repeated_launches_reuse_tables(dev, B, oracle):
         torch.cuda.synchronize()
         outh, oo, ol = out.cpu().numpy().tobytes(), ooff.cpu().tolist(), olen.cpu().tolist()
         assert [outh[o:o + n] for o, n in zip(oo, ol)] == want, r
+
+
+def test_lz4hc_table_reset_after_many_blocks_per_wave(dev, B, oracle):
+    """a wave's HC tables are zeroed once its blocks' index bases would pass 2^32 (~125 blocks
+    per wave, kHcMaxStamp); one call of 130 blocks per wave crosses that reset (a second launch after a
+    memset) and every block still equals the oracle.  The workspace stays at the one-block-per-wave
+    bound (CUs x 2 tables of 256 KiB)."""
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    waves = cus * 2
+    n = waves * 130
+    rng = random.Random(99)
+    pool = [oracle.textgen_chunk(700 + k, 40 + 13 * k) for k in range(31)] + [b"ab" * (20 + k) for k in range(7)] + \
+           [bytes(rng.getrandbits(8) for _ in range(60 + k)) for k in range(5)]
+    data = [pool[(i * 7) % len(pool)] for i in range(n)]
+    inp, off, ln = B.pack(data, dev)
+    out, ooff = B.out_slots([B.lz4_max_compressed_length(len(d)) for d in data], dev)
+    olen, st = B.lz4_encode(inp, off, ln, out, ooff, high=True)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    want = [oracle.lz4hc_compress(p) for p in pool]
+    outh, oo, ol = out.cpu().numpy().tobytes(), ooff.cpu().tolist(), olen.cpu().tolist()
+    for i in range(n):
+        assert outh[oo[i]:oo[i] + ol[i]] == want[(i * 7) % len(pool)], i
+    hb, _ = B.workspace_info(B.WS_LZ4HC_ENC)
+    assert 0 < hb <= waves * 256 * 1024

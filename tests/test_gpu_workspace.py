@@ -216,3 +216,42 @@ def test_trim_after_batchers_and_handles_are_freed(nx, B, oracle):
         B.workspaces_trim()
         _, owners = B.workspace_info(B.WS_DEC_RECORDS)
         assert owners == 0
+
+
+def test_encoder_reserve_under_a_byte_cap(nx, B, oracle):
+    """VERDICT r5 item 5 (the reference decodes under an allocator memory limit,
+    AbstractIntegrationTest.java:193-255): nx_snappy_encoder_reserve_ex caps the Snappy table workspace;
+    a standalone batch larger than the cap runs on the capped lanes in more launches, never grows it,
+    and its bytes equal the oracle's; the placement held at most the default peak (half the device)."""
+    _collect(B)
+    _, owners = B.workspace_info(B.WS_SNAPPY_ENC)
+    if owners:
+        pytest.skip("a live handle of another test holds the workspace")
+    B.workspace_placement_config(0, 0)  # the defaults (bench.py lifts them in its own process)
+    lanes = 20480  # above the one-chunk-per-wave form: dense launches of at most 20 480 chunks
+    cap = lanes * 128 * 1024 + 12345
+    got_bytes, peak = B.snappy_encoder_reserve(70000, cap)
+    assert got_bytes == lanes * 128 * 1024
+    total = torch.cuda.mem_get_info()[1]
+    assert got_bytes <= peak <= total // 2
+    dev = torch.device("cuda:0")
+    n = 50000
+    chunks = [oracle.textgen_chunk(5000 + (i % 97), 300 + (i % 97) * 37) for i in range(n)]
+    inp, off, ln = B.pack(chunks, dev, align=1)
+    out, ooff = B.out_slots([B.snappy_max_compressed_length(len(c)) for c in chunks], dev)
+    olen, st = B.snappy_encode(inp, off, ln, out, ooff)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    assert B.workspace_info(B.WS_SNAPPY_ENC)[0] == got_bytes  # not grown past the cap
+    outh, oo, ol = out.cpu().numpy().tobytes(), ooff.cpu().tolist(), olen.cpu().tolist()
+    want = {}
+    for i in list(range(0, n, 211)) + list(range(n - 300, n)):
+        k = i % 97
+        if k not in want:
+            want[k] = oracle.snappy_encode(chunks[i])
+        assert outh[oo[i]:oo[i] + ol[i]] == want[k], i
+    # a reserve above the cap is refused while the capped workspace lives; trim lifts the cap
+    from netty_amd import _lib
+    assert _lib.load().nx_snappy_encoder_reserve_ex(70000, cap // 2, None, None, None) != 0
+    B.workspaces_trim()
+    assert B.workspace_info(B.WS_SNAPPY_ENC) == (0, 0)
