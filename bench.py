@@ -248,6 +248,47 @@ def config4_cpu(O, seconds: float):
     z4 = [O.lz4_compress(s) for s in sample]
     res["lz4"] = {"encode_gib_s": rate(O.lz4_compress, sample),
                   "decode_gib_s": rate(lambda e: O.lz4_decompress(e[0], e[1]), [(e, len(s)) for e, s in zip(z4, sample)])}
+    # LZ4 HC (Lz4FrameEncoder(highCompressor = true): LZ4_compress_HC level 9), single thread and on every
+    # host core (the beside-rate the GPU's alt_codecs.lz4_hc leg is compared with)
+    from concurrent.futures import ThreadPoolExecutor
+    threads = host_cores()
+
+    def hc_worker(deadline):
+        done = 0
+        while time.perf_counter() < deadline:
+            for x in sample:
+                O.lz4hc_compress(x)
+            done += 1
+        return done
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL inside the C call
+        reps = sum(ex.map(hc_worker, [t0 + 2 * per] * threads))
+    t1 = time.perf_counter()
+    res["lz4_hc"] = {"encode_gib_s": rate(O.lz4hc_compress, sample),
+                     "encode_gib_s_all_cores": round(reps * U / (t1 - t0) / 2**30, 4), "cores": threads,
+                     "note": "oracle/netty_oracle.c orc_lz4hc_compress (liblz4 level 9 restated, pinned byte-equal to liblz4)"}
+    try:  # the library lz4-java's highCompressor() wraps: liblz4 level 9 (pyarrow's bundled copy), same sample
+        import pyarrow as pa
+        z = pa.Codec("lz4_raw", compression_level=9)
+
+        def lib_worker(deadline):
+            done = 0
+            while time.perf_counter() < deadline:
+                for x in sample:
+                    z.compress(x)
+                done += 1
+            return done
+
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            reps = sum(ex.map(lib_worker, [t0 + 2 * per] * threads))
+        t1 = time.perf_counter()
+        res["lz4_hc"]["liblz4_level9"] = {"encode_gib_s": rate(lambda x: z.compress(x), sample),
+                                          "encode_gib_s_all_cores": round(reps * U / (t1 - t0) / 2**30, 4),
+                                          "library": "liblz4 1.10.0 in pyarrow " + pa.__version__}
+    except ImportError:
+        pass
     return res
 
 
@@ -298,6 +339,58 @@ def load_traffic():
         if d.get("source_digest") == want:
             return {k: v["hbm_bytes_per_chunk"] for k, v in d["kernels"].items()}, os.path.relpath(f, ROOT)
     return None, f"no PMC summary for kernel sources {want} (run scripts/pmc_traffic.sh)"
+
+
+def load_issue():
+    """Per-kernel issue counters (scripts/pmc_issue.sh: instruction mix per chunk, VALU busy, wave-state
+    split) from the newest committed pmc_issue.json taken on these kernel sources, else (None, reason)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "**", "pmc_issue.json"), recursive=True), key=os.path.getmtime)
+    want = source_digest()
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("source_digest") == want:
+            return d["kernels"], os.path.relpath(f, ROOT)
+    return None, f"no issue-counter summary for kernel sources {want} (run scripts/pmc_issue.sh)"
+
+
+CLOCK_GHZ = 2.4  # MI355X max engine clock (MI355X_MICROARCH.md): the issue capacity's upper bound
+
+
+def issue_ceiling(issue, kernels, frames_per_launch: int, ms_per_launch: float, simds: int):
+    """roofline_decode.issue: the decoder's instruction stream against the chip's
+    issue capacity.  Per frame: wave-instructions by type summed over the kernels (PMC); live: VALU
+    busy = 2 cycles per wave64 VALU instruction x instructions per launch / (SIMDs x 2.4 GHz x the
+    launch's HIP-event time), a lower bound on the busy fraction (the chip runs below 2.4 GHz under load);
+    per kernel: VALU busy and the wave-state split measured in the profiled run itself."""
+    ks, src = issue
+    if not ks:
+        return {"source": src}
+    per = {}
+    rows = {}
+    for name, v in ks.items():
+        base = name.split("<")[0]
+        if not any(base == k.split("<")[0] for k in kernels):
+            continue
+        for t, x in v["insts_per_chunk"].items():
+            per[t] = per.get(t, 0.0) + x
+        rows[base] = {"valu_busy_profiled": round(v["valu_busy"], 4) if v.get("valu_busy") is not None else None,
+                      "insts_per_simd_cycle_profiled": round(v["insts_per_simd_cycle"], 4) if v.get("insts_per_simd_cycle") else None,
+                      "wave_split": {k: round(x, 4) for k, x in v.get("wave_split", {}).items()},
+                      "insts_per_frame": {t: round(x) for t, x in v["insts_per_chunk"].items()}}
+    if not per:
+        return {"source": src}
+    valu_cycles = 2.0 * per.get("VALU", 0.0) * frames_per_launch
+    cap = simds * CLOCK_GHZ * 1e9 * (ms_per_launch / 1e3)
+    return {"bound": "issue", "unit": "wave-instructions per frame", "insts_per_frame": {t: round(x) for t, x in per.items()},
+            "valu_salu_lds_per_frame": round(per.get("VALU", 0) + per.get("SALU", 0) + per.get("LDS", 0)),
+            "frames_per_launch": frames_per_launch, "ms_per_launch": round(ms_per_launch, 3),
+            "valu_busy_live": round(valu_cycles / cap, 4) if cap else None,
+            "all_insts_per_simd_cycle_live": round(sum(per.values()) * frames_per_launch / cap, 4) if cap else None,
+            "clock_ghz_assumed": CLOCK_GHZ, "simds": simds, "kernels": rows, "source": src}
 
 
 # ---------------------------------------------------------------------------------------- the GPU leg
@@ -654,6 +747,14 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
     traffic = load_traffic() if gpu else (None, "cpu test leg")
     r_dec = roofline(C_ + U, t_dec, n, DEC_KERNELS, traffic, copy_gbs)  # decode: C_in + U_out per chunk
     r_enc = roofline(U + C_, t_enc, n, ENC_KERNELS, traffic, copy_gbs)  # encode: U_in + C_out per chunk
+    if gpu and t_dec:
+        simds = torch.cuda.get_device_properties(dev).multi_processor_count * 4
+        # the decode calls' frames per launch: DEC_SUB; their time per frame from this run's events
+        fpl = min(getattr(leg, "dec_sub", n), n)
+        r_dec["issue"] = issue_ceiling(load_issue(), DEC_KERNELS, fpl, t_dec * fpl / n, simds)
+        if t_enc:
+            fpe = max(leg.enc_sizes) if hasattr(leg, "enc_sizes") else n
+            r_enc["issue"] = issue_ceiling(load_issue(), ENC_KERNELS, fpe, t_enc * fpe / n, simds)
     def fill_random_access():
         ceil = probe_ceiling(torch, dev) or {}
         got = ENC_PROBES_PER_CHUNK * n / (t_enc / 1e3)
@@ -705,6 +806,9 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
     }
     ok = S.all_true(ok, device=cdev)
     line["verified"] = ok
+    if rank == 0:  # progress on stderr (the JSON line comes at the end, after the extra legs)
+        print(f"[bench] strong leg: {line['value']} GiB/s, {line['ms_per_step']} ms/step, kernel ms/step "
+              f"{line['kernel_ms_per_step']}, verified {ok}", file=sys.stderr, flush=True)
     if gpu and rank == 0:
         line["device"] = device_info(torch, dev)
     if gpu and args.weak_chunks > 0:
@@ -724,6 +828,7 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
         ok = ok and wok
         line["verified"] = ok
         leg = wk
+        del wk  # `leg` is the only reference: `del leg` below frees the weak leg's buffers
     if gpu and rank == 0 and world == 1:
         from netty_amd import batch as B
         # a strided sample of the first sub-batch's GPU outputs (compressed bytes, masked CRCs), taken to
@@ -762,6 +867,15 @@ def run_rank(args, rank: int, world: int, local: int, backend: str = "nccl", leg
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, gpu_sample)
             ok = ok and line["cpu_baseline"].get("gpu_parity_sample", {}).get("verified", True)
+            hc_gpu = line.get("alt_codecs", {}).get("lz4_hc", {}).get("encode_gib_s")
+            hc_cpu = line["cpu_baseline"].get("config4_per_codec", {}).get("lz4_hc", {})
+            if hc_gpu and hc_cpu:
+                # highCompressor = true: below the host's own liblz4 on all cores, it stays on the JVM
+                # (DESIGN.md §5); the ratio makes that visible in every line
+                lib = hc_cpu.get("liblz4_level9", {}).get("encode_gib_s_all_cores")
+                hc_cpu["gpu_over_oracle_all_cores"] = round(hc_gpu / hc_cpu["encode_gib_s_all_cores"], 3)
+                if lib:
+                    hc_cpu["gpu_over_liblz4_all_cores"] = round(hc_gpu / lib, 3)
         line["verified"] = ok
     if rank == 0:
         emit(json.dumps(line))

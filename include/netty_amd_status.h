@@ -72,6 +72,10 @@
  * buffer size (%d bytes) exceeds the maximum allowable size (%d bytes)" when the blocks of the pending
  * bytes need more than maxEncodeSize (nx_lz4_frame_encoder_error has the message). */
 #define NX_ERR_LZ4_ENCODE_SIZE            (-58)
+/* Lz4FrameEncoder.encode after close() (Lz4FrameEncoder.java:233-239): IllegalStateException "encode
+ * finished and not enough space to write remaining data" when allocateBuffer(allowEmptyReturn) returned
+ * EMPTY_BUFFER, i.e. the message's blocks need fewer than blockSize bytes (:216-218). */
+#define NX_ERR_LZ4_ENCODE_FINISHED        (-59)
 
 /* Device frame scan (nx_snappy_frame_scan_batch), one code per SnappyFrameDecoder throw site: */
 /* :116-118  "Unexpected length of stream identifier: %d" */

@@ -15,6 +15,7 @@ from .handlers import (  # noqa: F401
     EncoderException,
     FastLzFrameDecoder,
     FastLzFrameEncoder,
+    IllegalStateException,
     Lz4FrameDecoder,
     Lz4FrameEncoder,
     LzfDecoder,

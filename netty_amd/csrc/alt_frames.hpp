@@ -336,7 +336,8 @@ struct nx_lz4_frame_encoder {
 };
 
 // allocateBuffer's maxEncodeSize check (handlers.cpp; the batcher's submit runs it too)
-int32_t nx_lz4_frame_encoder_check_size(nx_lz4_frame_encoder* e, uint64_t remaining);
+int32_t nx_lz4_frame_encoder_check_size(nx_lz4_frame_encoder* e, uint64_t remaining, int32_t* target_out = nullptr);
+int32_t nx_lz4_frame_encoder_check_finished(nx_lz4_frame_encoder* e, size_t n, int32_t target);
 
 struct nx_alt_decoder_base {
     nx::h::Gpu g;

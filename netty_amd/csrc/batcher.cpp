@@ -1033,8 +1033,12 @@ int32_t launch_inner(nx_batcher* b, Batch* bt) {
     // preambles), into a device mirror that one DMA copy then moves.  The copy engine does not hold
     // CUs or flood the memory system with partial writes while the next batch parses (round 4 e2e:
     // the finish kernel's host writes ran at 53 GB/s and slowed a concurrent k_parse 2-3x).
+    // The spill area is reserved for rare malformed chunks: it counts neither as expected bytes nor
+    // against them (counted in out_used it leaned mid-sized flushes away from the DMA path).
     const uint64_t est = bt->est_out + 8ull * nej + sizeof(DecRes) * nda + sizeof(nx::bt::AltRes) * (naj ? bt->apc.size() : 0);
-    const bool dma_out = bt->out_used >= nx::bt::kDmaOutMin && est * 5 >= bt->out_used * 4;
+    const uint64_t spill_res = ndc ? spill_cap : 0;
+    const uint64_t used_wo_spill = bt->out_used > spill_res ? bt->out_used - spill_res : 0;
+    const bool dma_out = bt->out_used >= nx::bt::kDmaOutMin && est * 5 >= used_wo_spill * 4;
     nx::h::DevBuf& mirror = b->dmirror[b->flushes % kStreams];
     if (dma_out && !mirror.ensure(bt->out_used)) return NX_ERR_HIP;
     uint8_t* const ob = dma_out ? mirror.as<uint8_t>() : bt->out.d;
@@ -1979,7 +1983,9 @@ extern "C" int64_t nx_lz4_frame_encoder_submit(nx_lz4_frame_encoder* e, nx_batch
     // plus the buffered bytes; a bare flush (op 1, no bytes) sizes the buffer (:296-304); finishEncode
     // checks nothing (:306-315).  Nothing is queued or buffered when it fails.
     if (n > 0 || op == 0 || (op == 1 && !e->buf.empty())) {
-        const int32_t r = nx_lz4_frame_encoder_check_size(e, (uint64_t)n + e->buf.size());
+        int32_t target = 0;
+        int32_t r = nx_lz4_frame_encoder_check_size(e, (uint64_t)n + e->buf.size(), &target);
+        if (r == NX_OK) r = nx_lz4_frame_encoder_check_finished(e, n, target);  // IllegalStateException after close
         if (r != NX_OK) return r;
     }
     std::lock_guard<std::mutex> lk(b->mu);

@@ -15,6 +15,7 @@ extern "C" const char* nx_status_string(int32_t s) {
         case NX_ERR_LZ4_CHECKSUM_MISMATCH: return "stream corrupted: mismatching checksum";
         case NX_ERR_LZ4_END_CHECKSUM: return "stream corrupted: checksum error";
         case NX_ERR_LZ4_ENCODE_SIZE: return "requested encode buffer size exceeds the maximum allowable size";
+        case NX_ERR_LZ4_ENCODE_FINISHED: return "encode finished and not enough space to write remaining data";
         case NX_ERR_SNAPPY_PREAMBLE_TOO_LONG: return "Preamble is greater than 4 bytes";
         case NX_ERR_SNAPPY_OFFSET_ZERO: return "Offset is less than minimum permissible value";
         case NX_ERR_SNAPPY_OFFSET_NEGATIVE: return "Offset is greater than maximum value supported by this implementation";

@@ -853,7 +853,8 @@ int64_t lz4_flush_blocks(nx_lz4_frame_encoder* e, const uint8_t* src, size_t n, 
 // allocateBuffer's size check (:190-214): the blocks of `remaining` pending bytes, each
 // maxCompressedLength(curSize) + HEADER_LENGTH, against maxEncodeSize (Java int arithmetic: a sum
 // that overflows is negative and fails too).  Returns NX_OK or NX_ERR_LZ4_ENCODE_SIZE with the message.
-int32_t nx_lz4_frame_encoder_check_size(nx_lz4_frame_encoder* e, uint64_t remaining) {
+int32_t nx_lz4_frame_encoder_check_size(nx_lz4_frame_encoder* e, uint64_t remaining, int32_t* target_out) {
+    if (target_out) *target_out = 0;
     if (remaining > 0x7FFFFFFFull) {  // int remaining < 0 (:195-197)
         e->err = "too much data to allocate a buffer for compression";
         return NX_ERR_LZ4_ENCODE_SIZE;
@@ -872,7 +873,17 @@ int32_t nx_lz4_frame_encoder_check_size(nx_lz4_frame_encoder* e, uint64_t remain
         e->err = buf;
         return NX_ERR_LZ4_ENCODE_SIZE;
     }
+    if (target_out) *target_out = t32;
     return NX_OK;
+}
+
+// encode() after close() (:233-239): write()'s allocateBuffer(allowEmptyReturn = true) hands encode an
+// EMPTY_BUFFER when the message's blocks need fewer than blockSize bytes (:216-218), and encode then
+// throws; a larger message gets a buffer of its size and passes through.
+int32_t nx_lz4_frame_encoder_check_finished(nx_lz4_frame_encoder* e, size_t n, int32_t target) {
+    if (!e->finished || n == 0 || target >= (int32_t)e->block_size) return NX_OK;
+    e->err = "encode finished and not enough space to write remaining data";
+    return NX_ERR_LZ4_ENCODE_FINISHED;
 }
 
 extern "C" int64_t nx_lz4_frame_encoder_encode(nx_lz4_frame_encoder* e, const uint8_t* in, size_t n, uint8_t* out,
@@ -880,10 +891,12 @@ extern "C" int64_t nx_lz4_frame_encoder_encode(nx_lz4_frame_encoder* e, const ui
     const nx::NoGrowScope no_grow;
     if (!e || (!in && n)) return NX_ERR_INVALID_ARG;
     {   // MessageToByteEncoder.write: allocateBuffer before encode (:190-214), also after close()
-        const int32_t r = nx_lz4_frame_encoder_check_size(e, (uint64_t)n + e->buf.size());
+        int32_t target = 0;
+        int32_t r = nx_lz4_frame_encoder_check_size(e, (uint64_t)n + e->buf.size(), &target);
+        if (r == NX_OK) r = nx_lz4_frame_encoder_check_finished(e, n, target);
         if (r != NX_OK) return r;
     }
-    if (e->finished) {  // :233-239 — after close() the bytes pass through
+    if (e->finished) {  // :233-239 — after close() a message of at least a block's buffer passes through
         if (out_cap < n) return NX_ERR_INVALID_ARG;
         if (n) memcpy(out, in, n);
         return (int64_t)n;

@@ -37,6 +37,10 @@ class DecompressionException(DecoderException):
     """DecompressionException.java:23"""
 
 
+class IllegalStateException(Exception):
+    """java.lang.IllegalStateException (Lz4FrameEncoder.encode after close, Lz4FrameEncoder.java:233-239)"""
+
+
 class CompressionException(EncoderException):
     """CompressionException.java:23"""
 
@@ -262,9 +266,16 @@ class Lz4FrameEncoder(_Encoder):
         cap = _lib.load().nx_lz4_frame_max_encoded_length(n, self.block_size)
         return (C.c_uint8 * cap)(), cap
 
-    def _ret(self, r, out) -> bytes:
-        if r == -58:  # NX_ERR_LZ4_ENCODE_SIZE: allocateBuffer's EncoderException
+    def raise_for(self, r):
+        """the reference's exception for a handle status: NX_ERR_LZ4_ENCODE_SIZE (-58) is allocateBuffer's
+        EncoderException, NX_ERR_LZ4_ENCODE_FINISHED (-59) encode's IllegalStateException after close"""
+        if r == -58:
             raise EncoderException(_lib.load().nx_lz4_frame_encoder_error(self._h).decode())
+        if r == -59:
+            raise IllegalStateException(_lib.load().nx_lz4_frame_encoder_error(self._h).decode())
+
+    def _ret(self, r, out) -> bytes:
+        self.raise_for(r)
         if r < 0:
             raise CompressionException(_lib.status_string(r))
         return bytes(out[:r])
@@ -384,7 +395,9 @@ class Batcher:
             return self._ticket(L.nx_lzf_encoder_submit(encoder._h, self._h, buf, len(buf)), "nx_lzf_encoder_submit")
         if isinstance(encoder, Lz4FrameEncoder):
             buf = bytes(data)
-            return self._ticket(L.nx_lz4_frame_encoder_submit(encoder._h, self._h, buf, len(buf), op), "nx_lz4_frame_encoder_submit")
+            t = L.nx_lz4_frame_encoder_submit(encoder._h, self._h, buf, len(buf), op)
+            encoder.raise_for(t)
+            return self._ticket(t, "nx_lz4_frame_encoder_submit")
         if registered_ptr is not None:
             t = L.nx_snappy_frame_encoder_submit(encoder._h, self._h, C.c_void_p(registered_ptr), len(data), 1)
         else:

@@ -1282,10 +1282,18 @@ static void hc_sequence(const uint8_t** ip, uint8_t** op, const uint8_t** anchor
     *anchor = *ip;
 }
 
+static int32_t lz4hc_compress_ctx(hc_ctx* c, const uint8_t* in, int32_t n, uint8_t* out);
+/* One zeroed LZ4_streamHC_t per call (LZ4_compress_HC's fresh state), on the heap so that calls on
+ * several host threads (bench.py's cpu_baseline) do not share it. */
 int32_t orc_lz4hc_compress(const uint8_t* in, int32_t n, uint8_t* out) {
-    static hc_ctx C;
-    hc_ctx* c = &C;
-    memset(c, 0, sizeof *c);
+    hc_ctx* c = (hc_ctx*)calloc(1, sizeof(hc_ctx));
+    if (!c) return -1;
+    const int32_t r = lz4hc_compress_ctx(c, in, n, out);
+    free(c);
+    return r;
+}
+
+static int32_t lz4hc_compress_ctx(hc_ctx* c, const uint8_t* in, int32_t n, uint8_t* out) {
     c->in = in;
     c->next = HC_START;
     const uint8_t* ip = in;

@@ -1,12 +1,12 @@
 """Summarise the FETCH_SIZE / WRITE_SIZE passes of scripts/pmc_traffic.sh per kernel: HBM bytes per
-64 KiB chunk.  The passes run bench.py over --total-chunks CHUNKS with the bench's own call shapes (round
-6: one encode launch of CHUNKS = 327 680, decode calls of 262 144 + 65 536 frames).  Every pass over
-the chunks (the timed step, verify's pass and its first-call re-runs) runs one CRC32C dispatch per
-encode call, with the encode and decode of the same chunks beside it, so a kernel's bytes per chunk =
-its total bytes / (CHUNKS x CRC dispatches / encode calls per pass).  FETCH_SIZE is
-doubled as MI355X_MICROARCH.md's HBM section prescribes for gfx950 (it tallies 128-B read requests
-at 64 B); WRITE_SIZE is taken as is.  The summary records the digest of the kernel sources it was
-taken on (bench.source_digest()); bench.py uses a summary only when that digest matches.  Units: bytes."""
+64 KiB chunk.  The passes run bench.py with --total-chunks = --sub-chunks = CHUNKS (round 6: 327 680,
+one launch of the dense encoder, whose decode call the library runs as parse/expand pairs of 262 144 +
+65 536 frames), so every pass (the timed step, verify's pass and its first-call re-runs) encodes and
+decodes all CHUNKS chunks, once per dense-encoder dispatch: a kernel's bytes per chunk = its total
+bytes / (CHUNKS x encoder dispatches).  FETCH_SIZE is doubled as MI355X_MICROARCH.md's HBM section
+prescribes for gfx950 (it tallies 128-B read requests at 64 B); WRITE_SIZE is taken as is.  The
+summary records the digest of the kernel sources it was taken on (bench.source_digest()); bench.py
+uses a summary only when that digest matches.  Units: bytes."""
 import collections, csv, glob, json, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
@@ -22,14 +22,10 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
                 continue
             agg[name][r["Counter_Name"]] += float(r["Counter_Value"]) * 1024.0  # KiB -> bytes
             disp[(name, c)].add(r["Dispatch_Id"])
-calls = 1  # encode calls per pass: from the bench line the pass printed
-for line in open(f"{root}/traffic_FETCH_SIZE.log", errors="ignore"):
-    if line.startswith("{"):
-        calls = len(json.loads(line)["config"]["calls"]["encode_calls"])
-crc = [k for k in agg if k.startswith("nx::k_crc32c_masked")]
-passes = max(len(disp[(crc[0], "FETCH_SIZE")]), 1) / calls if crc else 1.0
+enc = [k for k in agg if k.startswith("nx::enc::k_snappy_encode<true, false>")]
+passes = float(max(len(disp[(enc[0], "FETCH_SIZE")]), 1)) if enc else 1.0
 out = {"source": f"rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE; bench.py --total-chunks {chunks} "
-                 f"--steps 1 --warmup 0 --weak-chunks 0 (the bench's call shapes)",
+                 f"--sub-chunks {chunks} --steps 1 --warmup 0 --weak-chunks 0 --no-latency --no-probe-ceiling",
        "source_digest": bench.source_digest(), "fetch_correction": 2.0, "chunks_per_pass": chunks, "passes": passes,
        "kernels": {}}
 for name, d in agg.items():

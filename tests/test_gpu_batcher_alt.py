@@ -93,8 +93,9 @@ def test_lz4_encoder_jobs_equal_sync(nx, oracle, block_size, high):
         msgs = _msgs(oracle, rng, rng.randint(2, 6))
         op = [rng.choice((0, 0, 0, 1)) for _ in msgs]
         op[-1] = rng.choice((1, 2))
-        if rng.random() < 0.3:  # a message after close passes through (:233-239)
-            msgs.append(b"after close")
+        if rng.random() < 0.3:  # a message after close passes through if its blocks need >= blockSize bytes (:216-239)
+            n_min = next(n for n in range(block_size + 1) if n + n // 255 + 37 >= block_size)
+            msgs.append((b"after close " * (n_min // 12 + 1))[:max(1, n_min)])
             op.append(0)
             op[-2] = 2
         it = iter(op)

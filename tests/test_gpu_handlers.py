@@ -347,7 +347,39 @@ def test_lz4_block_size_and_flush(nx, oracle):
             + oracle.lz4_frame_end(level))
     assert comp == want
     assert b"".join(nx.Lz4FrameDecoder(True).channel_read(comp)) == data
-    assert enc.encode(b"raw after close") == b"raw after close"
+
+
+@pytest.mark.parametrize("block_size", [64, 4096, 1 << 16])
+def test_lz4_encode_after_close(nx, block_size):
+    """after close(), write()'s allocateBuffer(allowEmptyReturn = true) returns EMPTY_BUFFER
+    when the message's blocks need fewer than blockSize bytes (Lz4FrameEncoder.java:216-218), and
+    encode() then throws IllegalStateException (:233-239); a message whose blocks need at least
+    blockSize bytes gets a buffer and passes through unchanged.  Both through the synchronous handle
+    and as batcher jobs, and an empty message passes either way."""
+    # smallest n with n + n / 255 + 16 + 21 >= blockSize (maxCompressedLength + HEADER_LENGTH)
+    n_min = next(n for n in range(block_size + 1) if n + n // 255 + 37 >= block_size)
+    small, big = b"s" * max(1, n_min - 1), bytes(range(256)) * (n_min // 256 + 1)
+    big = big[:max(n_min, 1)]
+    for path in ("sync", "batcher"):
+        enc = nx.Lz4FrameEncoder(block_size)
+        b = nx.Batcher() if path == "batcher" else None
+
+        def run(data, op=0):
+            if b is None:
+                return enc.encode(data) if op == 0 else enc.encode(data) + enc.finish_encode()
+            t = b.submit_encode(enc, data, op=op)
+            b.flush()
+            b.wait(t)
+            return b.result(t)[0]
+
+        run(b"x" * 10, op=2)  # closes the stream
+        if block_size > 37:
+            with pytest.raises(nx.IllegalStateException, match="encode finished and not enough space to write remaining data"):
+                run(small)
+        assert run(big) == big
+        assert run(b"") == b""
+        if b is not None:
+            b.close()
 
 
 def test_lzf_encoder_total_length_argument(nx, oracle):

@@ -425,6 +425,28 @@ def test_lz4hc_compress_equals_liblz4_level9(oracle):
         assert oracle.lz4_decompress(hc, len(data)) == (0, data), name
 
 
+# The liblz4 the LZ4 / LZ4 HC pins above ran against: pyarrow 25.0.0's libarrow carries
+# liblz4's LZ4_VERSION_STRING "1.10.0" (liblz4 exports no version call there, so it is read from the
+# library's strings).  Lz4FrameEncoder's lz4-java 1.8.0 bundles liblz4 1.9.3: the pins assume the fast
+# compressor and HC level 9 kept their output from 1.9.3 to 1.10.0 (1.10's level changes were to HC
+# levels 1-2), so parity with lz4-java's own bytes is "parity unpinned" by a 1.9.3 run.
+LZ4_PIN_LIBRARY = "liblz4 1.10.0 (pyarrow 25.0.0)"
+
+
+def test_lz4_pin_library_version_recorded():
+    pa = pytest.importorskip("pyarrow")
+    import glob
+    import os
+    import re
+    libs = glob.glob(os.path.join(os.path.dirname(pa.__file__), "libarrow.so.*"))
+    assert libs
+    blob = open(sorted(libs)[0], "rb").read()
+    versions = set(re.findall(rb"\x00(1\.(?:9|10|11)\.\d+)\x00", blob))
+    want = LZ4_PIN_LIBRARY.split()[1].encode()
+    assert want in versions, (versions, "pyarrow's bundled liblz4 changed: re-check the LZ4 pins and LZ4_PIN_LIBRARY")
+    assert pa.__version__ in LZ4_PIN_LIBRARY
+
+
 def test_snappy_blocks_decode_with_libsnappy(oracle, kat):
     """Independent decode cross-check: pyarrow's bundled libsnappy decodes every
     Netty-format block the oracle encodes (Netty's encoder output differs from libsnappy's, so this
