@@ -110,8 +110,11 @@ inline LaneGrid lane_grid(uint32_t n, int cus, unsigned waves_per_cu) {
 // relative to the chunk's output start; writes are sequential except for back-patches (token,
 // literal-run count), which land in LDS while their unit is staged and in global memory after.
 // GOut is the plain global form (small-batch forms, large LZ4 blocks).
-constexpr uint32_t kStageUnit = 128;
-constexpr uint32_t kStageStride = 132;  // bytes per lane slot: 33 dwords, lanes' dwords on distinct banks
+#ifndef NX_STAGE_UNIT  // build option for A/B runs (scripts/build_lib_variant.sh): 64 halves the LDS per block
+#define NX_STAGE_UNIT 128
+#endif
+constexpr uint32_t kStageUnit = NX_STAGE_UNIT;
+constexpr uint32_t kStageStride = kStageUnit + 4;  // bytes per lane slot: lanes' dwords on distinct banks
 struct GOut {
     uint8_t* p;
     __device__ __forceinline__ void set(int32_t pos, uint32_t v) { p[pos] = (uint8_t)v; }

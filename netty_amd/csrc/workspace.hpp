@@ -32,7 +32,16 @@ struct WsSpec {
 // SnappyEnc: 20 waves per CU (5 blocks of 256, 327 680 lanes on 256 CUs: 40 GiB of tables; round 6).
 // Lz4HcEnc: 2^15 x 8 bytes = liblz4's HC tables per lane (u32 hashTable[2^15] + u16 chainTable[2^16]),
 // 2 waves per CU, always one block per wave (kHcMaxSlots: at most cus * 2 tables, 128 MiB on 256 CUs).
-constexpr WsSpec kWsSpec[] = {{8, 14, 20}, {8, 13, 16}, {8, 13, 8}, {8, 14, 8}, {0, 0, 0}, {8, 15, 2}};
+#ifndef NX_LZ4_WPCU  // build options for A/B runs of the alt encoders' occupancy (scripts/build_lib_variant.sh)
+#define NX_LZ4_WPCU 16
+#endif
+#ifndef NX_FLZ_WPCU
+#define NX_FLZ_WPCU 8
+#endif
+#ifndef NX_LZF_WPCU
+#define NX_LZF_WPCU 8
+#endif
+constexpr WsSpec kWsSpec[] = {{8, 14, 20}, {8, 13, NX_LZ4_WPCU}, {8, 13, NX_FLZ_WPCU}, {8, 14, NX_LZF_WPCU}, {0, 0, 0}, {8, 15, 2}};
 constexpr size_t kDecSlotBytes = 16384u * 4u + 8u;  // records of one frame + its count and length
 constexpr uint32_t kDecMaxFrames = 262144;           // frames per parse/expand launch pair
 
