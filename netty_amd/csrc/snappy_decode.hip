@@ -756,7 +756,10 @@ __global__ void __launch_bounds__(kWaves * 64, 6)
 // byte of the chunk never crosses a page, blocks wholly past the end are not loaded), the wave
 // waits once, then each lane parses tags until its window runs out.  One memory latency per ~20
 // tags instead of one per tag for whichever lane happens to cross a block.
-constexpr int kParseBlock = 256;
+#ifndef NX_PARSE_BLOCK  // lanes per k_parse workgroup (build option: 128 fits a block beside three k_expand workgroups)
+#define NX_PARSE_BLOCK 256
+#endif
+constexpr int kParseBlock = NX_PARSE_BLOCK;
 constexpr int kWinDw = 17;
 // (Round 4: a register prefetch of the following window at each reload measured 1.5 % slower end to
 // end, 54.7 vs 53.9 ms per 262 144 frames on one box, and was removed.)
