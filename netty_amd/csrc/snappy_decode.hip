@@ -59,7 +59,7 @@ constexpr int kFB = 512;          // flush block (64 lanes x 8 B)
 constexpr int32_t kGuardTrip = -99;
 constexpr uint32_t kRecCap = 16384;      // records per frame slot (64 KiB)
 constexpr int32_t kNeedFused = -1000;    // internal status: the frame goes to k_decode_fused
-constexpr uint32_t kSubBatch = 262144;   // frames per parse/expand launch pair (16 GiB of record slots)
+constexpr uint32_t kSubBatch = NX_DEC_MAX_FRAMES;  // frames per parse/expand launch pair (262 144: 16 GiB of record slots)
 constexpr uint32_t kFusedMaxFrames = 32768;  // batches up to this size decode on k_decode_fused alone
 constexpr int kDecodeAuto = 0, kDecodeFused = 1, kDecodePair = 2;  // decode_batch modes
 

@@ -32,18 +32,21 @@ struct WsSpec {
 // SnappyEnc: 20 waves per CU (5 blocks of 256, 327 680 lanes on 256 CUs: 40 GiB of tables; round 6).
 // Lz4HcEnc: 2^15 x 8 bytes = liblz4's HC tables per lane (u32 hashTable[2^15] + u16 chainTable[2^16]),
 // 2 waves per CU, always one block per wave (kHcMaxSlots: at most cus * 2 tables, 128 MiB on 256 CUs).
-#ifndef NX_LZ4_WPCU  // build options for A/B runs of the alt encoders' occupancy (scripts/build_lib_variant.sh)
+#ifndef NX_LZ4_WPCU  // build options for A/B runs of the alt encoders' occupancy (scripts/build_lib_variant.sh; LZ4 at 20: level)
 #define NX_LZ4_WPCU 16
 #endif
-#ifndef NX_FLZ_WPCU
-#define NX_FLZ_WPCU 8
+#ifndef NX_FLZ_WPCU  // FastLZ: 16 waves per CU since round 6 (profiles/r06/s4: 310 vs 351-360 ms per 262 144 chunks)
+#define NX_FLZ_WPCU 16
 #endif
-#ifndef NX_LZF_WPCU
+#ifndef NX_LZF_WPCU  // LZF: 16 waves per CU measured level with 8 (profiles/r06/s4), so the smaller workspace stays
 #define NX_LZF_WPCU 8
 #endif
 constexpr WsSpec kWsSpec[] = {{8, 14, 20}, {8, 13, NX_LZ4_WPCU}, {8, 13, NX_FLZ_WPCU}, {8, 14, NX_LZF_WPCU}, {0, 0, 0}, {8, 15, 2}};
 constexpr size_t kDecSlotBytes = 16384u * 4u + 8u;  // records of one frame + its count and length
-constexpr uint32_t kDecMaxFrames = 262144;           // frames per parse/expand launch pair
+#ifndef NX_DEC_MAX_FRAMES  // build option for A/B runs (scripts/build_lib_variant.sh)
+#define NX_DEC_MAX_FRAMES 262144
+#endif
+constexpr uint32_t kDecMaxFrames = NX_DEC_MAX_FRAMES;  // frames per parse/expand launch pair
 
 struct WsUse {  // an in-flight part lease: slots [a, b), done when ev completes
     size_t a, b;
