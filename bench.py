@@ -37,10 +37,10 @@ CHUNK = 65536
 CONFIG5_CHUNKS = 1638400  # 100 GiB of 64 KiB chunks
 # kernels whose PMC traffic backs roofline.traffic; the summary must have been taken on these sources
 PMC_SOURCES = ("netty_amd/csrc/snappy_encode.hip", "netty_amd/csrc/snappy_decode.hip", "netty_amd/csrc/crc32c.hip",
-               "netty_amd/csrc/nx_common.hpp")
+               "netty_amd/csrc/nx_common.hpp", "netty_amd/csrc/workspace.hpp")  # (workspace.hpp: the launch geometry)
 # the alt-codec legs' kernels (their parses share the Snappy decoder's translation unit and expander)
 ALT_PMC_SOURCES = ("netty_amd/csrc/fastlz.hip", "netty_amd/csrc/lzf.hip", "netty_amd/csrc/lz4.hip",
-                   "netty_amd/csrc/snappy_decode.hip", "netty_amd/csrc/nx_common.hpp")
+                   "netty_amd/csrc/snappy_decode.hip", "netty_amd/csrc/nx_common.hpp", "netty_amd/csrc/workspace.hpp")
 
 
 def parse(argv=None):
