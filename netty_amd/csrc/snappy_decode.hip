@@ -781,7 +781,8 @@ struct BurstWinT {
     // are the (up to) 5 header bytes at chunk position p in the window?
     __device__ __forceinline__ bool has(uint32_t p) const {
         const uint32_t q = p + pad;
-        return q >= base && (q + 5u <= base + kBytes || base + kBytes >= end);
+        // bitwise, not short-circuit: one compare chain instead of nested exec-mask regions
+        return (q >= base) & ((q + 5u <= base + kBytes) | (base + kBytes >= end));
     }
     // (called with p inside the chunk, so end >= 1).  Every block is loaded, those wholly past the
     // end from the last block that holds a chunk byte instead (their bytes are unspecified), so the
@@ -926,6 +927,17 @@ struct RecWriterT {
         }
     }
     __device__ __forceinline__ bool put(uint32_t r) {
+        if constexpr (!DEFER) {  // the row write needs no exec region: a lane at capacity writes its own row
+            const bool ok = n < kRecCap;
+            q[n & (QR - 1u)] = r;
+            if (ok & ((n & (QR - 1u)) == QR - 1u)) {
+                v4u* d = reinterpret_cast<v4u*>(slot + ((n - (QR - 1u)) >> 2));
+#pragma unroll
+                for (uint32_t k = 0; k < kV; ++k) d[k] = row(k);
+            }
+            n += ok ? 1u : 0u;
+            return ok;
+        }
         if (n >= kRecCap) return false;
         drain();
         q[n & (QR - 1u)] = r;
@@ -979,12 +991,12 @@ template <int K, class Has, class Step>
 __device__ __forceinline__ void burst_steps(const bool& run, Has has, Step step) {
     if constexpr (K > 0) {
         for (;;) {
-            const bool act = run && has();
-            if (!__any(act) || __popcll(__ballot(run && !act)) >= K) break;
+            const bool act = run & has();
+            if (!__any(act) || __popcll(__ballot(run & !act)) >= K) break;
             if (act) step();
         }
     } else {
-        while (run && has()) step();
+        while (run & has()) step();
     }
 }
 #ifndef NX_ALT_RELOAD_K  // the FastLZ / LZF parses: the all-lanes rule measured best (round 5 s27)

@@ -715,10 +715,9 @@ extern "C" int32_t nx_snappy_encoder_reserve_ex(uint32_t max_chunks, uint64_t ma
     NX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     if (bytes) *bytes = 0;
     if (peak) *peak = 0;
-    if (max_chunks <= (uint32_t)cus) return NX_OK;  // the LDS form needs no workspace
     nx::SharedWs& W = nx::shared_ws(nx::WsKind::SnappyEnc, dev);
     uint32_t units = max_chunks;
-    if (max_bytes) {
+    if (max_bytes) {  // the cap holds for later batches even when this reservation needs no tables
         size_t lanes = (size_t)(max_bytes / kEncTableBytes);
         if (lanes > nx::kSpreadMaxChunks) lanes = lanes / 256 * 256;
         if (lanes == 0) return NX_ERR_INVALID_ARG;
@@ -727,6 +726,7 @@ extern "C" int32_t nx_snappy_encoder_reserve_ex(uint32_t max_chunks, uint64_t ma
         W.cap = lanes;
         if (units > lanes) units = (uint32_t)lanes;
     }
+    if (max_chunks <= (uint32_t)cus) return NX_OK;  // the LDS form needs no workspace
     const int32_t r = nx::ws_hold(nx::WsKind::SnappyEnc, dev, units, (hipStream_t)stream);
     if (r != NX_OK) return r;
     {
