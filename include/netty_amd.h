@@ -91,6 +91,10 @@ int32_t nx_workspace_placement_config(uint64_t peak_bytes, int32_t max_candidate
  * full-occupancy launches (1 638 400 chunks: 5 x 327 680 on 256 CUs); a caller cutting a large job
  * into calls (bench.py) makes each call one of them. */
 int32_t nx_snappy_encode_plan(uint32_t n, uint32_t* sizes, uint32_t cap, uint32_t* count);
+/* The same plan for `slots` resident lanes on `cus` CUs, host arithmetic only (no device is touched):
+ * k = ceil(n / slots) launches, equal in steps of cus x 128 chunks, the rest below one step on the last. */
+int32_t nx_snappy_encode_plan_for(uint32_t n, uint32_t slots, int32_t cus, uint32_t* sizes, uint32_t cap,
+                                  uint32_t* count);
 int32_t nx_workspaces_trim(void);
 int32_t nx_workspaces_forget_stream(void* stream);
 int32_t nx_workspace_info(int32_t kind, uint64_t* bytes, int32_t* owners);

@@ -122,6 +122,7 @@ _SIGS = {
     "nx_snappy_encoder_reserve": (i32, [u32, vp]),
     "nx_snappy_encoder_reserve_ex": (i32, [u32, u64, vp, C.POINTER(u64), C.POINTER(u64)]),
     "nx_snappy_encode_plan": (i32, [u32, C.POINTER(u32), u32, C.POINTER(u32)]),
+    "nx_snappy_encode_plan_for": (i32, [u32, u32, i32, C.POINTER(u32), u32, C.POINTER(u32)]),
     "nx_workspace_placement_config": (i32, [u64, i32]),
     "nx_snappy_encode_placement": (i32, [C.POINTER(C.c_float), i32, C.POINTER(i32), C.POINTER(i32)]),
     "nx_workspaces_trim": (i32, []),

@@ -743,6 +743,15 @@ extern "C" int32_t nx_snappy_encoder_reserve(uint32_t max_chunks, void* stream) 
     return nx_snappy_encoder_reserve_ex(max_chunks, 0, stream, nullptr, nullptr);
 }
 
+// The plan itself for a given lane count and CU count (host arithmetic only: no device is touched),
+// for callers that size their own work and for the CPU tests.  slots = resident lanes of the dense
+// form (CUs x 20 x 64 for an uncapped workspace).
+extern "C" int32_t nx_snappy_encode_plan_for(uint32_t n, uint32_t slots, int32_t cus, uint32_t* sizes, uint32_t cap, uint32_t* count) {
+    if (!count || (cap && !sizes) || slots == 0 || cus <= 0) return NX_ERR_INVALID_ARG;
+    *count = (uint32_t)enc_plan(n, slots, cus, sizes, cap);
+    return NX_OK;
+}
+
 // The launches nx_snappy_encode_batch makes for n chunks on the current device with its present
 // workspace (the one a batch of n would grow to when there is none yet): *count launches of
 // sizes[0..] chunks (at most `cap` written).  A caller that cuts a large job into encode calls uses

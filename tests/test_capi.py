@@ -74,3 +74,34 @@ def test_one_decode_path_no_environment_kernel_selection():
     assert "NX_EXPANDER" not in seen and "NX_DECODE_MODE" not in seen
     for f in ("expand_units.hpp", "expand_frame.hpp"):
         assert not os.path.exists(os.path.join(src, f))
+
+
+def _plan(n, slots=327680, cus=256):
+    import ctypes
+    from netty_amd import _lib
+    L = _lib.load()
+    sizes = (ctypes.c_uint32 * 256)()
+    cnt = ctypes.c_uint32(0)
+    assert L.nx_snappy_encode_plan_for(n, slots, cus, sizes, 256, ctypes.byref(cnt)) == 0
+    return [sizes[i] for i in range(cnt.value)]
+
+
+def test_encode_launch_plan_host_arithmetic():
+    """The Snappy encoder's launch plan (round 6), host-only: k = ceil(n / slots) launches,
+    equal in steps of half a block per CU, the rest below one step on the last, never above the slots."""
+    assert _plan(1638400) == [327680] * 5  # N = 1 of the 100 GiB job
+    assert _plan(819200) == [294912, 262144, 262144]  # N = 2
+    assert _plan(409600) == [196608, 212992]  # N = 4
+    assert _plan(204800) == [204800]  # N = 8
+    assert _plan(1048576) == [262144] * 4  # the weak 1 M field
+    assert _plan(0) == [] and _plan(1) == [1]
+    import random
+    rng = random.Random(5)
+    for _ in range(2000):
+        cus = rng.choice((64, 80, 256, 304))
+        slots = rng.choice((cus * 1280, cus * 1024, 65536, 20480, 16640, 100 * 256))
+        n = rng.randrange(1, 3_000_000)
+        p = _plan(n, slots, cus)
+        assert sum(p) == n and max(p) <= slots and len(p) == -(-n // slots), (n, slots, cus, p)
+        if len(p) > 1:  # equal launches: within one step (+ the last launch's rest), or a plain equal split
+            assert max(p) - min(p) <= 2 * cus * 128 or max(p) - min(p) <= -(-n // len(p)), (n, slots, cus, p)
