@@ -12,12 +12,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_two_ranks_one_gpu(oracle):
+@pytest.mark.parametrize("sub", ["96", "0"])  # fixed calls; the library's launch plan (round 6)
+def test_two_ranks_one_gpu(oracle, sub):
     import torch.multiprocessing as mp
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import bench
     import mp_rank
-    argv = ["--total-chunks", "301", "--sub-chunks", "96", "--steps", "1", "--warmup", "1", "--weak-chunks", "40",
+    argv = ["--total-chunks", "301", "--sub-chunks", sub, "--steps", "1", "--warmup", "1", "--weak-chunks", "40",
             "--no-cpu-baseline", "--no-e2e", "--no-alt", "--no-frame-scan", "--no-probe-ceiling"]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
