@@ -319,11 +319,62 @@ int main(int argc, char** argv) {
         }
         nx_batcher_free(b);
     }
+    // Round 6 entry points: the LZ4 frame encoder after close (IllegalStateException for a message whose
+    // blocks need fewer than blockSize bytes, pass-through for a larger one, sync and batcher), the
+    // host-side launch plan, the placement bound and a byte-capped Snappy reservation.
+    size_t r6_checks = 0;
+    {
+        nx_batcher* b = nx_batcher_new();
+        for (int path = 0; path < 2 && b; ++path) {
+            nx_lz4_frame_encoder* e = nx_lz4_frame_encoder_new_ex(4096, 0, 0x7FFFFFFF);
+            Bytes t(nx_lz4_frame_max_encoded_length(8192, 4096) + 64);
+            if (nx_lz4_frame_encoder_close(e, t.data(), t.size()) < 0) fail("r6: lz4 close");
+            const Bytes small = make_msg(&tg, 0, 100, 7), big = make_msg(&tg, 1, 5000, 8);
+            int64_t rs, rb;
+            if (path == 0) {
+                rs = nx_lz4_frame_encoder_encode(e, small.data(), small.size(), t.data(), t.size());
+                rb = nx_lz4_frame_encoder_encode(e, big.data(), big.size(), t.data(), t.size());
+                if (rb != (int64_t)big.size() || memcmp(t.data(), big.data(), big.size()) != 0) fail("r6: lz4 pass-through after close");
+            } else {
+                rs = nx_lz4_frame_encoder_submit(e, b, small.data(), small.size(), 0);
+                rb = nx_lz4_frame_encoder_submit(e, b, big.data(), big.size(), 0);
+                if (rb <= 0) fail("r6: lz4 pass-through job after close");
+                else {
+                    nx_batcher_flush(b);
+                    nx_batcher_wait(b, rb);
+                    const nx_msg* ms = nullptr;
+                    size_t nm = 0;
+                    const char* err = nullptr;
+                    if (nx_batcher_result(b, rb, &ms, &nm, &err) != NX_OK || nm != 1 || ms[0].len != big.size() ||
+                        memcmp(ms[0].data, big.data(), big.size()) != 0)
+                        fail("r6: lz4 pass-through job bytes");
+                    nx_batcher_release(b, rb);
+                }
+            }
+            const char* msg = nx_lz4_frame_encoder_error(e);
+            if (rs != NX_ERR_LZ4_ENCODE_FINISHED || !msg || strcmp(msg, "encode finished and not enough space to write remaining data") != 0)
+                fail("r6: lz4 encode after close");
+            nx_lz4_frame_encoder_free(e);
+            ++r6_checks;
+        }
+        if (b) nx_batcher_free(b);
+        uint32_t sizes[8] = {0}, cnt = 0;
+        if (nx_snappy_encode_plan_for(1638400, 327680, 256, sizes, 8, &cnt) != NX_OK || cnt != 5 || sizes[4] != 327680) fail("r6: plan");
+        if (nx_snappy_encode_plan_for(819200, 327680, 256, sizes, 2, &cnt) != NX_OK || cnt != 3) fail("r6: plan (cap)");
+        if (nx_workspace_placement_config(0, 0) != NX_OK) fail("r6: placement config");
+        if (nx_workspaces_trim() != NX_OK) fail("r6: trim");
+        uint64_t bytes = 0, peak = 0;
+        if (nx_snappy_encoder_reserve_ex(40000, 20480ull * 131072ull + 5, nullptr, &bytes, &peak) != NX_OK || bytes != 20480ull * 131072ull ||
+            peak < bytes)
+            fail("r6: capped reserve");
+        if (nx_snappy_encoder_reserve_ex(40000, 1000ull * 131072ull, nullptr, nullptr, nullptr) == NX_OK) fail("r6: cap below a live workspace");
+        r6_checks += 3;
+    }
     const int32_t trim = nx_workspaces_trim();
     if (trim != NX_OK) fail("nx_workspaces_trim");
-    printf("{\"codecs\": %zu, \"rounds\": %d, \"round_trips\": %zu, \"batch_jobs\": %zu, \"corrupt_runs\": %zu, \"failures\": %d, "
-           "\"failure_list\": \"%s\", \"verified\": %s}\n",
-           codecs.size(), rounds, round_trips, batch_jobs, corrupt_runs, g_fail, g_list.c_str(), g_fail ? "false" : "true");
+    printf("{\"codecs\": %zu, \"rounds\": %d, \"round_trips\": %zu, \"batch_jobs\": %zu, \"corrupt_runs\": %zu, \"round6_checks\": %zu, "
+           "\"failures\": %d, \"failure_list\": \"%s\", \"verified\": %s}\n",
+           codecs.size(), rounds, round_trips, batch_jobs, corrupt_runs, r6_checks, g_fail, g_list.c_str(), g_fail ? "false" : "true");
     fflush(stdout);
     return g_fail ? 1 : 0;
 }
