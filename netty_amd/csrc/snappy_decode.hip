@@ -465,10 +465,17 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
         }
         // Rounds.  Round 0 writes every piece with no producer in this pass; then a pending piece is
         // ready once none of its producers is pending (every valid piece not pending is written).
+        // Round 6 (profiles/r06/s12): from round 1 on, every valid piece whose producers are all written
+        // writes again, pending or not (its sources are final, so a piece written in an earlier round
+        // writes the same bytes), so the update needs no test of the lane's own pending bit; and the
+        // lanes that write are a lane mask in an SGPR pair selecting the write mask (inline v_cndmask)
+        // instead of a per-lane bool rebuilt from exec-masked pieces every round.  14 -> 8 VALU and
+        // 5 fewer SALU per round; k_expand 36.9 -> 35.1 ms per 262 144 frames.
         const uint32_t w = sp >> 2;
         const uint32_t ra0 = lbase + (w & lmask), ra1 = lbase + ((w + 1u) & lmask);
-        bool ready = valid && !dep;
         uint64_t pending = depm;
+        const uint64_t validm = last >= 63u ? ~0ull : ((2ull << last) - 1ull);  // the valid pieces: lanes 0..last
+        uint64_t readym = validm & ~depm;  // round 0: every valid piece without a producer in the pass
         for (int round = 0;; ++round) {
             // stage (literal) or ring (near copy): one unaligned 4-byte read, all lanes
             uint32_t lo = lds32[ra0];
@@ -481,13 +488,14 @@ __device__ bool expand_tags(FrameIO& io, uint32_t lds_base, uint32_t O, uint32_t
                 val = overlap ? ov : val;
             }
             // one masked atomic write per lane: the piece's bytes, or nothing (mask 0)
-            const uint32_t m = ready ? bmask : 0u;
+            uint32_t m;
+            asm volatile("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(m) : "v"(bmask), "s"(readym));
             asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(waddr), "v"(m), "v"((val << sh) & m) : "memory");
-            if (!pending) break;
-            if (round >= 64) return false;
-            ready = ((pending >> lane) & 1ull) != 0 && (need & pending) == 0ull;
-            pending &= ~__ballot(ready);
+            if (!pending || round >= 64) break;
+            readym = __ballot((need & pending) == 0ull) & validm;  // every producer written (a ballot of the compare itself)
+            pending &= ~readym;
         }
+        if (pending) return false;  // the round guard tripped
         if (rn) asm volatile("" : "+v"(*rn));
         // Flush at the END of the pass, its bytes final (round 3; was at the start, flush_to(ps)): the
         // flush's stores then precede the next pass's far-copy loads by a pass of work, so the wait
