@@ -53,7 +53,11 @@ namespace nx {
 namespace dec {
 
 constexpr int kWaves = 12;        // waves per workgroup (2 workgroups per CU → 24 waves/CU)
-constexpr int kRing = 4096;       // decoded-output history per wave
+#ifndef NX_RING  // decoded-output history per wave, bytes (a power of two, >= 2048: far reads stay two flushes back)
+#define NX_RING 2048  // (round 6: 4096 -> 2048 makes room for 32 k_expand waves per CU, below)
+#endif
+constexpr int kRing = NX_RING;     // decoded-output history per wave
+static_assert((kRing & (kRing - 1)) == 0 && kRing >= 2048, "ring");
 constexpr int kStage = 1024;      // compressed-input ring per wave
 constexpr int kFB = 512;          // flush block (64 lanes x 8 B)
 constexpr int32_t kGuardTrip = -99;
@@ -93,17 +97,27 @@ static_assert(2 * (kTabBytes + kWaves * sizeof(WaveLds)) <= 160 * 1024, "two wor
 //   scalar control) were bit-exact but slower, 56.7 vs 49.9: the kernel is issue-bound (PMC: each
 //   wave issues 36 % of its cycles, stalls on issue 27 %), and the longer dependency chains of
 //   128-piece passes cost more rounds than the shared control saved.
-// NX_EXPAND_STAGE=1 / NX_EXPAND_WAVES=n rebuild the alternatives for A/B runs.
+// Round 6 (`profiles/r06/s16`, three alternations on one box, ms of k_expand per 262 144 frames): more
+// waves per SIMD pay once the round loop is short.  Residency was capped at 6 per SIMD twice over: by
+// SGPRs (106 per wave: floor(800 / (112 + 16)) = 6) and by LDS (4 KiB ring per wave).  A 2 KiB ring
+// alone (more far copies, same waves) 35.69 -> 35.97; with 4-wave workgroups, 7 per CU (94 SGPRs, 28
+// waves) 35.28; 8 per CU (the launch bounds hold SGPRs to 78, the rest spilled to VGPR lanes; 32
+// waves, 8 per SIMD) **34.79**, and the FastLZ / LZ4 decoders 5-6.5 % faster.  Shipped: 2 KiB ring,
+// 4-wave workgroups, 8 per CU.
+// NX_EXPAND_STAGE=1 / NX_EXPAND_WAVES=n / NX_EXPAND_MINB=n / NX_EXPAND_NUM_SGPR=n rebuild the alternatives for A/B runs.
 #ifndef NX_EXPAND_STAGE
 #define NX_EXPAND_STAGE 0
 #endif
 constexpr bool kExpandStaged = NX_EXPAND_STAGE != 0;
 constexpr size_t kExpandWaveLds = kExpandStaged ? sizeof(WaveLds) : offsetof(WaveLds, stage);
 #ifndef NX_EXPAND_WAVES
-#define NX_EXPAND_WAVES (NX_EXPAND_STAGE ? 12 : 8)
+#define NX_EXPAND_WAVES (NX_EXPAND_STAGE ? 12 : 4)
 #endif
 constexpr int kExpandWaves = NX_EXPAND_WAVES;
-static_assert(kTabBytes + kExpandWaves * kExpandWaveLds <= 160 * 1024 / (NX_EXPAND_STAGE ? 2 : 3), "k_expand workgroups per CU");
+#ifndef NX_EXPAND_MINB  // launch bounds: workgroups per CU the register budget must allow (8 x 4 waves: 78 SGPRs)
+#define NX_EXPAND_MINB (NX_EXPAND_STAGE ? 3 : 8)
+#endif
+static_assert(kTabBytes + kExpandWaves * kExpandWaveLds <= 160 * 1024 / NX_EXPAND_MINB, "k_expand workgroups per CU");
 
 typedef uint32_t __attribute__((aligned(1))) u32u;
 typedef __attribute__((address_space(1))) const uint8_t gu8;
@@ -1134,7 +1148,12 @@ __global__ void __launch_bounds__(kParseBlock) k_parse(const uint8_t* __restrict
 // =====================================================================================
 // k_expand: one wave per frame executes the frame's records
 // =====================================================================================
-__global__ void __launch_bounds__(kExpandWaves * 64, kExpandStaged ? 6 : 3)
+#ifdef NX_EXPAND_NUM_SGPR  // an explicit SGPR budget (residency: floor(800 / (ceil(sgprs / 16) * 16 + 16)) waves per SIMD)
+#define NX_EXPAND_SGPR_ATTR __attribute__((amdgpu_num_sgpr(NX_EXPAND_NUM_SGPR)))
+#else
+#define NX_EXPAND_SGPR_ATTR
+#endif
+__global__ void __launch_bounds__(kExpandWaves * 64, NX_EXPAND_MINB) NX_EXPAND_SGPR_ATTR
     k_expand(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,
              uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ rec,
              const uint32_t* __restrict__ nrec, uint32_t* __restrict__ out_len, int32_t* __restrict__ status,

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round 6 session 16: k_expand occupancy.  Its waves per SIMD are capped at 6 by SGPRs (106 per wave:
+# floor(800 / (112 + 16)) = 6) and by LDS (4 KiB output ring per wave).  dbase = the product (ring 4 KiB,
+# 8-wave workgroups, 3 per CU, 24 waves); r2k = ring 2 KiB, same shape (more far copies, same waves);
+# w4b7 = ring 2 KiB, 4-wave workgroups, 7 per CU (94 SGPRs: 28 waves); w4b8 = the same at 8 per CU
+# (78 SGPRs with spills to VGPR lanes: 32 waves).  Decoder GPU tests on the three variants, then the four
+# libraries alternated three times (kernel trace + alt decoders).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+ROOT=$(pwd)
+O=gpurun_out/r6s16
+mkdir -p $O
+export TMPDIR=/tmp
+fatal() { case $1 in 124|134|137|139) echo "fatal rc $1 in $2" >> $O/steps.log; cp $O/../lib_product_backup16.so netty_amd/libnetty_amd.so; exit $1;; esac; }
+cp netty_amd/libnetty_amd.so $O/../lib_product_backup16.so
+T="tests/test_gpu_snappy.py tests/test_gpu_decode_fuzz.py tests/test_gpu_lz4.py tests/test_gpu_fastlz_lzf.py tests/test_gpu_frame_fuzz.py tests/test_gpu_frame_scan.py"
+for v in r2k w4b7 w4b8; do
+  cp netty_amd/build_variants/libnetty_amd_$v.so netty_amd/libnetty_amd.so || exit 1
+  timeout -k 10 400 python -u -m pytest $T -x -q -m gpu --timeout 120 --timeout-method thread > $O/pytest_$v.log 2>&1; rc=$?
+  echo "pytest.$v $rc" >> $O/steps.log; fatal $rc pytest$v
+  [ $rc -ne 0 ] && { cp $O/../lib_product_backup16.so netty_amd/libnetty_amd.so; exit $rc; }
+done
+for r in 1 2 3; do
+  for v in dbase r2k w4b7 w4b8; do
+    cp netty_amd/build_variants/libnetty_amd_$v.so netty_amd/libnetty_amd.so || exit 1
+    (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$O/kt_${v}_$r" -o k -- \
+        python3 "$ROOT/scripts/dec_curve.py" 4 262144 > "$ROOT/$O/dec_${v}_$r.log" 2>&1); rc=$?; echo "$v.$r $rc" >> $O/steps.log; fatal $rc $v
+    f=$(find $O/kt_${v}_$r -name "*kernel_trace.csv" | head -n 1); [ -n "$f" ] && python3 scripts/trace_list.py "$f" k_parse k_expand > $O/trace_${v}_$r.txt
+    rm -rf $O/kt_${v}_$r
+    echo -n "$v " >> $O/alt_dec.log
+    timeout -k 10 240 python scripts/alt_dec_time.py 262144 3 >> $O/alt_dec.log 2>&1; rc=$?; echo "alt.$v.$r $rc" >> $O/steps.log; fatal $rc alt$v
+  done
+done
+cp $O/../lib_product_backup16.so netty_amd/libnetty_amd.so
+exit 0
